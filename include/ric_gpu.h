@@ -1,0 +1,126 @@
+/* ric_gpu.h -- C-ABI of the MI355X-native rududu .ric encode/decode path.
+ *
+ * Drop-in boundary for the reference's src/lib codec API (the reference has no
+ * C binding; these entry points are what an FFI over its C++ classes would
+ * bind).  Each function names the reference interface it replaces
+ * (paths relative to the reference repository root).  Plain pointers and
+ * sizes only; every call returns RIC_OK (0) or a negative RIC_E_* status.
+ *
+ * Objects:
+ *   ric_wavelet -- CWavelet2D (src/lib/wavelet2d.h:27-88): the band pyramid,
+ *                  resident in HBM of one GPU; DWT / quantiser / dequantiser /
+ *                  inverse DWT are HIP kernels.
+ *   ric_mux     -- CMuxCodec (src/lib/muxcodec.h:66-277): the serial range
+ *                  coder / raw-bit multiplexer, on the host, with an explicit
+ *                  capacity (the reference has none).
+ *   ric_codec   -- CompressImage / DecompressImage (src/ric/ric.cpp:123-251)
+ *                  as a reusable object for one image geometry.
+ */
+#ifndef RIC_GPU_H
+#define RIC_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RIC_OK          0
+#define RIC_E_ARG      -1   /* invalid argument / geometry */
+#define RIC_E_HIP      -2   /* HIP runtime error (no GPU, OOM, launch failure) */
+#define RIC_E_CAPACITY -3   /* output buffer too small */
+#define RIC_E_FORMAT   -4   /* bad .ric magic (the reference throws BAD_MAGIC = 2) */
+#define RIC_E_STREAM   -5   /* decoder ran past the end of the stream */
+
+/* transforms: enum trans, src/lib/utils.h:28 */
+#define RIC_CDF97 0
+#define RIC_CDF53 1
+#define RIC_HAAR  2
+
+typedef struct ric_wavelet ric_wavelet;
+typedef struct ric_mux ric_mux;
+typedef struct ric_codec ric_codec;
+
+/* ------------------------------------------------------------- library */
+const char* ric_version(void);
+/* number of visible HIP devices (0 when none) */
+int ric_device_count(void);
+/* last HIP error string of this thread (for diagnostics) */
+const char* ric_last_error(void);
+
+/* --------------------------------------------------------- ric_wavelet */
+/* CWavelet2D::CWavelet2D(int x, int y, int level, int level_chg, int Align)
+ * (src/lib/wavelet2d.h:29, wavelet2d.cpp:38-81).  Align is implicit. */
+int ric_wavelet_create(ric_wavelet** out, int x, int y, int level, int level_chg, int device);
+/* CWavelet2D::~CWavelet2D (src/lib/wavelet2d.cpp:64-67) */
+void ric_wavelet_destroy(ric_wavelet* w);
+/* run this object's kernels on an existing hipStream_t (NULL: own stream) */
+int ric_wavelet_set_stream(ric_wavelet* w, void* hip_stream);
+/* block until this object's queued GPU work is done */
+int ric_wavelet_sync(ric_wavelet* w);
+/* CWavelet2D::SetWeight(trans t, float baseWeight) (src/lib/wavelet2d.h:36) */
+int ric_set_weight(ric_wavelet* w, int trans, float base_weight);
+/* CWavelet2D::Transform<short>(short* pImage, int Stride, trans t)
+ * (src/lib/wavelet2d.h:33).  image_on_device: pImage is a device pointer.
+ * The caller's image is only read (the reference uses it as scratch). */
+int ric_transform(ric_wavelet* w, const int16_t* image, int stride, int trans, int image_on_device);
+/* CWavelet2D::TransformI<short>(short* pImageEnd, int Stride, trans t)
+ * (src/lib/wavelet2d.h:34).  Takes the image START (the reference takes the
+ * end pointer, src/lib/wavelet2d.cpp:960-990). */
+int ric_transform_inv(ric_wavelet* w, int16_t* image, int stride, int trans, int image_on_device);
+/* CWavelet2D::CodeBand(CMuxCodec*, int Quant, int lambda) (src/lib/wavelet2d.h:39) */
+int ric_code_band(ric_wavelet* w, ric_mux* m, int quant, int lambda);
+/* CWavelet2D::DecodeBand(CMuxCodec*) (src/lib/wavelet2d.h:38) */
+int ric_decode_band(ric_wavelet* w, ric_mux* m);
+/* CWavelet2D::TSUQi(int Quant) (src/lib/wavelet2d.h:42) */
+int ric_tsuqi(ric_wavelet* w, int quant);
+/* band pyramid introspection, canonical order: levels finest->coarsest
+ * D, H, V, then the coarsest LL.  Replaces reads of the public
+ * DBand/HBand/VBand/LBand/pLow members (src/lib/wavelet2d.h:46-51) and
+ * CBand::DimX/DimY/type/Weight/pBand (src/lib/band.h:43-59). */
+int ric_band_count(ric_wavelet* w);
+int ric_band_info(ric_wavelet* w, int index, int* dimx, int* dimy, int* is_int, float* weight);
+int ric_band_read(ric_wavelet* w, int index, int32_t* host_out);
+int ric_band_write(ric_wavelet* w, int index, const int32_t* host_in);
+
+/* ------------------------------------------------------------- ric_mux */
+/* CMuxCodec(unsigned char* pStream, unsigned short firstWord)
+ * (src/lib/muxcodec.h:102): encoder writing at most cap bytes into buf. */
+int ric_mux_create_encoder(ric_mux** out, uint8_t* buf, size_t cap, uint16_t first_word);
+/* CMuxCodec(unsigned char* pStream) (src/lib/muxcodec.h:103): decoder over
+ * len bytes of buf (the reference reads its payload from buf + 2). */
+int ric_mux_create_decoder(ric_mux** out, const uint8_t* buf, size_t len);
+/* CMuxCodec::endCoding() (src/lib/muxcodec.h:106): *len_out = end - buf. */
+int ric_mux_end(ric_mux* m, size_t* len_out);
+/* CMuxCodec::getSize() (src/lib/muxcodec.h:107) */
+size_t ric_mux_size(ric_mux* m);
+void ric_mux_destroy(ric_mux* m);
+
+/* ----------------------------------------------------------- ric_codec */
+/* One reusable encoder/decoder for w x h images with 1 (gray) or 3 (RGB)
+ * channels (src/ric/ric.cpp:123-251: 5 levels, level_chg 1, YCoCg, Quants). */
+int ric_codec_create(ric_codec** out, int w, int h, int channels, int device);
+void ric_codec_destroy(ric_codec* c);
+int ric_codec_set_stream(ric_codec* c, void* hip_stream);
+/* CompressImage: pix = channels planes of w*h bytes (R,G,B planar), on the
+ * device if pix_on_device.  Writes the whole .ric file (9-byte header +
+ * payload) to out (host), *len_out = its size. */
+int ric_codec_encode(ric_codec* c, const uint8_t* pix, int pix_on_device, int q, int trans,
+                     uint8_t* out, size_t cap, size_t* len_out);
+/* DecompressImage: decodes a whole .ric file (host bytes) of this geometry.
+ * pix_out: channels planes of w*h bytes (device if pix_on_device, may be
+ * NULL); planes_out: the int16 planes before the 8-bit clip (device if
+ * pix_on_device, may be NULL). */
+int ric_codec_decode(ric_codec* c, const uint8_t* ric, size_t len, int dither,
+                     uint8_t* pix_out, int16_t* planes_out, int pix_on_device);
+/* .ric header fields (src/ric/ric.cpp:114-121, 187-200) */
+int ric_read_header(const uint8_t* ric, size_t len, int* w, int* h, int* channels, int* q, int* trans);
+/* src/ric/ric.cpp:42-49 */
+int ric_quants(int idx);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RIC_GPU_H */

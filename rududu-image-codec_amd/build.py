@@ -1,0 +1,67 @@
+"""Build librududu_amd.so in-tree: HIP kernels with hipcc for gfx950, host
+sources with g++ against the ROCm headers.  Usage: python build.py [-j N]."""
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+OUT = os.path.join(HERE, "librududu_amd.so")
+OBJ = os.path.join(HERE, "build")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+ARCH = os.environ.get("RIC_OFFLOAD_ARCH", "gfx950")
+
+COMMON = ["-O3", "-std=c++17", "-fPIC", "-fwrapv", "-I" + os.path.join(REPO, "include"), "-I" + CSRC]
+
+
+def _sources():
+    return sorted(f for f in os.listdir(CSRC) if f.endswith((".hip", ".cpp")))
+
+
+def _headers_mtime():
+    m = 0.0
+    for d in (CSRC, os.path.join(REPO, "include")):
+        for f in os.listdir(d):
+            if f.endswith((".h", ".inc")):
+                m = max(m, os.path.getmtime(os.path.join(d, f)))
+    return m
+
+
+def _compile(src, hdr_mtime):
+    path = os.path.join(CSRC, src)
+    obj = os.path.join(OBJ, src + ".o")
+    if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(path), hdr_mtime):
+        return obj
+    if src.endswith(".hip"):
+        cmd = [os.path.join(ROCM, "bin", "hipcc"), "--offload-arch=" + ARCH] + COMMON + ["-c", path, "-o", obj]
+    else:
+        cmd = ["g++"] + COMMON + ["-Wall", "-D__HIP_PLATFORM_AMD__", "-I" + os.path.join(ROCM, "include"),
+                                  "-c", path, "-o", obj]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("compile failed: %s\n%s" % (" ".join(cmd), r.stderr))
+    return obj
+
+
+def build(jobs=8, verbose=False):
+    os.makedirs(OBJ, exist_ok=True)
+    hdr = _headers_mtime()
+    srcs = _sources()
+    with ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(lambda s: _compile(s, hdr), srcs))
+    if os.path.exists(OUT) and os.path.getmtime(OUT) >= max(os.path.getmtime(o) for o in objs):
+        return OUT
+    cmd = [os.path.join(ROCM, "bin", "hipcc"), "--offload-arch=" + ARCH, "-shared", "-fPIC"] + objs + ["-o", OUT]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("link failed: %s\n%s" % (" ".join(cmd), r.stderr))
+    if verbose:
+        print("built", OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    j = int(sys.argv[sys.argv.index("-j") + 1]) if "-j" in sys.argv else 8
+    build(j, verbose=True)

@@ -1,0 +1,640 @@
+// capi.cpp -- the C-ABI (include/ric_gpu.h): object lifetimes, HBM arenas,
+// and the orchestration of the GPU stages and the host serial coder.
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+#include <algorithm>
+
+#include "ric_gpu.h"
+#include "ric_types.h"
+#include "ric_kernels.h"
+#include "ric_image.h"
+#include "entropy.h"
+
+using namespace ric;
+
+namespace {
+
+thread_local std::string g_err;
+
+bool hip_fail(hipError_t e, const char* what)
+{
+	if (e == hipSuccess) return false;
+	g_err = std::string(what) + ": " + hipGetErrorString(e);
+	return true;
+}
+
+#define HIPCHK(x) do { if (hip_fail((x), #x)) return RIC_E_HIP; } while (0)
+
+int tr_any(bool sh, int v) { return sh ? (int)(int16_t)v : v; }
+
+// CBandCodec::makeThres + clen (src/lib/bandcodec.cpp:129-157)
+void make_thres(bool sh, int* thres, int quant, int lambda)
+{
+	static const int blen[17] = {20, 40, 55, 66, 75, 81, 85, 88, 89, 88, 85, 81, 75, 66, 55, 40, 20};
+	static const uint8_t kk[] = {0,0,0,0,0,0,0,0,0,0,0,1,1,1,1,2};
+	static const uint8_t mps[] = {1,1,2,2,2,5,5,5,5,5,5,5,5,5,5,5};
+	for (int i = 0; i < 16; i++) {
+		int clen1 = (kk[i] + 1) * 5 + mps[i];
+		int t = tr_any(sh, (quant + ((lambda * (blen[i + 1] - blen[i] + clen1) + 8) >> 4)) & 0xFFFE);
+		if (t > quant * 2) t = tr_any(sh, quant * 2);
+		if (t < (quant & 0xFFFE)) t = tr_any(sh, quant & 0xFFFE);
+		thres[i] = t;
+	}
+}
+
+}  // namespace
+
+struct ric_wavelet {
+	int device = 0;
+	Pyramid P;
+	char* d_arena = nullptr;
+	char* h_arena = nullptr;          // pinned mirror of the band arena
+	int16_t* d_img = nullptr;         // scratch for host-resident images
+	size_t img_pitch = 0;             // elements
+	hipStream_t st = nullptr;
+	bool own_stream = false;
+	bool host_valid = false;          // bands live on the host (after a decode)
+};
+
+struct ric_mux {
+	Mux m;
+	uint8_t* buf = nullptr;
+	bool encoder = true;
+};
+
+struct ric_codec {
+	int device = 0;
+	int w = 0, h = 0, channels = 1;
+	ric_wavelet* wav = nullptr;
+	int16_t* d_planes = nullptr;      // channels coding planes, pitch
+	uint8_t* d_pix = nullptr;         // staging for host pixels
+	int16_t* d_out = nullptr;         // staging for host int16 output planes
+	long pitch = 0;
+	std::vector<uint8_t> stream;      // coder buffer
+};
+
+namespace {
+
+int set_dev(int device) { return hip_fail(hipSetDevice(device), "hipSetDevice") ? RIC_E_HIP : RIC_OK; }
+
+// bands region [first band, end of the coarsest LL] in the arena
+void band_span(const Pyramid& P, size_t& lo, size_t& hi)
+{
+	lo = (size_t)-1; hi = 0;
+	for (int i = 0; i < P.nbands(); i++) {
+		const Band& B = const_cast<Pyramid&>(P).band(i);
+		lo = std::min(lo, B.off);
+		hi = std::max(hi, B.off + B.bytes());
+	}
+}
+
+int to_host(ric_wavelet* w)
+{
+	size_t lo, hi;
+	band_span(w->P, lo, hi);
+	HIPCHK(hipMemcpyAsync(w->h_arena + lo, w->d_arena + lo, hi - lo, hipMemcpyDeviceToHost, w->st));
+	HIPCHK(hipStreamSynchronize(w->st));
+	return RIC_OK;
+}
+
+int to_device(ric_wavelet* w)
+{
+	if (!w->host_valid) return RIC_OK;
+	size_t lo, hi;
+	band_span(w->P, lo, hi);
+	HIPCHK(hipMemcpyAsync(w->d_arena + lo, w->h_arena + lo, hi - lo, hipMemcpyHostToDevice, w->st));
+	// the host arena is rewritten by the next DecodeBand: wait for the copy
+	HIPCHK(hipStreamSynchronize(w->st));
+	w->host_valid = false;
+	return RIC_OK;
+}
+
+BandView view(ric_wavelet* w, const Band& B)
+{
+	BandView v;
+	v.p = w->h_arena + B.off; v.pitch = B.pitch; v.dx = B.dx; v.dy = B.dy; v.is_int = B.is_int;
+	return v;
+}
+
+int forward(ric_wavelet* w, const int16_t* dimg, long stride, int trans)
+{
+	Pyramid& P = w->P;
+	for (int l = 0; l < P.nlev; l++) {
+		const void* src;
+		long sp;
+		int vec;
+		if (l == 0) {
+			src = dimg; sp = stride;
+			vec = (stride % 4 == 0) && ((uintptr_t)dimg % 8 == 0);
+		} else {
+			const Band& LL = P.L[l - 1].b[BL];
+			src = w->d_arena + LL.off; sp = LL.pitch; vec = 1;
+		}
+		launch_fwd_level(P.L[l], src, sp, w->d_arena, trans, vec, w->st);
+	}
+	HIPCHK(hipGetLastError());
+	w->host_valid = false;
+	return RIC_OK;
+}
+
+int inverse(ric_wavelet* w, int16_t* dimg, long stride, int trans)
+{
+	Pyramid& P = w->P;
+	int rc = to_device(w);
+	if (rc) return rc;
+	for (int l = P.nlev - 1; l >= 0; l--) {
+		const Level& L = P.L[l];
+		void* out;
+		long po;
+		int out_int;
+		if (l == 0) { out = dimg; po = stride; out_int = 0; }
+		else { const Band& LL = P.L[l - 1].b[BL]; out = w->d_arena + LL.off; po = LL.pitch; out_int = LL.is_int; }
+		launch_inv_level(L, L.b[BL], w->d_arena, out, po, out_int, trans, w->st);
+	}
+	HIPCHK(hipGetLastError());
+	return RIC_OK;
+}
+
+// CWavelet2D::CodeBand, src/lib/wavelet2d.cpp:83-177
+int code_band(ric_wavelet* w, Mux& m, int quant, int lambda)
+{
+	Pyramid& P = w->P;
+	// buildTree on every level, finest first (bandcodec.cpp:239-319)
+	int qin = quant;
+	for (int l = 0; l < P.nlev; l++) {
+		const bool sh = !P.L[l].is_int;
+		qin = tr_any(sh, qin);
+		QuantParams qp;
+		for (int b = 0; b < 3; b++) {
+			const Band& B = P.L[l].b[b];
+			int lbda = (int)((float)lambda / B.weight);
+			int Q = tr_any(sh, (int16_t)(int)((float)qin / B.weight));
+			if (Q == 0) Q = 1;
+			qp.Q[b] = Q;
+			qp.iQ[b] = (1 << 16) / Q;
+			make_thres(sh, qp.thres[b], Q, lbda);
+		}
+		launch_quant_level(P, l, qp, w->d_arena, w->st);
+	}
+	// CBand::TSUQ on the coarsest LL with Thres 0.5 (band.h:65-92)
+	{
+		Band& B = P.coarsest_ll();
+		int Q = (int)((float)quant / B.weight);
+		if (Q == 0) Q = 1;
+		int iQ = (1 << 16) / Q;
+		int T0 = tr_any(!B.is_int, (int)(0.5f * (float)Q));
+		launch_quant_ll(P, Q, iQ, T0, w->d_arena, w->st);
+	}
+	HIPCHK(hipGetLastError());
+	int rc = to_host(w);
+	if (rc) return rc;
+	// serial part: LL DPCM, then coarse -> fine, V, H, D (wavelet2d.cpp:119-159)
+	pred_encode(m, view(w, P.coarsest_ll()));
+	for (int l = P.nlev - 1; l >= 0; l--) {
+		const int order[3] = {BV, BH, BD};
+		for (int k = 0; k < 3; k++) {
+			const Band& B = P.L[l].b[order[k]];
+			BandView par;
+			if (l + 1 < P.nlev) par = view(w, P.L[l + 1].b[order[k]]);
+			tree_encode(m, view(w, B), par, l == 0, l > 0);
+		}
+	}
+	w->host_valid = true;   // the bands now hold the encoder's final state
+	return RIC_OK;
+}
+
+// CWavelet2D::DecodeBand, src/lib/wavelet2d.cpp:179-222
+int decode_band(ric_wavelet* w, Mux& m)
+{
+	Pyramid& P = w->P;
+	// every band is overwritten: pred writes the LL, tree() Clear()s its band first
+	BandView ll = view(w, P.coarsest_ll());
+	pred_decode(m, ll);
+	for (int l = P.nlev - 1; l >= 0; l--) {
+		const int order[3] = {BV, BH, BD};
+		for (int k = 0; k < 3; k++) {
+			BandView par;
+			if (l + 1 < P.nlev) par = view(w, P.L[l + 1].b[order[k]]);
+			tree_decode(m, view(w, P.L[l].b[order[k]]), par, l == 0, l > 0);
+		}
+	}
+	w->host_valid = true;
+	return m.overflow() ? RIC_E_STREAM : RIC_OK;
+}
+
+// CWavelet2D::TSUQi / CBand::TSUQi (src/lib/wavelet2d.cpp:248-268, band.h:94-107)
+int tsuqi(ric_wavelet* w, int quant)
+{
+	int rc = to_device(w);
+	if (rc) return rc;
+	Pyramid& P = w->P;
+	for (int i = 0; i < P.nbands(); i++) {
+		const Band& B = P.band(i);
+		const bool sh = !B.is_int;
+		int q = tr_any(sh, quant);
+		q = tr_any(sh, (int)((float)q / B.weight));
+		if (q == 0) q = 1;
+		launch_dequant_band(B, q, w->d_arena, w->st);
+	}
+	HIPCHK(hipGetLastError());
+	return RIC_OK;
+}
+
+int ensure_img(ric_wavelet* w)
+{
+	if (w->d_img) return RIC_OK;
+	w->img_pitch = ((size_t)w->P.w + 63) / 64 * 64;
+	HIPCHK(hipMalloc(&w->d_img, w->img_pitch * w->P.h * sizeof(int16_t)));
+	return RIC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* ric_version(void) { return "rududu-image-codec_amd 0.1 (gfx950)"; }
+
+int ric_device_count(void)
+{
+	int n = 0;
+	if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+	return n;
+}
+
+const char* ric_last_error(void) { return g_err.c_str(); }
+
+int ric_wavelet_create(ric_wavelet** out, int x, int y, int level, int level_chg, int device)
+{
+	if (!out || x < 8 || y < 8 || x > 65535 || y > 65535 || level < 1) return RIC_E_ARG;
+	*out = nullptr;
+	if (set_dev(device)) return RIC_E_HIP;
+	ric_wavelet* w = new ric_wavelet;
+	w->device = device;
+	w->P.build(x, y, level, level_chg);
+	w->P.set_weight(CDF97);
+	// the memset runs on the object's own (non-blocking) stream: a null-stream
+	// memset would not be ordered before this stream's copies and kernels
+	if (hip_fail(hipMalloc(&w->d_arena, w->P.arena_bytes), "hipMalloc arena") ||
+	    hip_fail(hipHostMalloc(&w->h_arena, w->P.arena_bytes, 0), "hipHostMalloc arena") ||
+	    hip_fail(hipStreamCreateWithFlags(&w->st, hipStreamNonBlocking), "hipStreamCreate") ||
+	    hip_fail(hipMemsetAsync(w->d_arena, 0, w->P.arena_bytes, w->st), "hipMemset arena") ||
+	    hip_fail(hipStreamSynchronize(w->st), "hipStreamSynchronize")) {
+		ric_wavelet_destroy(w);
+		return RIC_E_HIP;
+	}
+	memset(w->h_arena, 0, w->P.arena_bytes);
+	w->own_stream = true;
+	*out = w;
+	return RIC_OK;
+}
+
+void ric_wavelet_destroy(ric_wavelet* w)
+{
+	if (!w) return;
+	(void)hipSetDevice(w->device);
+	if (w->st) (void)hipStreamSynchronize(w->st);
+	if (w->d_arena) (void)hipFree(w->d_arena);
+	if (w->d_img) (void)hipFree(w->d_img);
+	if (w->h_arena) (void)hipHostFree(w->h_arena);
+	if (w->own_stream && w->st) (void)hipStreamDestroy(w->st);
+	delete w;
+}
+
+int ric_wavelet_set_stream(ric_wavelet* w, void* s)
+{
+	if (!w) return RIC_E_ARG;
+	if (set_dev(w->device)) return RIC_E_HIP;
+	HIPCHK(hipStreamSynchronize(w->st));
+	if (w->own_stream) (void)hipStreamDestroy(w->st);
+	if (s) { w->st = (hipStream_t)s; w->own_stream = false; }
+	else { HIPCHK(hipStreamCreateWithFlags(&w->st, hipStreamNonBlocking)); w->own_stream = true; }
+	return RIC_OK;
+}
+
+int ric_wavelet_sync(ric_wavelet* w)
+{
+	if (!w) return RIC_E_ARG;
+	if (set_dev(w->device)) return RIC_E_HIP;
+	HIPCHK(hipStreamSynchronize(w->st));
+	return RIC_OK;
+}
+
+int ric_set_weight(ric_wavelet* w, int trans, float base_weight)
+{
+	if (!w || trans < 0 || trans > 2) return RIC_E_ARG;
+	w->P.set_weight(trans, base_weight);
+	return RIC_OK;
+}
+
+int ric_transform(ric_wavelet* w, const int16_t* image, int stride, int trans, int on_device)
+{
+	if (!w || !image || stride < w->P.w || trans < 0 || trans > 2) return RIC_E_ARG;
+	if (set_dev(w->device)) return RIC_E_HIP;
+	if (!on_device) {
+		int rc = ensure_img(w);
+		if (rc) return rc;
+		HIPCHK(hipMemcpy2DAsync(w->d_img, w->img_pitch * 2, image, (size_t)stride * 2, (size_t)w->P.w * 2,
+		                        w->P.h, hipMemcpyHostToDevice, w->st));
+		return forward(w, w->d_img, (long)w->img_pitch, trans);
+	}
+	return forward(w, image, stride, trans);
+}
+
+int ric_transform_inv(ric_wavelet* w, int16_t* image, int stride, int trans, int on_device)
+{
+	if (!w || !image || stride < w->P.w || trans < 0 || trans > 2) return RIC_E_ARG;
+	if (set_dev(w->device)) return RIC_E_HIP;
+	if (!on_device) {
+		int rc = ensure_img(w);
+		if (rc) return rc;
+		rc = inverse(w, w->d_img, (long)w->img_pitch, trans);
+		if (rc) return rc;
+		HIPCHK(hipMemcpy2DAsync(image, (size_t)stride * 2, w->d_img, w->img_pitch * 2, (size_t)w->P.w * 2,
+		                        w->P.h, hipMemcpyDeviceToHost, w->st));
+		HIPCHK(hipStreamSynchronize(w->st));
+		return RIC_OK;
+	}
+	return inverse(w, image, stride, trans);
+}
+
+int ric_code_band(ric_wavelet* w, ric_mux* m, int quant, int lambda)
+{
+	if (!w || !m || !m->encoder) return RIC_E_ARG;
+	if (set_dev(w->device)) return RIC_E_HIP;
+	int rc = code_band(w, m->m, quant, lambda);
+	if (rc) return rc;
+	return m->m.overflow() ? RIC_E_CAPACITY : RIC_OK;
+}
+
+int ric_decode_band(ric_wavelet* w, ric_mux* m)
+{
+	if (!w || !m || m->encoder) return RIC_E_ARG;
+	if (set_dev(w->device)) return RIC_E_HIP;
+	return decode_band(w, m->m);
+}
+
+int ric_tsuqi(ric_wavelet* w, int quant)
+{
+	if (!w) return RIC_E_ARG;
+	if (set_dev(w->device)) return RIC_E_HIP;
+	return tsuqi(w, quant);
+}
+
+int ric_band_count(ric_wavelet* w) { return w ? w->P.nbands() : RIC_E_ARG; }
+
+int ric_band_info(ric_wavelet* w, int index, int* dimx, int* dimy, int* is_int, float* weight)
+{
+	if (!w || index < 0 || index >= w->P.nbands()) return RIC_E_ARG;
+	const Band& B = w->P.band(index);
+	if (dimx) *dimx = B.dx;
+	if (dimy) *dimy = B.dy;
+	if (is_int) *is_int = B.is_int;
+	if (weight) *weight = B.weight;
+	return RIC_OK;
+}
+
+int ric_band_read(ric_wavelet* w, int index, int32_t* out)
+{
+	if (!w || !out || index < 0 || index >= w->P.nbands()) return RIC_E_ARG;
+	if (set_dev(w->device)) return RIC_E_HIP;
+	const Band& B = w->P.band(index);
+	if (!w->host_valid) {
+		HIPCHK(hipMemcpyAsync(w->h_arena + B.off, w->d_arena + B.off, B.bytes(), hipMemcpyDeviceToHost, w->st));
+		HIPCHK(hipStreamSynchronize(w->st));
+	}
+	for (int y = 0; y < B.dy; y++)
+		for (int x = 0; x < B.dx; x++) {
+			size_t i = (size_t)y * B.pitch + x;
+			out[(size_t)y * B.dx + x] = B.is_int ? ((int32_t*)(w->h_arena + B.off))[i] : ((int16_t*)(w->h_arena + B.off))[i];
+		}
+	return RIC_OK;
+}
+
+int ric_band_write(ric_wavelet* w, int index, const int32_t* in)
+{
+	if (!w || !in || index < 0 || index >= w->P.nbands()) return RIC_E_ARG;
+	if (set_dev(w->device)) return RIC_E_HIP;
+	int rc = to_device(w);
+	if (rc) return rc;
+	const Band& B = w->P.band(index);
+	HIPCHK(hipStreamSynchronize(w->st));
+	for (int y = 0; y < B.dy; y++)
+		for (int x = 0; x < B.dx; x++) {
+			size_t i = (size_t)y * B.pitch + x;
+			int32_t v = in[(size_t)y * B.dx + x];
+			if (B.is_int) ((int32_t*)(w->h_arena + B.off))[i] = v;
+			else ((int16_t*)(w->h_arena + B.off))[i] = (int16_t)v;
+		}
+	HIPCHK(hipMemcpyAsync(w->d_arena + B.off, w->h_arena + B.off, B.bytes(), hipMemcpyHostToDevice, w->st));
+	HIPCHK(hipStreamSynchronize(w->st));
+	return RIC_OK;
+}
+
+int ric_mux_create_encoder(ric_mux** out, uint8_t* buf, size_t cap, uint16_t first_word)
+{
+	if (!out || !buf) return RIC_E_ARG;
+	ric_mux* m = new ric_mux;
+	m->encoder = true;
+	m->buf = buf;
+	m->m.init_encoder(buf, cap, first_word);
+	*out = m;
+	return RIC_OK;
+}
+
+int ric_mux_create_decoder(ric_mux** out, const uint8_t* buf, size_t len)
+{
+	if (!out || !buf || len < 4) return RIC_E_ARG;
+	ric_mux* m = new ric_mux;
+	m->encoder = false;
+	m->m.init_decoder(buf, len);
+	*out = m;
+	return RIC_OK;
+}
+
+int ric_mux_end(ric_mux* m, size_t* len_out)
+{
+	if (!m || !m->encoder) return RIC_E_ARG;
+	uint8_t* e = m->m.end_coding();
+	if (len_out) *len_out = (size_t)(e - m->buf);
+	return m->m.overflow() ? RIC_E_CAPACITY : RIC_OK;
+}
+
+size_t ric_mux_size(ric_mux* m) { return m ? m->m.size() : 0; }
+
+void ric_mux_destroy(ric_mux* m) { delete m; }
+
+int ric_quants(int idx)
+{
+	static const unsigned short Q[5] = {0x8000, 0x9000, 0xA800, 0xC000, 0xE000};
+	if (idx <= 0) return 0;
+	idx--;
+	int r = 14 - idx / 5;
+	return (short)((Q[idx % 5] + (1 << (r - 1))) >> r);
+}
+
+int ric_read_header(const uint8_t* ric, size_t len, int* w, int* h, int* channels, int* q, int* trans)
+{
+	if (!ric || len < 9) return RIC_E_ARG;
+	if (memcmp(ric, "RUD2", 4) != 0) return RIC_E_FORMAT;
+	if (w) *w = ric[4] | (ric[5] << 8);
+	if (h) *h = ric[6] | (ric[7] << 8);
+	if (q) *q = ric[8] & 31;
+	if (channels) *channels = ((ric[8] >> 5) & 1) ? 3 : 1;
+	if (trans) *trans = (ric[8] >> 6) & 3;
+	return RIC_OK;
+}
+
+int ric_codec_create(ric_codec** out, int w, int h, int channels, int device)
+{
+	if (!out || (channels != 1 && channels != 3)) return RIC_E_ARG;
+	*out = nullptr;
+	ric_codec* c = new ric_codec;
+	c->device = device; c->w = w; c->h = h; c->channels = channels;
+	int rc = ric_wavelet_create(&c->wav, w, h, 5, 1, device);   // WAV_LEVELS 5, level_chg 1 (ric.cpp:159)
+	if (rc) { delete c; return rc; }
+	c->pitch = ((long)w + 63) / 64 * 64;
+	if (hip_fail(hipMalloc(&c->d_planes, (size_t)c->pitch * h * channels * 2), "hipMalloc planes") ||
+	    hip_fail(hipMalloc(&c->d_pix, (size_t)w * h * channels), "hipMalloc pix") ||
+	    hip_fail(hipMalloc(&c->d_out, (size_t)w * h * channels * 2), "hipMalloc out")) {
+		ric_codec_destroy(c);
+		return RIC_E_HIP;
+	}
+	c->stream.resize((size_t)w * h * channels * 2 + 65536);
+	*out = c;
+	return RIC_OK;
+}
+
+void ric_codec_destroy(ric_codec* c)
+{
+	if (!c) return;
+	(void)hipSetDevice(c->device);
+	if (c->wav) ric_wavelet_destroy(c->wav);
+	if (c->d_planes) (void)hipFree(c->d_planes);
+	if (c->d_pix) (void)hipFree(c->d_pix);
+	if (c->d_out) (void)hipFree(c->d_out);
+	delete c;
+}
+
+int ric_codec_set_stream(ric_codec* c, void* s) { return c ? ric_wavelet_set_stream(c->wav, s) : RIC_E_ARG; }
+
+// CompressImage, src/ric/ric.cpp:123-180
+int ric_codec_encode(ric_codec* c, const uint8_t* pix, int on_device, int q, int trans,
+                     uint8_t* out, size_t cap, size_t* len_out)
+{
+	if (!c || !pix || !out || q < 0 || q > 31 || trans < 0 || trans > 2) return RIC_E_ARG;
+	if (set_dev(c->device)) return RIC_E_HIP;
+	ric_wavelet* w = c->wav;
+	const size_t npix = (size_t)c->w * c->h * c->channels;
+	const uint8_t* dpix = pix;
+	if (!on_device) {
+		HIPCHK(hipMemcpyAsync(c->d_pix, pix, npix, hipMemcpyHostToDevice, w->st));
+		dpix = c->d_pix;
+	}
+	launch_pix_in(dpix, c->d_planes, c->w, c->h, c->pitch, c->channels, q, w->st);
+	HIPCHK(hipGetLastError());
+	Mux m;
+	m.init_encoder(c->stream.data(), c->stream.size(), 0);
+	w->P.set_weight(trans);
+	const long plane = c->pitch * c->h;
+	for (int p = 0; p < c->channels; p++) {
+		const int boost = p ? 8 : 0;                // C_Q_BOOST for chroma (ric.cpp:164-168)
+		int rc = forward(w, c->d_planes + p * plane, c->pitch, trans);
+		if (rc) return rc;
+		rc = code_band(w, m, q ? ric_quants(q + 20 + boost) : 0, q ? ric_quants(q + 13 + boost) : 0);
+		if (rc) return rc;
+	}
+	uint8_t* e = m.end_coding();
+	if (m.overflow()) return RIC_E_CAPACITY;
+	const size_t len = (size_t)(e - c->stream.data());
+	const size_t total = 9 + len - 2;
+	if (len_out) *len_out = total;
+	if (total > cap) return RIC_E_CAPACITY;
+	memcpy(out, "RUD2", 4);
+	out[4] = c->w & 255; out[5] = (c->w >> 8) & 255; out[6] = c->h & 255; out[7] = (c->h >> 8) & 255;
+	out[8] = (uint8_t)((q & 31) | ((c->channels == 3) << 5) | ((trans & 3) << 6));
+	memcpy(out + 9, c->stream.data() + 2, len - 2);
+	return RIC_OK;
+}
+
+// DecompressImage, src/ric/ric.cpp:182-251
+int ric_codec_decode(ric_codec* c, const uint8_t* ric, size_t len, int dither,
+                     uint8_t* pix_out, int16_t* planes_out, int on_device)
+{
+	if (!c || !ric) return RIC_E_ARG;
+	int w_, h_, ch, q, trans;
+	int rc = ric_read_header(ric, len, &w_, &h_, &ch, &q, &trans);
+	if (rc) return rc;
+	if (w_ != c->w || h_ != c->h || ch != c->channels || trans > 2) return RIC_E_ARG;
+	if (set_dev(c->device)) return RIC_E_HIP;
+	ric_wavelet* w = c->wav;
+	// the reference reads W*H*C payload bytes at buf + 2 (ric.cpp:203-205)
+	const size_t npix = (size_t)c->w * c->h * c->channels;
+	const size_t pay = std::min(len - 9, npix);
+	std::vector<uint8_t> buf(pay + 2, 0);
+	memcpy(buf.data() + 2, ric + 9, pay);
+	Mux m;
+	m.init_decoder(buf.data(), buf.size());
+	w->P.set_weight(trans);
+	const long plane = c->pitch * c->h;
+	for (int p = 0; p < c->channels; p++) {
+		const int boost = p ? 8 : 0;
+		rc = decode_band(w, m);
+		if (rc && rc != RIC_E_STREAM) return rc;
+		if (q) { rc = tsuqi(w, ric_quants(q + 20 + boost)); if (rc) return rc; }
+		rc = inverse(w, c->d_planes + p * plane, c->pitch, trans);
+		if (rc) return rc;
+	}
+	if (dither && q && c->channels == 1) {
+		// dither() is a serial error diffusion (src/ric/ric.cpp:51-74): host side
+		std::vector<int16_t> img((size_t)c->w * c->h);
+		HIPCHK(hipMemcpy2DAsync(img.data(), (size_t)c->w * 2, c->d_planes, (size_t)c->pitch * 2, (size_t)c->w * 2,
+		                        c->h, hipMemcpyDeviceToHost, w->st));
+		HIPCHK(hipStreamSynchronize(w->st));
+		auto clip = [](int v) { return (int16_t)(v < 0 ? 0 : v > 255 ? 255 : v); };
+		int16_t* pi = img.data();
+		const int W = c->w, H = c->h;
+		for (int j = 0; j < H - 1; j++) {
+			pi[0] = clip(128 + ((pi[0] + 8) >> 4));
+			for (int i = 1; i < W - 1; i++) {
+				int16_t tmp = (int16_t)(pi[i] + 8);
+				pi[i] = (int16_t)(tmp >> 4);
+				tmp = (int16_t)(tmp - (pi[i] << 4));
+				pi[i + 1] += (int16_t)((tmp >> 1) - (tmp >> 4));
+				pi[i + W - 1] += (int16_t)((tmp >> 3) + (tmp >> 4));
+				pi[i + W] += (int16_t)((tmp >> 2) + (tmp >> 4));
+				pi[i + W + 1] += (int16_t)(tmp >> 4);
+				pi[i] = clip(pi[i] + 128);
+			}
+			pi += W;
+			pi[-1] = clip(128 + ((pi[-1] + 8) >> 4));
+		}
+		for (int i = 0; i < W; i++) pi[i] = clip(128 + ((pi[i] + 8) >> 4));
+		std::vector<uint8_t> px(img.size());
+		for (size_t i = 0; i < img.size(); i++) px[i] = (uint8_t)img[i];
+		if (on_device) {
+			if (pix_out) HIPCHK(hipMemcpyAsync(pix_out, px.data(), px.size(), hipMemcpyHostToDevice, w->st));
+			if (planes_out) HIPCHK(hipMemcpyAsync(planes_out, img.data(), img.size() * 2, hipMemcpyHostToDevice, w->st));
+			HIPCHK(hipStreamSynchronize(w->st));
+		} else {
+			if (pix_out) memcpy(pix_out, px.data(), px.size());
+			if (planes_out) memcpy(planes_out, img.data(), img.size() * 2);
+		}
+		return m.overflow() ? RIC_E_STREAM : RIC_OK;
+	}
+	uint8_t* dpix = on_device ? pix_out : (pix_out ? c->d_pix : nullptr);
+	int16_t* dpl = on_device ? planes_out : (planes_out ? c->d_out : nullptr);
+	launch_pix_out(c->d_planes, c->pitch, c->w, c->h, c->channels, q, dpix, dpl, w->st);
+	HIPCHK(hipGetLastError());
+	if (!on_device) {
+		if (pix_out) HIPCHK(hipMemcpyAsync(pix_out, c->d_pix, npix, hipMemcpyDeviceToHost, w->st));
+		if (planes_out) HIPCHK(hipMemcpyAsync(planes_out, c->d_out, npix * 2, hipMemcpyDeviceToHost, w->st));
+	}
+	HIPCHK(hipStreamSynchronize(w->st));
+	return m.overflow() ? RIC_E_STREAM : RIC_OK;
+}
+
+}  // extern "C"

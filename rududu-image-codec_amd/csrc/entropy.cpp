@@ -1,0 +1,657 @@
+// entropy.cpp -- host serial coder of the .ric path (see entropy.h).
+#include "entropy.h"
+
+#include <cstdlib>
+#include <algorithm>
+
+namespace ric {
+
+#include "huff_tables.inc"
+
+namespace {
+
+// Cnk[k][n] = C(n, k + 1) (src/lib/muxcodec.cpp:282-292), built once.
+struct CnkTable {
+	uint16_t v[8][16];
+	CnkTable()
+	{
+		for (int k = 0; k < 8; k++)
+			for (int n = 0; n < 16; n++) {
+				int kk = k + 1;
+				if (n < kk) { v[k][n] = 0; continue; }
+				uint32_t c = 1;
+				for (int i = 1; i <= kk; i++) c = c * (n - kk + i) / i;
+				v[k][n] = (uint16_t)c;
+			}
+	}
+};
+const CnkTable kCnk;
+
+// src/lib/muxcodec.cpp:294-332 (format constants)
+const uint8_t kCnkLen[16][8] = {
+	{0,0,0,0,0,0,0,0},{1,0,0,0,0,0,0,0},{2,2,0,0,0,0,0,0},{2,3,2,0,0,0,0,0},
+	{3,4,4,3,0,0,0,0},{3,4,5,4,3,0,0,0},{3,5,6,6,5,3,0,0},{3,5,6,7,6,5,3,0},
+	{4,6,7,7,7,7,6,4},{4,6,7,8,8,8,7,6},{4,6,8,9,9,9,9,8},{4,7,8,9,10,10,10,9},
+	{4,7,9,10,11,11,11,11},{4,7,9,10,11,12,12,12},{4,7,9,11,12,13,13,13},{4,7,10,11,13,13,14,14}};
+const uint16_t kCnkLost[16][8] = {
+	{0,0,0,0,0,0,0,0},{0,0,0,0,0,0,0,0},{1,1,0,0,0,0,0,0},{0,2,0,0,0,0,0,0},
+	{3,6,6,3,0,0,0,0},{2,1,12,1,2,0,0,0},{1,11,29,29,11,1,0,0},{0,4,8,58,8,4,0,0},
+	{7,28,44,2,2,44,28,7},{6,19,8,46,4,46,8,19},{5,9,91,182,50,50,182,91},
+	{4,62,36,17,232,100,232,17},{3,50,226,309,761,332,332,761},{2,37,148,23,46,1093,664,1093},
+	{1,23,57,683,1093,3187,1757,1757},{0,8,464,228,3824,184,4944,3514}};
+
+// taboo code tables for n = 2 (initTaboo(2), src/lib/muxcodec.cpp:113-129)
+struct TabooTable {
+	uint32_t nb[32], sum[32];
+	TabooTable()
+	{
+		const uint32_t k = 2;
+		nb[0] = 1;
+		for (uint32_t i = 1; i < k; i++) nb[i] = 1u << (i - 1);
+		for (uint32_t i = k; i < 32; i++) {
+			uint32_t acc = nb[i - k];
+			for (uint32_t j = i - k + 1; j < i; j++) acc += nb[j];
+			nb[i] = acc;
+		}
+		sum[0] = nb[0];
+		for (int i = 1; i < 32; i++) sum[i] = sum[i - 1] + nb[i];
+	}
+};
+const TabooTable kTaboo;
+
+// 8-bit first-level decode LUTs for the 33 static Huffman tables:
+// entry = sym << 8 | len, or 0 when the code is longer than 8 bits.
+struct HuffLut {
+	uint16_t lut[33][256];
+	HuffLut()
+	{
+		for (int t = 0; t < 33; t++) {
+			const uint16_t* tab = t < 17 ? kHuff_LOW[t] : kHuff_HIGH[t - 17];
+			int n = t < 17 ? 17 : 16;
+			for (int i = 0; i < 256; i++) {
+				lut[t][i] = 0;
+				for (int s = 0; s < n; s++) {
+					int len = tab[s] & 31;
+					if (len <= 8 && (i >> (8 - len)) == (tab[s] >> 5)) { lut[t][i] = (uint16_t)((s << 8) | len); break; }
+				}
+			}
+		}
+	}
+};
+const HuffLut kHuffLut;
+
+const uint16_t kBitThres[11] = {2584, 1512, 745, 371, 185, 92, 46, 23, 12, 6, 3};   // bitcodec.cpp:40-42
+const uint16_t kGeoThres[11] = {1512, 2584, 3351, 3725, 3911, 4004, 4050, 4073, 4084, 4090, 4093};  // geomcodec.cpp:44-46
+// K and shift (geomcodec.cpp:48-54); entry 24 guards an index the reference
+// never reaches on valid data.
+const uint8_t kGeoK[25] = {0,0,0,0,0,0,0,0,0,0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,14};
+const uint8_t kGeoShift[25] = {10,9,8,7,6,5,4,3,2,1,1,1,1,1,1,1,1,1,1,1,1,1,1,1,1};
+
+constexpr size_t kDecPad = 1 << 16;
+
+}  // namespace
+
+// ================================================================= Mux
+void Mux::init_encoder(uint8_t* buf, size_t cap, uint16_t first_word)
+{
+	base_ = buf;
+	limit_ = buf + cap;
+	low_ = (uint32_t)first_word << 16;
+	range_ = 1u << 16;
+	outcount_ = 0; nbits_ = 0; buffer_ = 0; reserved_ = nullptr; overflow_ = cap < 4;
+	p_ = buf + 4; init_ = buf + 2;
+	for (int i = 0; i < 4; i++) last_[i] = buf + i;
+}
+
+void Mux::init_decoder(const uint8_t* buf, size_t len)
+{
+	owned_ = (uint8_t*)calloc(len + kDecPad, 1);
+	memcpy(owned_, buf, len);
+	base_ = owned_;
+	limit_ = owned_ + len + kDecPad - 16;
+	range_ = 1u << 16;
+	nbits_ = 0; buffer_ = 0; overflow_ = false;
+	init_ = owned_ + 2; p_ = owned_ + 2;
+	code_ = low_ = ((uint32_t)p_[0] << 8) | p_[1];
+	p_ += 2;
+}
+
+Mux::~Mux() { free(owned_); }
+
+void Mux::normalize_enc()                  // src/lib/muxcodec.cpp:63-74
+{
+	flush_buffer(false);
+	do {
+		put(last_[outcount_++ & 3], (uint8_t)(low_ >> 24));
+		if (((low_ + range_ - 1) ^ low_) >= 0x01000000u) range_ = (0u - low_) & 4095u;
+		last_[(outcount_ + 3) & 3] = p_++;
+		range_ <<= 8;
+		low_ <<= 8;
+	} while (range_ <= 4096u);
+}
+
+void Mux::normalize_dec()                  // src/lib/muxcodec.cpp:76-85
+{
+	do {
+		if (((code_ - low_ + range_ - 1) ^ (code_ - low_)) >= 0x01000000u) range_ = (low_ - code_) & 4095u;
+		uint8_t b = *p_;
+		if (p_ < limit_) p_++; else overflow_ = true;
+		low_ = (low_ << 8) | b;
+		code_ = (code_ << 8) | b;
+		range_ <<= 8;
+	} while (range_ <= 4096u);
+}
+
+void Mux::empty_buffer()                   // src/lib/muxcodec.cpp:536-548
+{
+	do {
+		nbits_ -= 8;
+		uint8_t b = (uint8_t)(buffer_ >> nbits_);
+		if (!reserved_) put(p_++, b);
+		else { put(reserved_, b); reserved_ = nullptr; }
+	} while (nbits_ >= 8);
+}
+
+void Mux::flush_buffer(bool end)           // src/lib/muxcodec.cpp:550-570
+{
+	if (nbits_ >= 8) empty_buffer();
+	if (nbits_ > 0) {
+		if (end) {
+			uint8_t b = (uint8_t)(buffer_ << (8 - nbits_));
+			if (!reserved_) put(p_++, b);
+			else { put(reserved_, b); reserved_ = nullptr; }
+			nbits_ = 0;
+		} else if (!reserved_) {
+			reserved_ = p_++;
+		}
+	}
+}
+
+void Mux::fill_buffer(uint32_t len)        // src/lib/muxcodec.cpp:572-579
+{
+	do {
+		nbits_ += 8;
+		buffer_ = (buffer_ << 8) | p_[0];
+		if (p_ < limit_) p_++; else overflow_ = true;
+	} while (nbits_ < len);
+}
+
+uint8_t* Mux::end_coding()                 // src/lib/muxcodec.cpp:87-106
+{
+	flush_buffer(true);
+	if (range_ <= 4096u) normalize_enc();
+	const uint32_t last_out = 0x200 | 'W';
+	if ((low_ & 4095u) > (last_out & 4095u)) low_ += 4096u;
+	low_ = (low_ & ~4095u) | (last_out & 4095u);
+	put(last_[outcount_ & 3], (uint8_t)(low_ >> 24));
+	put(last_[(outcount_ + 1) & 3], (uint8_t)(low_ >> 16));
+	put(last_[(outcount_ + 2) & 3], (uint8_t)(low_ >> 8));
+	put(last_[(outcount_ + 3) & 3], (uint8_t)low_);
+	if (p_ > limit_) overflow_ = true;
+	return p_;
+}
+
+uint32_t Mux::huff_decode(int high, int idx)
+{
+	const int t = high ? 17 + idx : idx;
+	const uint32_t code = (((buffer_ << 16) | ((uint32_t)p_[0] << 8) | p_[1]) >> nbits_) & 0xFFFF;
+	uint32_t e = kHuffLut.lut[t][code >> 8];
+	uint32_t sym, len;
+	if (e) {
+		sym = e >> 8; len = e & 0xFF;
+	} else {
+		const uint16_t* tab = high ? kHuff_HIGH[idx] : kHuff_LOW[idx];
+		const int n = high ? 16 : 17;
+		sym = 0; len = tab[0] & 31;
+		for (int s = 0; s < n; s++) {
+			uint32_t l = tab[s] & 31;
+			if ((code >> (16 - l)) == (uint32_t)(tab[s] >> 5)) { sym = s; len = l; break; }
+		}
+	}
+	p_ -= (int)(nbits_ - len) >> 3;
+	if (p_ > limit_) { p_ = limit_; overflow_ = true; }
+	if (nbits_ < len) buffer_ = p_[-1];
+	nbits_ = (nbits_ - len) & 7;
+	return sym;
+}
+
+void Mux::taboo_code(uint32_t nb)
+{
+	const uint32_t nt = 2;
+	int i = 0, l;
+	uint32_t r = 0;
+	while (kTaboo.sum[i] <= nb) i++;
+	if (i == 0) { bits_code(0, nt); return; }
+	l = i; i--;
+	nb -= kTaboo.sum[i];
+	while (i > (int)nt) {
+		uint32_t k = i - nt + 1, cnt = kTaboo.nb[k], j = 0;
+		while (nb >= cnt) cnt += kTaboo.nb[k + ++j];
+		nb -= cnt - kTaboo.nb[k + j];
+		j = nt - j;
+		r = (r << j) | 1;
+		i -= j;
+	}
+	if (i == (int)nt) nb++;
+	r = ((((r << i) | (nb & ((1u << i) - 1))) << 1) | 1) << nt;
+	bits_code(r, l + nt);
+}
+
+uint32_t Mux::taboo_decode()
+{
+	const uint32_t nt = 2;
+	int i, l = nt;
+	uint32_t nb = 0;
+	if (nbits_ < nt) fill_buffer(nt);
+	uint32_t t = ((1u << nt) - 1) << (nbits_ - nt);
+	while ((~buffer_ & t) != t) {
+		l++;
+		if (l > (int)nbits_) { fill_buffer(l); t <<= 8; }
+		t >>= 1;
+		if (l > 40) { overflow_ = true; return 0; }
+	}
+	nbits_ -= l;
+	uint32_t cd = buffer_ >> (nbits_ + nt + 1);
+	i = l - nt;
+	if (i > 0) { i--; nb += kTaboo.sum[i]; }
+	while (i > (int)nt) {
+		uint32_t j = 1;
+		while (((cd >> (i - j)) & 1) == 0) j++;
+		nb += kTaboo.sum[i - j] - kTaboo.sum[i - nt];
+		i -= j;
+	}
+	if (i == (int)nt) nb -= 1;
+	nb += cd & ((1u << i) - 1);
+	return nb;
+}
+
+void Mux::enum_code(uint32_t bits, uint32_t k, uint32_t nmax)
+{
+	uint32_t code = 0, n = 0, row = 0;
+	if (k > ((nmax + 1) >> 1)) { k = nmax - k; bits ^= (1u << nmax) - 1; }
+	do {
+		if (bits & 1) { code += kCnk.v[row][n]; row++; }
+		n++;
+		bits >>= 1;
+	} while (bits != 0);
+	const uint32_t lost = kCnkLost[nmax - 1][k - 1], len = kCnkLen[nmax - 1][k - 1];
+	if (code < lost) bits_code(code, len - 1);
+	else bits_code(code + lost, len);
+}
+
+uint32_t Mux::enum_decode(uint32_t k, uint32_t nmax)
+{
+	int n = nmax - 1;
+	uint32_t bits = 0;
+	if (k > ((nmax + 1) >> 1)) { k = nmax - k; bits ^= (1u << nmax) - 1; }
+	int row = (int)k - 1;
+	const uint32_t lost = kCnkLost[nmax - 1][k - 1];
+	uint32_t code = bits_decode(kCnkLen[nmax - 1][k - 1] - 1);
+	if (code >= lost) code = ((code << 1) | bits_decode(1)) - lost;
+	do {
+		if (n >= 0 && code >= kCnk.v[row][n]) { bits ^= 1u << n; code -= kCnk.v[row][n]; row--; }
+		n--;
+		if (n < -1) break;
+	} while (row >= 0);
+	return bits;
+}
+
+void Mux::max_code(uint32_t value, uint32_t max)
+{
+	const uint32_t len = bitlen(max), lost = (1u << len) - max - 1;
+	if (value < lost) bits_code(value, len - 1);
+	else bits_code(value + lost, len);
+}
+
+uint32_t Mux::max_decode(uint32_t max)
+{
+	// maxDecode reads one bit even for max == 0 (src/lib/muxcodec.cpp:526-534),
+	// where maxCode wrote none: kept for bit-exactness with the reference.
+	uint32_t value = 0;
+	const uint32_t len = bitlen(max), lost = (1u << len) - max - 1;
+	if (len > 1) value = bits_decode(len - 1);
+	if (value >= lost) value = ((value << 1) | bits_decode(1)) - lost;
+	return value;
+}
+
+// ============================================================== models
+void BitModel::init()
+{
+	for (int i = 0; i < 16; i++) { freq[i] = 2048; shift[i] = 0; mps[i] = 0; }
+}
+
+inline void BitModel::adj(int c)           // shift_adj, bitcodec.h:81-92
+{
+	if (freq[c] > kBitThres[shift[c]]) {
+		if (shift[c] == 0) { mps[c] ^= 1; freq[c] = (uint16_t)(4096 - freq[c]); shift[c] = 1; }
+		else shift[c]--;
+	} else if (shift[c] < 9) shift[c]++;
+}
+
+inline void BitModel::code(Mux& m, uint32_t sym, int c)   // bitcodec.h:52-60
+{
+	const uint32_t s = sym ^ mps[c];
+	m.code_bin(freq[c], s ^ 1);
+	const int sh = shift[c];
+	freq[c] = (uint16_t)(freq[c] + (s << (9 - sh)) - (freq[c] >> (3 + sh)));
+	if ((uint16_t)(freq[c] - kBitThres[sh + 1]) > kBitThres[sh] - kBitThres[sh + 1]) adj(c);
+}
+
+inline uint32_t BitModel::decode(Mux& m, int c)           // bitcodec.h:62-70
+{
+	uint32_t sym = m.get_bit(freq[c]) ^ 1;
+	const int sh = shift[c];
+	freq[c] = (uint16_t)(freq[c] + (sym << (9 - sh)) - (freq[c] >> (3 + sh)));
+	sym ^= mps[c];
+	if ((uint16_t)(freq[c] - kBitThres[sh + 1]) > kBitThres[sh] - kBitThres[sh + 1]) adj(c);
+	return sym;
+}
+
+void GeomModel::init(const uint8_t* kinit)                // setCtx, geomcodec.cpp:31-41
+{
+	for (int c = 0; c < 16; c++) {
+		idx[c] = kinit[c];
+		freq[c] = idx[c] >= 9 ? 2048 : (uint16_t)((kGeoThres[idx[c] - 1] + kGeoThres[idx[c]]) >> 1);
+	}
+}
+
+inline void GeomModel::adj(int c)          // shift_adj, geomcodec.h:88-97
+{
+	const int s = kGeoShift[idx[c]];
+	if (freq[c] < kGeoThres[s - 1]) { if (idx[c] < 24) idx[c]++; }
+	else if (idx[c] > 0) idx[c]--;
+	if (idx[c] >= 9) freq[c] = 2048;
+}
+
+inline void GeomModel::code(Mux& m, uint32_t sym, int c)  // geomcodec.h:41-57
+{
+	const uint32_t k = kGeoK[idx[c]], f = freq[c];
+	const int s = kGeoShift[idx[c]];
+	for (uint32_t l = sym >> k; l > 0; l--) {
+		m.code_bin(f, 1);
+		freq[c] -= freq[c] >> (3 + s);
+	}
+	m.code_bin(f, 0);
+	if (k > 0) m.bits_code(sym & ((1u << k) - 1), k);
+	freq[c] += (4096 - freq[c]) >> (3 + s);
+	if ((uint16_t)(freq[c] - kGeoThres[s - 1]) > kGeoThres[s] - kGeoThres[s - 1]) adj(c);
+}
+
+inline uint32_t GeomModel::decode(Mux& m, int c)          // geomcodec.h:59-75
+{
+	const uint32_t k = kGeoK[idx[c]], f = freq[c];
+	const int s = kGeoShift[idx[c]];
+	uint32_t l = 0;
+	while (m.get_bit(f)) {
+		freq[c] -= freq[c] >> (3 + s);
+		l++;
+		if (l > (1u << 20)) break;           // corrupt stream guard
+	}
+	if (k > 0) l = (l << k) | m.bits_decode(k);
+	freq[c] += (4096 - freq[c]) >> (3 + s);
+	if ((uint16_t)(freq[c] - kGeoThres[s - 1]) > kGeoThres[s] - kGeoThres[s - 1]) adj(c);
+	return l;
+}
+
+// ========================================================== band scans
+namespace {
+
+template <typename C> constexpr bool is_short() { return sizeof(C) == 2; }
+
+template <typename C>
+void pred_t(Mux& m, const BandView& b, bool dec)
+{
+	static const uint8_t ginit[16] = {9,10,11,12,13,14,15,16,17,18,19,20,21,22,23,15};  // bandcodec.cpp:67-68
+	constexpr bool SH = is_short<C>();
+	GeomModel g; g.init(ginit);
+	C* c = (C*)b.p;
+	const long st = b.pitch;
+	if (!dec) m.taboo_code(s2u(c[0]));
+	else c[0] = (C)u2s((int)m.taboo_decode());
+	for (int i = 1; i < b.dx; i++) {
+		if (!dec) g.code(m, s2u(c[i] - c[i - 1]), 15);
+		else c[i] = (C)tr<SH>(c[i - 1] + u2s((int)g.decode(m, 15)));
+	}
+	for (int j = 1; j < b.dy; j++) {
+		c += st;
+		if (!dec) g.code(m, s2u(c[0] - c[-st]), 15);
+		else c[0] = (C)tr<SH>(c[-st] + u2s((int)g.decode(m, 15)));
+		for (int i = 1; i < b.dx; i++) {
+			int a = c[i - 1] - c[i - 1 - st], bb = c[i - st] - c[i - 1 - st];
+			int var = bitlen((uint32_t)((a < 0 ? -a : a) + (bb < 0 ? -bb : bb)));
+			if (!dec) g.code(m, s2u(c[i] - c[i - 1] - c[i - st] + c[i - 1 - st]), var);
+			else c[i] = (C)tr<SH>(c[i - 1] + c[i - st] - c[i - 1 - st] + u2s((int)g.decode(m, var)));
+		}
+	}
+}
+
+const uint8_t kKConv2[9][16] = {                 // bandcodec.cpp:409-420
+	{15}, {7,15}, {4,10,15}, {3,7,11,15}, {2,4,7,10,12,15}, {1,3,5,7,9,11,13,15},
+	{1,3,4,6,8,10,11,13,15}, {0,2,3,4,6,7,8,10,11,12,14,15},
+	{0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,15}};
+const uint8_t kKConv1[16] = {0,1,2,3,0,4,0,5,6,0,0,7,0,0,0,8};   // bandcodec.cpp:422-423
+
+// block_enum (full 4x4), src/lib/bandcodec.cpp:346-403
+template <typename C, bool HIGH, bool DEC>
+inline int block_full(Mux& m, GeomModel& g, C* blk, long st, int idx)
+{
+	constexpr bool SH = is_short<C>();
+	uint32_t k = 0;
+	if (!DEC) {
+		int tmp[16];
+		uint32_t sig = 0;
+		for (int j = 0; j < 4; j++)
+			for (int i = 0; i < 4; i++) {
+				int v = blk[j * st + i];
+				sig <<= 1;
+				if (v != 0) { tmp[k++] = v; sig |= 1; }
+			}
+		const uint16_t e = HIGH ? kHuff_HIGH[idx][k - 1] : kHuff_LOW[idx][k];
+		m.bits_code(e >> 5, e & 31);
+		if (HIGH || k != 0) {
+			if (k != 16) m.enum_code(sig, k, 16);
+			for (uint32_t i = 0; i < k; i++) {
+				g.code(m, (uc<SH>(tmp[i]) >> 1) - 1, k - 1);
+				m.bits_code(tmp[i] & 1, 1);
+			}
+		}
+	} else {
+		k = m.huff_decode(HIGH, idx) + (HIGH ? 1 : 0);
+		if (HIGH || k != 0) {
+			uint32_t sig = 0xFFFF;
+			if (k != 16) sig = m.enum_decode(k, 16);
+			for (int j = 0; j < 4; j++)
+				for (int i = 0; i < 4; i++) {
+					if (sig & (1u << 15)) {
+						uint32_t u = ((g.decode(m, k - 1) + 1) << 1) | m.bits_decode(1);
+						blk[j * st + i] = (C)tr<SH>(u2s_((int)u));
+					}
+					sig <<= 1;
+				}
+		}
+	}
+	return (int)k - (HIGH ? 1 : 0);
+}
+
+// block_enum (edge w x h), src/lib/bandcodec.cpp:405-478
+template <typename C, bool HIGH, bool DEC>
+inline void block_edge(Mux& m, GeomModel& g, C* blk, long st, int w, int h)
+{
+	constexpr bool SH = is_short<C>();
+	uint32_t k = 0;
+	const uint32_t cnt = (uint32_t)(w * h);
+	if (!DEC) {
+		int tmp[16];
+		uint32_t sig = 0;
+		for (int j = 0; j < h; j++)
+			for (int i = 0; i < w; i++) {
+				int v = blk[j * st + i];
+				sig <<= 1;
+				if (v != 0) { tmp[k++] = v; sig |= 1; }
+			}
+		if (HIGH) m.max_code(k - 1, cnt - 1); else m.max_code(k, cnt);
+		if (HIGH || k != 0) {
+			if (k != cnt) m.enum_code(sig, k, cnt);
+			for (uint32_t i = 0; i < k; i++) {
+				g.code(m, (uc<SH>(tmp[i]) >> 1) - 1, kKConv2[kKConv1[cnt]][k - 1]);
+				m.bits_code(tmp[i] & 1, 1);
+			}
+		}
+	} else {
+		k = HIGH ? m.max_decode(cnt - 1) + 1 : m.max_decode(cnt);
+		if (k > cnt) k = cnt;                 // corrupt-stream guard (never on valid data)
+		if (HIGH || k != 0) {
+			uint32_t sig = 0xFFFF;
+			if (k != cnt) sig = m.enum_decode(k, cnt);
+			for (int j = 0; j < h; j++)
+				for (int i = 0; i < w; i++) {
+					if (sig & (1u << (cnt - 1))) {
+						uint32_t u = ((g.decode(m, kKConv2[kKConv1[cnt]][k - 1]) + 1) << 1) | m.bits_decode(1);
+						blk[j * st + i] = (C)tr<SH>(u2s_((int)u));
+					}
+					sig <<= 1;
+				}
+		}
+	}
+}
+
+// maxLen<2, mode>, src/lib/bandcodec.cpp:324-344
+template <typename P, bool DEC>
+inline int max_len2(const P* p, long st)
+{
+	constexpr bool SH = is_short<P>();
+	int mx = 0, mn = 0;
+	for (int j = 0; j < 2; j++)
+		for (int i = 0; i < 2; i++) {
+			int v = p[j * st + i];
+			if (v > mx) mx = v;
+			if (DEC && v < mn) mn = v;
+		}
+	if (!DEC) return bitlen(uc<SH>(mx) >> 1);
+	mn = tr<SH>(mn < 0 ? -mn : mn);
+	if (mn > mx) mx = mn;
+	return bitlen((uint32_t)mx);
+}
+
+// CBandCodec::tree, src/lib/bandcodec.cpp:484-589
+template <typename C, typename P, bool HIGH, bool DEC>
+void tree_t(Mux& m, const BandView& b, const BandView& par, bool has_child)
+{
+	constexpr bool SH = is_short<C>();
+	static const uint8_t ginit[16] = {5,9,9,9,9,9,9,9,9,9,9,9,10,10,10,11};   // bandcodec.cpp:487
+	uint16_t kmean[16] = {2 << 10, 3 << 10, 4 << 10, 5 << 10, 8 << 10, 11 << 10, 13 << 10, 14 << 10,
+	                      15 << 10, 15 << 10, 15 << 10, 15 << 10, 15 << 10, 15 << 10, 15 << 10, 15 << 10};
+	const long st = b.pitch;
+	const int dx = b.dx, dy = b.dy;
+	P* pbase = (P*)par.p;
+	const long pst = par.pitch;
+	const int pdx = par.dx, pdy = par.dy;
+	const int mark = has_child ? kInsignif : 0;
+	C* band = (C*)b.p;
+	if (DEC) for (int j = 0; j < dy; j++) memset(band + j * st, 0, sizeof(C) * dx);   // Clear(), :503
+	GeomModel g; g.init(ginit);
+	BitModel tree, bord; tree.init(); bord.init();
+
+	auto edge_block = [&](C* c1, int i, int w, int h, P* pp, bool chk_row, int j) {
+		if (pp && (i >> 1) < pdx && (!chk_row || (j >> 1) < pdy) && pp[i >> 1] == kInsignif) pp[i >> 1] = 0;
+		uint32_t ins;
+		if (DEC) ins = bord.decode(m, 0);
+		else { ins = c1[i] == (C)kInsignif; bord.code(m, ins, 0); }
+		if (ins) { if (!DEC) c1[i] = 0; }
+		else block_edge<C, HIGH, DEC>(m, g, c1 + i, st, w, h);
+	};
+
+	int j = 0;
+	for (; j + 4 <= dy; j += 4) {
+		C* c1 = band + j * st;
+		C* c2 = c1 + 2 * st;
+		P* pp = pbase ? pbase + (long)(j >> 1) * pst : nullptr;
+		int i = 0, bs = 4;
+		if (j & 4) {
+			bs = -4;
+			i = dx & ~3;
+			if (dx > i) edge_block(c1, i, dx - i, 4, pp, false, j);
+			i += bs;
+		}
+		for (; i >= 0 && i + 4 <= dx; i += bs) {
+			int ctx = 15;
+			const int k = i >> 1;
+			if (pp) ctx = pp[k];
+			if (ctx == kInsignif) {
+				pp[k] = 0;
+				c1[i] = c1[i + 2] = c2[i] = c2[i + 2] = (C)tr<SH>(mark);
+				continue;
+			}
+			if (pp) ctx = max_len2<P, DEC>(pp + k, pst);
+			uint32_t ins;
+			if (DEC) ins = tree.decode(m, ctx);
+			else { ins = c1[i] == (C)kInsignif; tree.code(m, ins, ctx); }
+			if (ins) {
+				c1[i] = c1[i + 2] = c2[i] = c2[i + 2] = (C)tr<SH>(mark);
+			} else {
+				const int idx = (kmean[ctx] + (1 << 9)) >> 10;
+				const int kk = block_full<C, HIGH, DEC>(m, g, c1 + i, st, idx);
+				kmean[ctx] = (uint16_t)(kmean[ctx] + ((uint32_t)kk << 7) - (kmean[ctx] >> 3));
+			}
+		}
+		if (i > 0 && i < dx) edge_block(c1, i, dx - i, 4, pp, false, j);
+	}
+	if (j < dy) {
+		C* c1 = band + j * st;
+		P* pp = pbase ? pbase + (long)(j >> 1) * pst : nullptr;
+		const int h = dy - j;
+		int i = 0, bs = 4;
+		if (j & 4) {
+			bs = -4;
+			i = dx & ~3;
+			if (dx > i) edge_block(c1, i, dx - i, h, pp, true, j);
+			i += bs;
+		}
+		for (; i >= 0 && i + 4 <= dx; i += bs) {
+			if (pp && (j >> 1) < pdy && pp[i >> 1] == kInsignif) pp[i >> 1] = 0;
+			uint32_t ins;
+			if (DEC) ins = bord.decode(m, 0);
+			else { ins = c1[i] == (C)kInsignif; bord.code(m, ins, 0); }
+			if (ins) { if (!DEC) c1[i] = 0; }
+			else block_edge<C, HIGH, DEC>(m, g, c1 + i, st, 4, h);
+		}
+		if (i > 0 && i < dx) edge_block(c1, i, dx - i, h, pp, true, j);
+	}
+}
+
+template <bool DEC>
+void tree_dispatch(Mux& m, const BandView& b, const BandView& par, bool high, bool has_child)
+{
+	const bool pint = par.p ? par.is_int : b.is_int;
+	if (!b.is_int && !pint) {
+		if (high) tree_t<int16_t, int16_t, true, DEC>(m, b, par, has_child);
+		else tree_t<int16_t, int16_t, false, DEC>(m, b, par, has_child);
+	} else if (!b.is_int) {
+		if (high) tree_t<int16_t, int32_t, true, DEC>(m, b, par, has_child);
+		else tree_t<int16_t, int32_t, false, DEC>(m, b, par, has_child);
+	} else {
+		if (high) tree_t<int32_t, int32_t, true, DEC>(m, b, par, has_child);
+		else tree_t<int32_t, int32_t, false, DEC>(m, b, par, has_child);
+	}
+}
+
+}  // namespace
+
+void pred_encode(Mux& m, const BandView& b)
+{
+	if (b.is_int) pred_t<int32_t>(m, b, false); else pred_t<int16_t>(m, b, false);
+}
+void pred_decode(Mux& m, const BandView& b)
+{
+	if (b.is_int) pred_t<int32_t>(m, b, true); else pred_t<int16_t>(m, b, true);
+}
+void tree_encode(Mux& m, const BandView& b, const BandView& par, bool high, bool has_child)
+{
+	tree_dispatch<false>(m, b, par, high, has_child);
+}
+void tree_decode(Mux& m, const BandView& b, const BandView& par, bool high, bool has_child)
+{
+	tree_dispatch<true>(m, b, par, high, has_child);
+}
+
+}  // namespace ric

@@ -1,0 +1,119 @@
+// entropy.h -- the serial part of the .ric path, on the host: the multiplexed
+// carry-less range coder / raw-bit packer (CMuxCodec, src/lib/muxcodec.*), the
+// adaptive binary and geometric models (CBitCodec src/lib/bitcodec.*,
+// CGeomCodec src/lib/geomcodec.*) and the per-band zerotree / LL-DPCM scans
+// (CBandCodec::tree / pred, src/lib/bandcodec.cpp:62-104, 484-589).
+//
+// Everything here is inherently sequential (one adaptive state per band, one
+// range-coder state per stream: SURVEY.md §7.1); the data-parallel stages
+// (DWT, RD quantiser, dequantiser, inverse DWT) run on the GPU.
+#pragma once
+#include <cstdint>
+#include <cstddef>
+#include <cstring>
+#include "ric_types.h"
+
+namespace ric {
+
+// ------------------------------------------------------------------ mux
+class Mux {
+public:
+	// encoder over [buf, buf + cap); first two bytes are the reference's
+	// firstWord slots (src/lib/muxcodec.cpp:36-49)
+	void init_encoder(uint8_t* buf, size_t cap, uint16_t first_word = 0);
+	// decoder over a copy of [buf, buf + len) padded with zeros
+	void init_decoder(const uint8_t* buf, size_t len);
+	~Mux();
+
+	uint8_t* end_coding();                  // endCoding, muxcodec.cpp:87-106
+	size_t size() const { return (size_t)(p_ - init_); }   // getSize
+	bool overflow() const { return overflow_; }
+	uint8_t* buffer() const { return base_; }
+
+	inline void code_bin(uint32_t freq, uint32_t bit)    // codeBin, muxcodec.h:156-163
+	{
+		if (range_ <= 4096u) normalize_enc();
+		const uint32_t t = (range_ * freq) >> 12;
+		low_ += t & (0u - bit);
+		range_ = t + ((range_ - 2 * t) & (0u - bit));
+	}
+	inline uint32_t get_bit(uint32_t freq)                // getBit, muxcodec.h:205-213
+	{
+		if (range_ <= 4096u) normalize_dec();
+		const uint32_t t = (range_ * freq) >> 12;
+		const uint32_t tst = (uint32_t)(low_ < t) - 1u;
+		low_ -= t & tst;
+		range_ = t + ((range_ - 2 * t) & tst);
+		return 0u - tst;
+	}
+	inline void bits_code(uint32_t bits, uint32_t len)    // bitsCode, muxcodec.h:225-231
+	{
+		if (nbits_ + len > 32) empty_buffer();
+		buffer_ = (buffer_ << len) | bits;
+		nbits_ += len;
+	}
+	inline uint32_t bits_decode(uint32_t len)             // bitsDecode, muxcodec.h:233-239
+	{
+		if (nbits_ < len) fill_buffer(len);
+		nbits_ -= len;
+		return (buffer_ >> nbits_) & ((1u << len) - 1);
+	}
+	// canonical-table Huffman decode (huffDecode, muxcodec.h:241-276)
+	uint32_t huff_decode(int table_is_high, int idx);
+
+	void taboo_code(uint32_t nb);           // muxcodec.cpp:210-240 (n = 2)
+	uint32_t taboo_decode();                // muxcodec.cpp:242-280
+	void enum_code(uint32_t bits, uint32_t k, uint32_t nmax);   // muxcodec.cpp:341-365
+	uint32_t enum_decode(uint32_t k, uint32_t nmax);            // muxcodec.cpp:381-405
+	void max_code(uint32_t value, uint32_t max);                // muxcodec.cpp:516-524
+	uint32_t max_decode(uint32_t max);                          // muxcodec.cpp:526-534
+
+private:
+	void normalize_enc();
+	void normalize_dec();
+	void empty_buffer();
+	void flush_buffer(bool end);
+	void fill_buffer(uint32_t len);
+	inline void put(uint8_t* slot, uint8_t v) { if (slot < limit_) *slot = v; else overflow_ = true; }
+
+	uint8_t *base_ = nullptr, *p_ = nullptr, *init_ = nullptr, *limit_ = nullptr;
+	uint8_t *last_[4] = {nullptr, nullptr, nullptr, nullptr}, *reserved_ = nullptr;
+	uint8_t* owned_ = nullptr;              // decoder copy
+	uint32_t range_ = 0, low_ = 0, code_ = 0, outcount_ = 0, nbits_ = 0, buffer_ = 0;
+	bool overflow_ = false;
+};
+
+// ---------------------------------------------------------------- models
+struct BitModel {                           // CBitCodec (16 contexts)
+	uint16_t freq[16];
+	uint8_t shift[16], mps[16];
+	void init();
+	inline void adj(int c);
+	inline void code(Mux& m, uint32_t sym, int c);
+	inline uint32_t decode(Mux& m, int c);
+};
+
+struct GeomModel {                          // CGeomCodec (16 contexts)
+	uint16_t freq[16];
+	uint8_t idx[16];
+	void init(const uint8_t* kinit);
+	inline void adj(int c);
+	inline void code(Mux& m, uint32_t sym, int c);
+	inline uint32_t decode(Mux& m, int c);
+};
+
+// --------------------------------------------------------- band scans
+// Views of a band in host memory (arena layout: pitch in elements).
+struct BandView {
+	void* p = nullptr;
+	int pitch = 0, dx = 0, dy = 0, is_int = 0;
+};
+
+// CBandCodec::pred (LL DPCM), src/lib/bandcodec.cpp:62-104
+void pred_encode(Mux& m, const BandView& b);
+void pred_decode(Mux& m, const BandView& b);
+// CBandCodec::tree, src/lib/bandcodec.cpp:484-589.  par.p == nullptr: no parent.
+void tree_encode(Mux& m, const BandView& b, const BandView& par, bool high, bool has_child);
+void tree_decode(Mux& m, const BandView& b, const BandView& par, bool high, bool has_child);
+
+}  // namespace ric

@@ -1,0 +1,248 @@
+// quant.hip -- per-band RD quantiser + zerotree significance (buildTree), the
+// LL dead-zone quantiser and the dequantiser, hand-written for gfx950.
+//
+// k_quant_level restates CBandCodec::buildTree / tsuqBlock / makeThres
+// (src/lib/bandcodec.cpp:149-319) for the D, H and V bands of one level: one
+// lane per 4x4 block, the 16 coefficients held in registers.  The reference's
+// stable insertion sort of the RD candidates followed by the suffix
+// thresholding (bandcodec.cpp:115-127, 188-198) becomes a 16-key bitonic
+// network on packed (key << 4 | 15 - index) words: a candidate survives iff its
+// packed key is >= the smallest packed key whose sorted rank r fails
+// `key < rd_thres[r + cnt]`.  Levels run finest -> coarsest because a parent's
+// significance adds its four children's pRD (bandcodec.cpp:267-269).
+#include <hip/hip_runtime.h>
+#include "ric_types.h"
+#include "ric_kernels.h"
+
+namespace ric {
+
+namespace {
+
+struct QArgs {
+	void* band[3];
+	int pitch[3], dx[3], dy[3], bw[3];
+	int first[4];                 // block-index prefix over D, H, V
+	uint32_t* rd[3];
+	const uint32_t* crd[3];       // children pRD (nullptr at the finest level)
+	int cbw[3];
+	int Q[3], iQ[3];
+	int thres[3][16];
+};
+
+template <bool SH>
+__device__ __forceinline__ int quant_mag(int v, int iQ)
+{
+	// (tmp * iQuant + (1 << 15)) >> 16 with x86 wrap-around semantics
+	int tmp = (int)(uc<SH>(v) >> 1);
+	int q = (int)((uint32_t)tmp * (uint32_t)iQ + 32768u) >> 16;
+	return tr<SH>((q << 1) | (v & 1));
+}
+
+__device__ __forceinline__ void sort16_desc(uint32_t (&s)[16])
+{
+#pragma unroll
+	for (int k = 2; k <= 16; k <<= 1) {
+#pragma unroll
+		for (int j = k >> 1; j > 0; j >>= 1) {
+#pragma unroll
+			for (int i = 0; i < 16; i++) {
+				int l = i ^ j;
+				if (l > i) {
+					uint32_t a = s[i], b = s[l];
+					bool desc = (i & k) == 0;
+					uint32_t hi = a > b ? a : b, lo = a > b ? b : a;
+					s[i] = desc ? hi : lo;
+					s[l] = desc ? lo : hi;
+				}
+			}
+		}
+	}
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) k_quant_level(QArgs a, int nblk)
+{
+	constexpr bool SH = sizeof(T) == 2;
+	__shared__ int s_thres[3][16];
+	if (threadIdx.x < 48) s_thres[threadIdx.x / 16][threadIdx.x % 16] = a.thres[threadIdx.x / 16][threadIdx.x % 16];
+	__syncthreads();
+	int gid = blockIdx.x * blockDim.x + threadIdx.x;
+	if (gid >= nblk) return;
+	int b = gid >= a.first[2] ? 2 : gid >= a.first[1] ? 1 : 0;
+	int k = gid - a.first[b];
+	int bwid = a.bw[b];
+	int kx = k % bwid, ky = k / bwid;
+	int x0 = kx * 4, y0 = ky * 4;
+	int dx = a.dx[b], dy = a.dy[b], pitch = a.pitch[b];
+	int Q = a.Q[b], iQ = a.iQ[b];
+	T* base = (T*)a.band[b] + (long)y0 * pitch + x0;
+	uint32_t dist;
+
+	if (x0 + 4 <= dx && y0 + 4 <= dy) {
+		// tsuqBlock (RD), src/lib/bandcodec.cpp:159-213
+		int v[16];
+#pragma unroll
+		for (int r = 0; r < 4; r++) {
+			if constexpr (SH) {
+				uint2 u = *reinterpret_cast<const uint2*>(base + (long)r * pitch);
+				v[4 * r + 0] = (int16_t)(u.x & 0xffff); v[4 * r + 1] = (int16_t)(u.x >> 16);
+				v[4 * r + 2] = (int16_t)(u.y & 0xffff); v[4 * r + 3] = (int16_t)(u.y >> 16);
+			} else {
+				int4 u = *reinterpret_cast<const int4*>(base + (long)r * pitch);
+				v[4 * r + 0] = u.x; v[4 * r + 1] = u.y; v[4 * r + 2] = u.z; v[4 * r + 3] = u.w;
+			}
+		}
+		const int T0 = tr<SH>(Q >> 1);
+		const uint32_t th0 = uc<SH>(s_thres[b][0]);
+		int cnt = 0, ncand = 0;
+		uint32_t key[16];
+#pragma unroll
+		for (int i = 0; i < 16; i++) {
+			key[i] = 0;
+			int x = v[i];
+			if ((uint32_t)(x + T0) <= (uint32_t)(2 * T0)) { v[i] = 0; continue; }
+			x = tr<SH>(s2u_(x));
+			if (uc<SH>(x) < th0) {
+				v[i] = x;
+				key[i] = (uc<SH>(x) << 4) | (uint32_t)(15 - i);
+				ncand++;
+			} else {
+				cnt++;
+				v[i] = quant_mag<SH>(x, iQ);
+			}
+		}
+		if (ncand) {
+			uint32_t s[16];
+#pragma unroll
+			for (int i = 0; i < 16; i++) s[i] = key[i];
+			sort16_desc(s);
+			uint32_t thr = 0xFFFFFFFFu;
+#pragma unroll
+			for (int r = 0; r < 16; r++) {
+				if (r < ncand) {
+					int kv = tr<SH>((int)(s[r] >> 4));
+					if (!(kv < s_thres[b][r + cnt])) thr = s[r];
+				}
+			}
+			int surv = 0;
+#pragma unroll
+			for (int i = 0; i < 16; i++) {
+				if (key[i]) {
+					if (key[i] >= thr) { v[i] = tr<SH>(2 | (v[i] & 1)); surv++; }
+					else v[i] = 0;
+				}
+			}
+			cnt += surv;
+		}
+		uint64_t d = (uint64_t)cnt;
+		if (a.crd[b]) {
+			const uint32_t* c0 = a.crd[b] + (long)(2 * ky) * a.cbw[b];
+			const uint32_t* c1 = c0 + a.cbw[b];
+			d += (uint32_t)(c0[2 * kx] + c0[2 * kx + 1] + c1[2 * kx] + c1[2 * kx + 1]);
+		}
+		dist = d > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)d;
+		if (dist == 0) v[0] = kInsignif;
+#pragma unroll
+		for (int r = 0; r < 4; r++) {
+			if constexpr (SH) {
+				uint2 u;
+				u.x = (uint32_t)(uint16_t)v[4 * r] | ((uint32_t)(uint16_t)v[4 * r + 1] << 16);
+				u.y = (uint32_t)(uint16_t)v[4 * r + 2] | ((uint32_t)(uint16_t)v[4 * r + 3] << 16);
+				*reinterpret_cast<uint2*>(base + (long)r * pitch) = u;
+			} else {
+				*reinterpret_cast<int4*>(base + (long)r * pitch) = make_int4(v[4 * r], v[4 * r + 1], v[4 * r + 2], v[4 * r + 3]);
+			}
+		}
+	} else {
+		// edge tsuqBlock, src/lib/bandcodec.cpp:215-237 (children ignored)
+		int wdt = min(4, dx - x0), hgt = min(4, dy - y0);
+		const int T0 = tr<SH>((Q + ((Q - (Q >> 2)) >> 1)) >> 1);
+		int cnt = 0;
+		for (int r = 0; r < hgt; r++)
+			for (int c = 0; c < wdt; c++) {
+				T* p = base + (long)r * pitch + c;
+				int x = *p;
+				if ((uint32_t)(x + T0) <= (uint32_t)(2 * T0)) { *p = 0; continue; }
+				x = tr<SH>(s2u_(x));
+				cnt++;
+				*p = (T)quant_mag<SH>(x, iQ);
+			}
+		dist = (uint32_t)cnt;
+		if (dist == 0) *base = (T)kInsignif;
+	}
+	a.rd[b][(long)ky * bwid + kx] = dist;
+}
+
+template <typename T>
+__global__ void k_quant_ll(T* p, int pitch, int dx, int dy, int iQ, int T0)
+{
+	constexpr bool SH = sizeof(T) == 2;
+	int i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= dx * dy) return;
+	T* q = p + (long)(i / dx) * pitch + i % dx;
+	int v = *q;
+	if ((uint32_t)(v + T0) <= (uint32_t)(2 * T0)) *q = 0;
+	else *q = (T)tr<SH>((int)((uint32_t)v * (uint32_t)iQ + 32768u) >> 16);
+}
+
+template <typename T>
+__global__ void k_dequant(T* p, int pitch, int dx, int dy, int q)
+{
+	constexpr bool SH = sizeof(T) == 2;
+	int i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= dx * dy) return;
+	T* e = p + (long)(i / dx) * pitch + i % dx;
+	*e = (T)tr<SH>((int)((uint32_t)(int)*e * (uint32_t)q));
+}
+
+}  // namespace
+
+void launch_quant_level(const Pyramid& P, int l, const QuantParams& qp, char* arena, hipStream_t st)
+{
+	const Level& L = P.L[l];
+	QArgs a;
+	int n = 0;
+	for (int b = 0; b < 3; b++) {
+		const Band& B = L.b[b];
+		a.band[b] = arena + B.off;
+		a.pitch[b] = B.pitch; a.dx[b] = B.dx; a.dy[b] = B.dy; a.bw[b] = B.bw();
+		a.first[b] = n; n += B.bw() * B.bh();
+		a.rd[b] = (uint32_t*)(arena + B.rd_off);
+		if (l > 0) {
+			const Band& C = P.L[l - 1].b[b];
+			a.crd[b] = (const uint32_t*)(arena + C.rd_off);
+			a.cbw[b] = C.bw();
+		} else {
+			a.crd[b] = nullptr; a.cbw[b] = 0;
+		}
+		a.Q[b] = qp.Q[b]; a.iQ[b] = qp.iQ[b];
+		for (int i = 0; i < 16; i++) a.thres[b][i] = qp.thres[b][i];
+	}
+	a.first[3] = n;
+	if (n == 0) return;
+	dim3 grid((n + 255) / 256);
+	if (L.is_int) hipLaunchKernelGGL(k_quant_level<int32_t>, grid, dim3(256), 0, st, a, n);
+	else hipLaunchKernelGGL(k_quant_level<int16_t>, grid, dim3(256), 0, st, a, n);
+}
+
+void launch_quant_ll(const Pyramid& P, int Q, int iQ, int T0, char* arena, hipStream_t st)
+{
+	const Band& B = P.L[P.nlev - 1].b[BL];
+	(void)Q;
+	int n = B.dx * B.dy;
+	if (n == 0) return;
+	dim3 grid((n + 255) / 256);
+	if (B.is_int) hipLaunchKernelGGL(k_quant_ll<int32_t>, grid, dim3(256), 0, st, (int32_t*)(arena + B.off), B.pitch, B.dx, B.dy, iQ, T0);
+	else hipLaunchKernelGGL(k_quant_ll<int16_t>, grid, dim3(256), 0, st, (int16_t*)(arena + B.off), B.pitch, B.dx, B.dy, iQ, T0);
+}
+
+void launch_dequant_band(const Band& B, int q, char* arena, hipStream_t st)
+{
+	int n = B.dx * B.dy;
+	if (n == 0) return;
+	dim3 grid((n + 255) / 256);
+	if (B.is_int) hipLaunchKernelGGL(k_dequant<int32_t>, grid, dim3(256), 0, st, (int32_t*)(arena + B.off), B.pitch, B.dx, B.dy, q);
+	else hipLaunchKernelGGL(k_dequant<int16_t>, grid, dim3(256), 0, st, (int16_t*)(arena + B.off), B.pitch, B.dx, B.dy, q);
+}
+
+}  // namespace ric

@@ -1,0 +1,30 @@
+// ric_kernels.h -- host-side launchers of the HIP kernels (dwt.hip, quant.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include "ric_types.h"
+
+namespace ric {
+
+// Forward level: src (level input, in_is_int ? int32 : int16, pitch sp) -> the
+// level's D/H/V/L bands in the arena.  vec: src rows are 8/16-byte aligned.
+void launch_fwd_level(const Level& L, const void* src, long sp, char* arena, int trans, int vec,
+                      hipStream_t st);
+// Inverse level: D/H/V bands + lls (the level's LL) -> out (pitch po elements),
+// typed int32 if out_is_int else int16.
+void launch_inv_level(const Level& L, const Band& lls, char* arena, void* out, long po,
+                      int out_is_int, int trans, hipStream_t st);
+
+// Per-band quantiser parameters computed on the host (float32 exactly as the
+// reference: src/lib/bandcodec.cpp:243-247, 149-157).
+struct QuantParams {
+	int Q[3], iQ[3];
+	int thres[3][16];
+};
+// buildTree for the D/H/V bands of one level (finest level first).
+void launch_quant_level(const Pyramid& P, int l, const QuantParams& qp, char* arena, hipStream_t st);
+// CBand::TSUQ on the coarsest LL (src/lib/band.h:65-92).
+void launch_quant_ll(const Pyramid& P, int Q, int iQ, int T, char* arena, hipStream_t st);
+// CBand::TSUQi on one band (src/lib/band.h:94-107).
+void launch_dequant_band(const Band& B, int q, char* arena, hipStream_t st);
+
+}  // namespace ric

@@ -1,0 +1,266 @@
+"""ric_amd -- Python mirror of the reference's src/lib codec interface over the
+C-ABI in include/ric_gpu.h (librududu_amd.so).
+
+Names follow the reference: ``Wavelet2D`` ~ CWavelet2D (src/lib/wavelet2d.h),
+``MuxCodec`` ~ CMuxCodec (src/lib/muxcodec.h), ``Codec.compress`` /
+``Codec.decompress`` ~ CompressImage / DecompressImage (src/ric/ric.cpp).
+
+This module is plumbing for tests and the benchmark; the product is the HIP
+library.  Loading fails loudly when the library is missing -- there is no CPU
+fallback.  Device buffers are passed as raw pointers (e.g. a torch tensor's
+``data_ptr()``); host buffers as numpy arrays.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "librududu_amd.so")
+
+RIC_OK, RIC_E_ARG, RIC_E_HIP, RIC_E_CAPACITY, RIC_E_FORMAT, RIC_E_STREAM = 0, -1, -2, -3, -4, -5
+CDF97, CDF53, HAAR = 0, 1, 2
+
+_P, _I, _S, _F = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, ctypes.c_float
+
+
+class RicError(RuntimeError):
+    def __init__(self, rc, what):
+        self.rc = rc
+        super().__init__("%s failed: status %d (%s)" % (what, rc, last_error()))
+
+
+_lib = None
+
+
+def lib():
+    """Load librududu_amd.so (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError("librududu_amd.so not built: run `python %s`" % os.path.join(HERE, "build.py"))
+    L = ctypes.CDLL(LIB_PATH)
+    sig = {
+        "ric_version": (ctypes.c_char_p, []),
+        "ric_device_count": (_I, []),
+        "ric_last_error": (ctypes.c_char_p, []),
+        "ric_wavelet_create": (_I, [ctypes.POINTER(_P), _I, _I, _I, _I, _I]),
+        "ric_wavelet_destroy": (None, [_P]),
+        "ric_wavelet_set_stream": (_I, [_P, _P]),
+        "ric_wavelet_sync": (_I, [_P]),
+        "ric_set_weight": (_I, [_P, _I, _F]),
+        "ric_transform": (_I, [_P, _P, _I, _I, _I]),
+        "ric_transform_inv": (_I, [_P, _P, _I, _I, _I]),
+        "ric_code_band": (_I, [_P, _P, _I, _I]),
+        "ric_decode_band": (_I, [_P, _P]),
+        "ric_tsuqi": (_I, [_P, _I]),
+        "ric_band_count": (_I, [_P]),
+        "ric_band_info": (_I, [_P, _I, ctypes.POINTER(_I), ctypes.POINTER(_I), ctypes.POINTER(_I), ctypes.POINTER(_F)]),
+        "ric_band_read": (_I, [_P, _I, _P]),
+        "ric_band_write": (_I, [_P, _I, _P]),
+        "ric_mux_create_encoder": (_I, [ctypes.POINTER(_P), _P, _S, ctypes.c_uint16]),
+        "ric_mux_create_decoder": (_I, [ctypes.POINTER(_P), _P, _S]),
+        "ric_mux_end": (_I, [_P, ctypes.POINTER(_S)]),
+        "ric_mux_size": (_S, [_P]),
+        "ric_mux_destroy": (None, [_P]),
+        "ric_codec_create": (_I, [ctypes.POINTER(_P), _I, _I, _I, _I]),
+        "ric_codec_destroy": (None, [_P]),
+        "ric_codec_set_stream": (_I, [_P, _P]),
+        "ric_codec_encode": (_I, [_P, _P, _I, _I, _I, _P, _S, ctypes.POINTER(_S)]),
+        "ric_codec_decode": (_I, [_P, _P, _S, _I, _P, _P, _I]),
+        "ric_read_header": (_I, [_P, _S, ctypes.POINTER(_I), ctypes.POINTER(_I), ctypes.POINTER(_I),
+                                 ctypes.POINTER(_I), ctypes.POINTER(_I)]),
+        "ric_quants": (_I, [_I]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype, f.argtypes = res, args
+    _lib = L
+    return L
+
+
+def exported_symbols():
+    """Names of the C-ABI entry points this binding expects."""
+    lib()
+    return [n for n in dir(_lib) if n.startswith("ric_")]
+
+
+def last_error():
+    return lib().ric_last_error().decode(errors="replace")
+
+
+def _chk(rc, what):
+    if rc != RIC_OK:
+        raise RicError(rc, what)
+
+
+def _ptr(x):
+    if x is None:
+        return None
+    if isinstance(x, int):
+        return x
+    if isinstance(x, np.ndarray):
+        return x.ctypes.data
+    if hasattr(x, "data_ptr"):
+        return x.data_ptr()
+    raise TypeError(type(x))
+
+
+def quants(idx):
+    return lib().ric_quants(idx)
+
+
+class MuxCodec:
+    """CMuxCodec: host serial range coder / raw-bit multiplexer."""
+
+    def __init__(self, buf, first_word=None, length=None):
+        self._buf = buf
+        h = _P()
+        if first_word is not None:       # encoder: CMuxCodec(pStream, firstWord)
+            _chk(lib().ric_mux_create_encoder(ctypes.byref(h), _ptr(buf), buf.nbytes, first_word), "CMuxCodec(enc)")
+            self.encoder = True
+        else:                            # decoder: CMuxCodec(pStream)
+            n = buf.nbytes if length is None else length
+            _chk(lib().ric_mux_create_decoder(ctypes.byref(h), _ptr(buf), n), "CMuxCodec(dec)")
+            self.encoder = False
+        self.h = h
+
+    def endCoding(self):
+        n = _S()
+        _chk(lib().ric_mux_end(self.h, ctypes.byref(n)), "endCoding")
+        return n.value
+
+    def getSize(self):
+        return lib().ric_mux_size(self.h)
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.ric_mux_destroy(self.h)
+            self.h = None
+
+
+class Wavelet2D:
+    """CWavelet2D(x, y, level, level_chg): band pyramid resident in HBM."""
+
+    def __init__(self, x, y, level, level_chg=0, device=0):
+        h = _P()
+        _chk(lib().ric_wavelet_create(ctypes.byref(h), x, y, level, level_chg, device), "CWavelet2D")
+        self.h = h
+        self.DimX, self.DimY = x, y
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.ric_wavelet_destroy(self.h)
+            self.h = None
+
+    def set_stream(self, stream_ptr):
+        _chk(lib().ric_wavelet_set_stream(self.h, stream_ptr), "set_stream")
+
+    def sync(self):
+        _chk(lib().ric_wavelet_sync(self.h), "sync")
+
+    def SetWeight(self, t, baseWeight=1.0):
+        _chk(lib().ric_set_weight(self.h, t, baseWeight), "SetWeight")
+
+    def Transform(self, image, stride, t, on_device=None):
+        dev = on_device if on_device is not None else not isinstance(image, np.ndarray)
+        _chk(lib().ric_transform(self.h, _ptr(image), stride, t, int(dev)), "Transform")
+
+    def TransformI(self, image, stride, t, on_device=None):
+        dev = on_device if on_device is not None else not isinstance(image, np.ndarray)
+        _chk(lib().ric_transform_inv(self.h, _ptr(image), stride, t, int(dev)), "TransformI")
+
+    def CodeBand(self, codec, quant, lam):
+        _chk(lib().ric_code_band(self.h, codec.h, quant, lam), "CodeBand")
+
+    def DecodeBand(self, codec):
+        rc = lib().ric_decode_band(self.h, codec.h)
+        if rc not in (RIC_OK, RIC_E_STREAM):
+            _chk(rc, "DecodeBand")
+        return rc
+
+    def TSUQi(self, quant):
+        _chk(lib().ric_tsuqi(self.h, quant), "TSUQi")
+
+    def band_count(self):
+        return lib().ric_band_count(self.h)
+
+    def band_info(self, i):
+        dx, dy, isint, w = _I(), _I(), _I(), _F()
+        _chk(lib().ric_band_info(self.h, i, ctypes.byref(dx), ctypes.byref(dy), ctypes.byref(isint),
+                                 ctypes.byref(w)), "band_info")
+        return dx.value, dy.value, isint.value, w.value
+
+    def bands(self):
+        """All bands in canonical order (finest->coarsest D,H,V; then LL)."""
+        out = []
+        for i in range(self.band_count()):
+            dx, dy, _, _ = self.band_info(i)
+            a = np.zeros((dy, dx), np.int32)
+            _chk(lib().ric_band_read(self.h, i, a.ctypes.data), "band_read")
+            out.append(a)
+        return out
+
+    def write_band(self, i, arr):
+        a = np.ascontiguousarray(arr, np.int32)
+        _chk(lib().ric_band_write(self.h, i, a.ctypes.data), "band_write")
+
+
+def read_header(ric):
+    b = np.frombuffer(ric, np.uint8)
+    w, h, c, q, t = _I(), _I(), _I(), _I(), _I()
+    _chk(lib().ric_read_header(b.ctypes.data, len(ric), ctypes.byref(w), ctypes.byref(h), ctypes.byref(c),
+                               ctypes.byref(q), ctypes.byref(t)), "read_header")
+    return w.value, h.value, c.value, q.value, t.value
+
+
+class Codec:
+    """CompressImage / DecompressImage for one image geometry on one GPU."""
+
+    def __init__(self, w, h, channels=1, device=0):
+        hd = _P()
+        _chk(lib().ric_codec_create(ctypes.byref(hd), w, h, channels, device), "ric_codec_create")
+        self.h = hd
+        self.w, self.hgt, self.channels = w, h, channels
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.ric_codec_destroy(self.h)
+            self.h = None
+
+    def set_stream(self, stream_ptr):
+        _chk(lib().ric_codec_set_stream(self.h, stream_ptr), "set_stream")
+
+    def compress(self, pix, q=9, trans=None, on_device=None):
+        """pix: (channels, h, w) uint8 numpy array or device pointer/tensor.
+        Returns the .ric file bytes."""
+        if trans is None:
+            trans = CDF53 if q == 0 else CDF97          # ric -t default (src/ric/ric.cpp:313)
+        dev = on_device if on_device is not None else not isinstance(pix, np.ndarray)
+        if not dev:
+            pix = np.ascontiguousarray(pix, np.uint8)
+        cap = self.w * self.hgt * self.channels * 2 + 65536
+        out = np.empty(cap, np.uint8)
+        n = _S()
+        _chk(lib().ric_codec_encode(self.h, _ptr(pix), int(dev), q, trans, out.ctypes.data, cap, ctypes.byref(n)),
+             "CompressImage")
+        return out[:n.value].tobytes()
+
+    def decompress(self, ric, dither=False, pix_out=None, planes_out=None):
+        """Host mode (default): returns (pix uint8 (c,h,w), planes int16 (c,h,w)).
+        Device mode: pass device pointers/tensors in pix_out / planes_out."""
+        b = np.frombuffer(ric, np.uint8)
+        if pix_out is None and planes_out is None:
+            pix = np.zeros((self.channels, self.hgt, self.w), np.uint8)
+            planes = np.zeros((self.channels, self.hgt, self.w), np.int16)
+            rc = lib().ric_codec_decode(self.h, b.ctypes.data, len(ric), int(dither), pix.ctypes.data,
+                                        planes.ctypes.data, 0)
+            if rc not in (RIC_OK, RIC_E_STREAM):
+                _chk(rc, "DecompressImage")
+            return pix, planes
+        rc = lib().ric_codec_decode(self.h, b.ctypes.data, len(ric), int(dither), _ptr(pix_out),
+                                    _ptr(planes_out), 1)
+        if rc not in (RIC_OK, RIC_E_STREAM):
+            _chk(rc, "DecompressImage")
+        return rc
