@@ -119,6 +119,19 @@ int ric_read_header(const uint8_t* ric, size_t len, int* w, int* h, int* channel
 /* src/ric/ric.cpp:42-49 */
 int ric_quants(int idx);
 
+/* ------------------------------------------------------ instrumentation */
+/* Stage timers (no reference counterpart).  Stage order: 0 forward level 0,
+ * 1 forward all levels, 2 quantiser, 3 bands D2H, 4 host entropy encode,
+ * 5 host entropy decode, 6 bands H2D, 7 dequantiser, 8 inverse all levels,
+ * 9 pixel conversion in, 10 pixel conversion out.  GPU stages are HIP events
+ * on the object's stream; ms are sums, counts the number of samples. */
+#define RIC_PROF_STAGES 11
+int ric_prof_enable(ric_wavelet* w, int on);
+int ric_prof_read(ric_wavelet* w, double* ms, long* counts, int n);
+ric_wavelet* ric_codec_wavelet(ric_codec* c);
+/* SURVEY.md §8(d) synthetic image: channels planes of w*h bytes */
+void ric_synth_image(int w, int h, int channels, int frame, uint8_t* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -7,6 +7,7 @@
 #include <string>
 #include <vector>
 #include <algorithm>
+#include <chrono>
 
 #include "ric_gpu.h"
 #include "ric_types.h"
@@ -46,9 +47,54 @@ void make_thres(bool sh, int* thres, int quant, int lambda)
 	}
 }
 
+// Stage timers (ric_prof_*): GPU stages by hipEvents on the object's stream,
+// host stages by a steady clock.  Harvested at the sync points that already
+// exist (no extra synchronisation in the timed path).
+enum Stage { S_FWD0, S_FWD, S_QUANT, S_D2H, S_HENC, S_HDEC, S_H2D, S_DEQ, S_INV, S_PIXIN, S_PIXOUT, S_COUNT };
+
+struct Prof {
+	bool on = false;
+	hipEvent_t a[S_COUNT] = {}, b[S_COUNT] = {};
+	bool pending[S_COUNT] = {};
+	double ms[S_COUNT] = {};
+	long n[S_COUNT] = {};
+	void enable(bool e)
+	{
+		on = e;
+		if (e && !a[0])
+			for (int i = 0; i < S_COUNT; i++) { (void)hipEventCreate(&a[i]); (void)hipEventCreate(&b[i]); }
+	}
+	void destroy()
+	{
+		if (!a[0]) return;
+		for (int i = 0; i < S_COUNT; i++) { (void)hipEventDestroy(a[i]); (void)hipEventDestroy(b[i]); }
+		a[0] = nullptr;
+	}
+	void begin(int s, hipStream_t st) { if (on && !pending[s]) (void)hipEventRecord(a[s], st); }
+	void end(int s, hipStream_t st) { if (on && !pending[s]) { (void)hipEventRecord(b[s], st); pending[s] = true; } }
+	void harvest()
+	{
+		if (!on) return;
+		for (int i = 0; i < S_COUNT; i++)
+			if (pending[i] && hipEventQuery(b[i]) == hipSuccess) {
+				float t = 0;
+				if (hipEventElapsedTime(&t, a[i], b[i]) == hipSuccess) { ms[i] += t; n[i]++; }
+				pending[i] = false;
+			}
+	}
+	void host(int s, double t_ms) { if (on) { ms[s] += t_ms; n[s]++; } }
+	void reset() { for (int i = 0; i < S_COUNT; i++) { ms[i] = 0; n[i] = 0; } }
+};
+
+double now_ms()
+{
+	return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 }  // namespace
 
 struct ric_wavelet {
+	Prof prof;
 	int device = 0;
 	Pyramid P;
 	char* d_arena = nullptr;
@@ -96,8 +142,11 @@ int to_host(ric_wavelet* w)
 {
 	size_t lo, hi;
 	band_span(w->P, lo, hi);
+	w->prof.begin(S_D2H, w->st);
 	HIPCHK(hipMemcpyAsync(w->h_arena + lo, w->d_arena + lo, hi - lo, hipMemcpyDeviceToHost, w->st));
+	w->prof.end(S_D2H, w->st);
 	HIPCHK(hipStreamSynchronize(w->st));
+	w->prof.harvest();
 	return RIC_OK;
 }
 
@@ -106,9 +155,12 @@ int to_device(ric_wavelet* w)
 	if (!w->host_valid) return RIC_OK;
 	size_t lo, hi;
 	band_span(w->P, lo, hi);
+	w->prof.begin(S_H2D, w->st);
 	HIPCHK(hipMemcpyAsync(w->d_arena + lo, w->h_arena + lo, hi - lo, hipMemcpyHostToDevice, w->st));
+	w->prof.end(S_H2D, w->st);
 	// the host arena is rewritten by the next DecodeBand: wait for the copy
 	HIPCHK(hipStreamSynchronize(w->st));
+	w->prof.harvest();
 	w->host_valid = false;
 	return RIC_OK;
 }
@@ -123,6 +175,7 @@ BandView view(ric_wavelet* w, const Band& B)
 int forward(ric_wavelet* w, const int16_t* dimg, long stride, int trans)
 {
 	Pyramid& P = w->P;
+	w->prof.begin(S_FWD, w->st);
 	for (int l = 0; l < P.nlev; l++) {
 		const void* src;
 		long sp;
@@ -134,8 +187,11 @@ int forward(ric_wavelet* w, const int16_t* dimg, long stride, int trans)
 			const Band& LL = P.L[l - 1].b[BL];
 			src = w->d_arena + LL.off; sp = LL.pitch; vec = 1;
 		}
+		if (l == 0) w->prof.begin(S_FWD0, w->st);
 		launch_fwd_level(P.L[l], src, sp, w->d_arena, trans, vec, w->st);
+		if (l == 0) w->prof.end(S_FWD0, w->st);
 	}
+	w->prof.end(S_FWD, w->st);
 	HIPCHK(hipGetLastError());
 	w->host_valid = false;
 	return RIC_OK;
@@ -146,6 +202,7 @@ int inverse(ric_wavelet* w, int16_t* dimg, long stride, int trans)
 	Pyramid& P = w->P;
 	int rc = to_device(w);
 	if (rc) return rc;
+	w->prof.begin(S_INV, w->st);
 	for (int l = P.nlev - 1; l >= 0; l--) {
 		const Level& L = P.L[l];
 		void* out;
@@ -155,6 +212,7 @@ int inverse(ric_wavelet* w, int16_t* dimg, long stride, int trans)
 		else { const Band& LL = P.L[l - 1].b[BL]; out = w->d_arena + LL.off; po = LL.pitch; out_int = LL.is_int; }
 		launch_inv_level(L, L.b[BL], w->d_arena, out, po, out_int, trans, w->st);
 	}
+	w->prof.end(S_INV, w->st);
 	HIPCHK(hipGetLastError());
 	return RIC_OK;
 }
@@ -165,6 +223,7 @@ int code_band(ric_wavelet* w, Mux& m, int quant, int lambda)
 	Pyramid& P = w->P;
 	// buildTree on every level, finest first (bandcodec.cpp:239-319)
 	int qin = quant;
+	w->prof.begin(S_QUANT, w->st);
 	for (int l = 0; l < P.nlev; l++) {
 		const bool sh = !P.L[l].is_int;
 		qin = tr_any(sh, qin);
@@ -189,10 +248,12 @@ int code_band(ric_wavelet* w, Mux& m, int quant, int lambda)
 		int T0 = tr_any(!B.is_int, (int)(0.5f * (float)Q));
 		launch_quant_ll(P, Q, iQ, T0, w->d_arena, w->st);
 	}
+	w->prof.end(S_QUANT, w->st);
 	HIPCHK(hipGetLastError());
 	int rc = to_host(w);
 	if (rc) return rc;
 	// serial part: LL DPCM, then coarse -> fine, V, H, D (wavelet2d.cpp:119-159)
+	const double t0 = now_ms();
 	pred_encode(m, view(w, P.coarsest_ll()));
 	for (int l = P.nlev - 1; l >= 0; l--) {
 		const int order[3] = {BV, BH, BD};
@@ -203,6 +264,7 @@ int code_band(ric_wavelet* w, Mux& m, int quant, int lambda)
 			tree_encode(m, view(w, B), par, l == 0, l > 0);
 		}
 	}
+	w->prof.host(S_HENC, now_ms() - t0);
 	w->host_valid = true;   // the bands now hold the encoder's final state
 	return RIC_OK;
 }
@@ -212,6 +274,7 @@ int decode_band(ric_wavelet* w, Mux& m)
 {
 	Pyramid& P = w->P;
 	// every band is overwritten: pred writes the LL, tree() Clear()s its band first
+	const double t0 = now_ms();
 	BandView ll = view(w, P.coarsest_ll());
 	pred_decode(m, ll);
 	for (int l = P.nlev - 1; l >= 0; l--) {
@@ -222,6 +285,7 @@ int decode_band(ric_wavelet* w, Mux& m)
 			tree_decode(m, view(w, P.L[l].b[order[k]]), par, l == 0, l > 0);
 		}
 	}
+	w->prof.host(S_HDEC, now_ms() - t0);
 	w->host_valid = true;
 	return m.overflow() ? RIC_E_STREAM : RIC_OK;
 }
@@ -232,6 +296,7 @@ int tsuqi(ric_wavelet* w, int quant)
 	int rc = to_device(w);
 	if (rc) return rc;
 	Pyramid& P = w->P;
+	w->prof.begin(S_DEQ, w->st);
 	for (int i = 0; i < P.nbands(); i++) {
 		const Band& B = P.band(i);
 		const bool sh = !B.is_int;
@@ -240,6 +305,7 @@ int tsuqi(ric_wavelet* w, int quant)
 		if (q == 0) q = 1;
 		launch_dequant_band(B, q, w->d_arena, w->st);
 	}
+	w->prof.end(S_DEQ, w->st);
 	HIPCHK(hipGetLastError());
 	return RIC_OK;
 }
@@ -297,6 +363,7 @@ void ric_wavelet_destroy(ric_wavelet* w)
 	if (!w) return;
 	(void)hipSetDevice(w->device);
 	if (w->st) (void)hipStreamSynchronize(w->st);
+	w->prof.destroy();
 	if (w->d_arena) (void)hipFree(w->d_arena);
 	if (w->d_img) (void)hipFree(w->d_img);
 	if (w->h_arena) (void)hipHostFree(w->h_arena);
@@ -534,7 +601,9 @@ int ric_codec_encode(ric_codec* c, const uint8_t* pix, int on_device, int q, int
 		HIPCHK(hipMemcpyAsync(c->d_pix, pix, npix, hipMemcpyHostToDevice, w->st));
 		dpix = c->d_pix;
 	}
+	w->prof.begin(S_PIXIN, w->st);
 	launch_pix_in(dpix, c->d_planes, c->w, c->h, c->pitch, c->channels, q, w->st);
+	w->prof.end(S_PIXIN, w->st);
 	HIPCHK(hipGetLastError());
 	Mux m;
 	m.init_encoder(c->stream.data(), c->stream.size(), 0);
@@ -627,14 +696,60 @@ int ric_codec_decode(ric_codec* c, const uint8_t* ric, size_t len, int dither,
 	}
 	uint8_t* dpix = on_device ? pix_out : (pix_out ? c->d_pix : nullptr);
 	int16_t* dpl = on_device ? planes_out : (planes_out ? c->d_out : nullptr);
+	w->prof.begin(S_PIXOUT, w->st);
 	launch_pix_out(c->d_planes, c->pitch, c->w, c->h, c->channels, q, dpix, dpl, w->st);
+	w->prof.end(S_PIXOUT, w->st);
 	HIPCHK(hipGetLastError());
 	if (!on_device) {
 		if (pix_out) HIPCHK(hipMemcpyAsync(pix_out, c->d_pix, npix, hipMemcpyDeviceToHost, w->st));
 		if (planes_out) HIPCHK(hipMemcpyAsync(planes_out, c->d_out, npix * 2, hipMemcpyDeviceToHost, w->st));
 	}
 	HIPCHK(hipStreamSynchronize(w->st));
+	w->prof.harvest();
 	return m.overflow() ? RIC_E_STREAM : RIC_OK;
+}
+
+int ric_prof_enable(ric_wavelet* w, int on)
+{
+	if (!w) return RIC_E_ARG;
+	if (set_dev(w->device)) return RIC_E_HIP;
+	w->prof.enable(on != 0);
+	w->prof.reset();
+	return RIC_OK;
+}
+
+int ric_prof_read(ric_wavelet* w, double* ms, long* counts, int n)
+{
+	if (!w || !ms || !counts) return RIC_E_ARG;
+	if (set_dev(w->device)) return RIC_E_HIP;
+	HIPCHK(hipStreamSynchronize(w->st));
+	w->prof.harvest();
+	for (int i = 0; i < n && i < S_COUNT; i++) { ms[i] = w->prof.ms[i]; counts[i] = w->prof.n[i]; }
+	return S_COUNT;
+}
+
+ric_wavelet* ric_codec_wavelet(ric_codec* c) { return c ? c->wav : nullptr; }
+
+// SURVEY.md §8(d) synthetic generator (integer-only, bit-reproducible)
+void ric_synth_image(int w, int h, int channels, int frame, uint8_t* out)
+{
+	for (int c = 0; c < channels; c++) {
+		uint32_t s = 0x9E3779B9u + 0x1000u * (uint32_t)frame + (uint32_t)c;
+		const int phase = 32 * c;
+		uint8_t* o = out + (size_t)c * w * h;
+		for (int y = 0; y < h; y++) {
+			const int gy = (y * 255) / (h - 1);
+			for (int x = 0; x < w; x++) {
+				s ^= s << 13; s ^= s >> 17; s ^= s << 5;
+				const int noise = (int)(s >> 28) - 8;
+				const int grad = ((x * 255) / (w - 1) + gy) >> 2;
+				int t = (x + 2 * y + phase) & 127;
+				t = t < 64 ? t : 127 - t;
+				const int v = grad + t + noise + 32;
+				*o++ = (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v);
+			}
+		}
+	}
 }
 
 }  // extern "C"
