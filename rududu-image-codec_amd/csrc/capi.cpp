@@ -127,21 +127,10 @@ namespace {
 
 int set_dev(int device) { return hip_fail(hipSetDevice(device), "hipSetDevice") ? RIC_E_HIP : RIC_OK; }
 
-// bands region [first band, end of the coarsest LL] in the arena
-void band_span(const Pyramid& P, size_t& lo, size_t& hi)
+// region A (+ B with records): see Pyramid in ric_types.h
+int to_host(ric_wavelet* w, bool records = false)
 {
-	lo = (size_t)-1; hi = 0;
-	for (int i = 0; i < P.nbands(); i++) {
-		const Band& B = const_cast<Pyramid&>(P).band(i);
-		lo = std::min(lo, B.off);
-		hi = std::max(hi, B.off + B.bytes());
-	}
-}
-
-int to_host(ric_wavelet* w)
-{
-	size_t lo, hi;
-	band_span(w->P, lo, hi);
+	const size_t lo = 0, hi = records ? w->P.b_end : w->P.a_end;
 	w->prof.begin(S_D2H, w->st);
 	HIPCHK(hipMemcpyAsync(w->h_arena + lo, w->d_arena + lo, hi - lo, hipMemcpyDeviceToHost, w->st));
 	w->prof.end(S_D2H, w->st);
@@ -153,8 +142,7 @@ int to_host(ric_wavelet* w)
 int to_device(ric_wavelet* w)
 {
 	if (!w->host_valid) return RIC_OK;
-	size_t lo, hi;
-	band_span(w->P, lo, hi);
+	const size_t lo = 0, hi = w->P.a_end;
 	w->prof.begin(S_H2D, w->st);
 	HIPCHK(hipMemcpyAsync(w->d_arena + lo, w->h_arena + lo, hi - lo, hipMemcpyHostToDevice, w->st));
 	w->prof.end(S_H2D, w->st);
@@ -248,9 +236,11 @@ int code_band(ric_wavelet* w, Mux& m, int quant, int lambda)
 		int T0 = tr_any(!B.is_int, (int)(0.5f * (float)Q));
 		launch_quant_ll(P, Q, iQ, T0, w->d_arena, w->st);
 	}
+	// zerotree symbolisation of every level (parents must be quantised first)
+	for (int l = 0; l < P.nlev; l++) launch_blocks_level(P, l, w->d_arena, w->st);
 	w->prof.end(S_QUANT, w->st);
 	HIPCHK(hipGetLastError());
-	int rc = to_host(w);
+	int rc = to_host(w, true);
 	if (rc) return rc;
 	// serial part: LL DPCM, then coarse -> fine, V, H, D (wavelet2d.cpp:119-159)
 	const double t0 = now_ms();
@@ -259,9 +249,8 @@ int code_band(ric_wavelet* w, Mux& m, int quant, int lambda)
 		const int order[3] = {BV, BH, BD};
 		for (int k = 0; k < 3; k++) {
 			const Band& B = P.L[l].b[order[k]];
-			BandView par;
-			if (l + 1 < P.nlev) par = view(w, P.L[l + 1].b[order[k]]);
-			tree_encode(m, view(w, B), par, l == 0, l > 0);
+			const uint64_t* rec = (const uint64_t*)(w->h_arena + P.rec_off[l][order[k]]);
+			tree_encode_records(m, rec, view(w, B), l == 0);
 		}
 	}
 	w->prof.host(S_HENC, now_ms() - t0);

@@ -1,5 +1,6 @@
 // entropy.cpp -- host serial coder of the .ric path (see entropy.h).
 #include "entropy.h"
+#include "symbols.h"
 
 #include <cstdlib>
 #include <algorithm>
@@ -99,6 +100,7 @@ void Mux::init_encoder(uint8_t* buf, size_t cap, uint16_t first_word)
 	low_ = (uint32_t)first_word << 16;
 	range_ = 1u << 16;
 	outcount_ = 0; nbits_ = 0; buffer_ = 0; reserved_ = nullptr; overflow_ = cap < 4;
+	ebuf_ = 0; ebits_ = 0;
 	p_ = buf + 4; init_ = buf + 2;
 	for (int i = 0; i < 4; i++) last_[i] = buf + i;
 }
@@ -144,23 +146,23 @@ void Mux::normalize_dec()                  // src/lib/muxcodec.cpp:76-85
 
 void Mux::empty_buffer()                   // src/lib/muxcodec.cpp:536-548
 {
-	do {
-		nbits_ -= 8;
-		uint8_t b = (uint8_t)(buffer_ >> nbits_);
+	while (ebits_ >= 8) {
+		ebits_ -= 8;
+		uint8_t b = (uint8_t)(ebuf_ >> ebits_);
 		if (!reserved_) put(p_++, b);
 		else { put(reserved_, b); reserved_ = nullptr; }
-	} while (nbits_ >= 8);
+	}
 }
 
 void Mux::flush_buffer(bool end)           // src/lib/muxcodec.cpp:550-570
 {
-	if (nbits_ >= 8) empty_buffer();
-	if (nbits_ > 0) {
+	if (ebits_ >= 8) empty_buffer();
+	if (ebits_ > 0) {
 		if (end) {
-			uint8_t b = (uint8_t)(buffer_ << (8 - nbits_));
+			uint8_t b = (uint8_t)(ebuf_ << (8 - ebits_));
 			if (!reserved_) put(p_++, b);
 			else { put(reserved_, b); reserved_ = nullptr; }
-			nbits_ = 0;
+			ebits_ = 0;
 		} else if (!reserved_) {
 			reserved_ = p_++;
 		}
@@ -373,6 +375,20 @@ inline void GeomModel::code(Mux& m, uint32_t sym, int c)  // geomcodec.h:41-57
 	}
 	m.code_bin(f, 0);
 	if (k > 0) m.bits_code(sym & ((1u << k) - 1), k);
+	freq[c] += (4096 - freq[c]) >> (3 + s);
+	if ((uint16_t)(freq[c] - kGeoThres[s - 1]) > kGeoThres[s] - kGeoThres[s - 1]) adj(c);
+}
+
+inline void GeomModel::code_signed(Mux& m, uint32_t sym, uint32_t sign, int c)
+{
+	const uint32_t k = kGeoK[idx[c]], f = freq[c];
+	const int s = kGeoShift[idx[c]];
+	for (uint32_t l = sym >> k; l > 0; l--) {
+		m.code_bin(f, 1);
+		freq[c] -= freq[c] >> (3 + s);
+	}
+	m.code_bin(f, 0);
+	m.bits_code(((sym & ((1u << k) - 1)) << 1) | sign, k + 1);
 	freq[c] += (4096 - freq[c]) >> (3 + s);
 	if ((uint16_t)(freq[c] - kGeoThres[s - 1]) > kGeoThres[s] - kGeoThres[s - 1]) adj(c);
 }
@@ -635,7 +651,72 @@ void tree_dispatch(Mux& m, const BandView& b, const BandView& par, bool high, bo
 	}
 }
 
+// CBandCodec::tree<encode> over the GPU block records (symbols.h).  Only the
+// adaptive state and the coder run here: tree/border bins, the Huffman table
+// choice from k_mean, the geometric codes of the coefficients.
+template <typename C, bool HIGH>
+void tree_rec_t(Mux& m, const uint64_t* rec, const BandView& b)
+{
+	constexpr bool SH = is_short<C>();
+	static const uint8_t ginit[16] = {5,9,9,9,9,9,9,9,9,9,9,9,10,10,10,11};   // bandcodec.cpp:487
+	uint16_t kmean[16] = {2 << 10, 3 << 10, 4 << 10, 5 << 10, 8 << 10, 11 << 10, 13 << 10, 14 << 10,
+	                      15 << 10, 15 << 10, 15 << 10, 15 << 10, 15 << 10, 15 << 10, 15 << 10, 15 << 10};
+	GeomModel g; g.init(ginit);
+	BitModel tree, bord; tree.init(); bord.init();
+	const C* band = (const C*)b.p;
+	const long st = b.pitch;
+	const int bw = (b.dx + 3) >> 2, bh = (b.dy + 3) >> 2, nfx = b.dx >> 2;
+	long s = 0;
+	for (int by = 0; by < bh; by++) {
+		const C* row = band + (long)by * 4 * st;
+		for (int p = 0; p < bw; p++, s++) {
+			const uint64_t r = rec[s];
+			if (BlockRec::prop(r)) continue;
+			const int bx = !(by & 1) ? p : (nfx < bw ? (p == 0 ? nfx : nfx - p) : nfx - 1 - p);
+			const C* blk = row + bx * 4;
+			const uint32_t ins = BlockRec::insig(r);
+			uint32_t mask = BlockRec::mask(r);
+			if (BlockRec::edge(r)) {
+				bord.code(m, ins, 0);
+				if (ins) continue;
+				m.bits_code(BlockRec::raw(r), BlockRec::rawlen(r));
+				const int w = BlockRec::w(r), gc = BlockRec::gctx(r);
+				while (mask) {
+					const int i = __builtin_ctz(mask);
+					mask &= mask - 1;
+					const int v = blk[(i / w) * st + (i % w)];
+					g.code_signed(m, (uc<SH>(v) >> 1) - 1, v & 1, gc);
+				}
+			} else {
+				const int ctx = BlockRec::ctx(r);
+				tree.code(m, ins, ctx);
+				if (ins) continue;
+				const uint32_t k = BlockRec::k(r);
+				const int idx = (kmean[ctx] + (1 << 9)) >> 10;
+				const uint16_t e = HIGH ? kHuff_HIGH[idx][k - 1] : kHuff_LOW[idx][k];
+				const uint32_t rl = BlockRec::rawlen(r);
+				m.bits_code(((uint32_t)(e >> 5) << rl) | BlockRec::raw(r), (e & 31) + rl);
+				const int gc = (int)k - 1;
+				while (mask) {
+					const int i = __builtin_ctz(mask);
+					mask &= mask - 1;
+					const int v = blk[(i >> 2) * st + (i & 3)];
+					g.code_signed(m, (uc<SH>(v) >> 1) - 1, v & 1, gc);
+				}
+				const uint32_t kk = k - (HIGH ? 1 : 0);
+				kmean[ctx] = (uint16_t)(kmean[ctx] + (kk << 7) - (kmean[ctx] >> 3));
+			}
+		}
+	}
+}
+
 }  // namespace
+
+void tree_encode_records(Mux& m, const uint64_t* rec, const BandView& b, bool high)
+{
+	if (b.is_int) { if (high) tree_rec_t<int32_t, true>(m, rec, b); else tree_rec_t<int32_t, false>(m, rec, b); }
+	else { if (high) tree_rec_t<int16_t, true>(m, rec, b); else tree_rec_t<int16_t, false>(m, rec, b); }
+}
 
 void pred_encode(Mux& m, const BandView& b)
 {

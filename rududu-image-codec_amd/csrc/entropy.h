@@ -46,11 +46,15 @@ public:
 		range_ = t + ((range_ - 2 * t) & tst);
 		return 0u - tst;
 	}
-	inline void bits_code(uint32_t bits, uint32_t len)    // bitsCode, muxcodec.h:225-231
+	// bitsCode, muxcodec.h:225-231.  The encoder keeps a 64-bit FIFO: between
+	// two range-coder normalisations only the order of the bits matters, and
+	// every normalisation first writes all complete bytes (flushBuffer<false>),
+	// so batching the byte writes does not move any byte.  len <= 56.
+	inline void bits_code(uint32_t bits, uint32_t len)
 	{
-		if (nbits_ + len > 32) empty_buffer();
-		buffer_ = (buffer_ << len) | bits;
-		nbits_ += len;
+		if (ebits_ + len > 64) empty_buffer();
+		ebuf_ = (ebuf_ << len) | bits;
+		ebits_ += len;
 	}
 	inline uint32_t bits_decode(uint32_t len)             // bitsDecode, muxcodec.h:233-239
 	{
@@ -80,6 +84,8 @@ private:
 	uint8_t *last_[4] = {nullptr, nullptr, nullptr, nullptr}, *reserved_ = nullptr;
 	uint8_t* owned_ = nullptr;              // decoder copy
 	uint32_t range_ = 0, low_ = 0, code_ = 0, outcount_ = 0, nbits_ = 0, buffer_ = 0;
+	uint64_t ebuf_ = 0;                     // encoder raw-bit FIFO
+	uint32_t ebits_ = 0;
 	bool overflow_ = false;
 };
 
@@ -100,6 +106,8 @@ struct GeomModel {                          // CGeomCodec (16 contexts)
 	inline void adj(int c);
 	inline void code(Mux& m, uint32_t sym, int c);
 	inline uint32_t decode(Mux& m, int c);
+	// code sym then one raw sign bit, the remainder and the sign as one chunk
+	inline void code_signed(Mux& m, uint32_t sym, uint32_t sign, int c);
 };
 
 // --------------------------------------------------------- band scans
@@ -115,5 +123,7 @@ void pred_decode(Mux& m, const BandView& b);
 // CBandCodec::tree, src/lib/bandcodec.cpp:484-589.  par.p == nullptr: no parent.
 void tree_encode(Mux& m, const BandView& b, const BandView& par, bool high, bool has_child);
 void tree_decode(Mux& m, const BandView& b, const BandView& par, bool high, bool has_child);
+// Encoder over GPU block records (symbols.h): rec[s] for scan position s.
+void tree_encode_records(Mux& m, const uint64_t* rec, const BandView& b, bool high);
 
 }  // namespace ric

@@ -24,6 +24,9 @@ struct QuantParams {
 void launch_quant_level(const Pyramid& P, int l, const QuantParams& qp, char* arena, hipStream_t st);
 // CBand::TSUQ on the coarsest LL (src/lib/band.h:65-92).
 void launch_quant_ll(const Pyramid& P, int Q, int iQ, int T, char* arena, hipStream_t st);
+// Zerotree block records of the D/H/V bands of level l (symbols.h), written
+// at P.rec_off[l][b]; needs every level quantised (parents are read).
+void launch_blocks_level(const Pyramid& P, int l, char* arena, hipStream_t st);
 // CBand::TSUQi on one band (src/lib/band.h:94-107).
 void launch_dequant_band(const Band& B, int q, char* arena, hipStream_t st);
 

@@ -62,26 +62,29 @@ struct Level {
 };
 
 // CWavelet2D::Init geometry (src/lib/wavelet2d.cpp:69-81, src/lib/band.cpp:51-65).
+// Arena layout (one allocation on the device, a pinned mirror on the host):
+//   region A [0, a_end):     the coded bands (D/H/V of every level + coarsest LL)
+//   region B [a_end, b_end): per-block zerotree records of the 3*nlev high bands
+//   region C [b_end, end):   device-only scratch: intermediate LL planes, pRD
+// Encode copies A+B to the host, decode copies A back to the device.
 struct Pyramid {
 	int nlev = 0;
 	int w = 0, h = 0, levels = 0, lc = 0;
 	Level L[kMaxLevels];
-	size_t arena_bytes = 0;
+	size_t arena_bytes = 0, a_end = 0, b_end = 0;
+	size_t rec_off[kMaxLevels][3] = {};
 
 	void build(int w_, int h_, int levels_, int lc_)
 	{
 		w = w_; h = h_; levels = levels_; lc = lc_;
 		nlev = 0;
 		int lw = w, lh = h, lev = levels;
-		size_t off = 0;
-		auto place = [&](Band& B, int dx, int dy, int is_int) {
+		auto dims = [](Band& B, int dx, int dy, int is_int) {
 			B.dx = dx; B.dy = dy; B.is_int = is_int;
 			B.pitch = ((dx + 63) / 64) * 64;
 			if (B.pitch == 0) B.pitch = 64;
 			int ss = is_int ? 4 : 2;
 			B.ref_align = ((dx * ss + 31) & -32) / ss;
-			B.off = off; off += ((B.bytes() + 255) / 256) * 256 + 256;
-			B.rd_off = off; off += (((size_t)B.bw() * B.bh() * 4 + 255) / 256) * 256 + 256;
 		};
 		int prev_int = 0;
 		while (true) {
@@ -89,15 +92,27 @@ struct Pyramid {
 			Lv.w = lw; Lv.h = lh;
 			Lv.is_int = lev <= lc;
 			Lv.in_is_int = nlev == 0 ? Lv.is_int : prev_int;
-			place(Lv.b[BD], (lw + 1) >> 1, (lh + 1) >> 1, Lv.is_int);
-			place(Lv.b[BH], lw >> 1, (lh + 1) >> 1, Lv.is_int);
-			place(Lv.b[BV], (lw + 1) >> 1, lh >> 1, Lv.is_int);
-			place(Lv.b[BL], lw >> 1, lh >> 1, Lv.is_int);
+			dims(Lv.b[BD], (lw + 1) >> 1, (lh + 1) >> 1, Lv.is_int);
+			dims(Lv.b[BH], lw >> 1, (lh + 1) >> 1, Lv.is_int);
+			dims(Lv.b[BV], (lw + 1) >> 1, lh >> 1, Lv.is_int);
+			dims(Lv.b[BL], lw >> 1, lh >> 1, Lv.is_int);
 			prev_int = Lv.is_int;
 			nlev++;
 			if (!(lev > 1 && lw > 15 && lh > 15) || nlev == kMaxLevels) break;
 			lw >>= 1; lh >>= 1; lev--;
 		}
+		size_t off = 0;
+		auto take = [&](size_t bytes) { size_t o = off; off += (bytes + 255) / 256 * 256; return o; };
+		for (int l = 0; l < nlev; l++)
+			for (int b = 0; b < 3; b++) L[l].b[b].off = take(L[l].b[b].bytes());
+		L[nlev - 1].b[BL].off = take(L[nlev - 1].b[BL].bytes());
+		a_end = off;
+		for (int l = 0; l < nlev; l++)
+			for (int b = 0; b < 3; b++) rec_off[l][b] = take((size_t)L[l].b[b].bw() * L[l].b[b].bh() * 8);
+		b_end = off;
+		for (int l = 0; l + 1 < nlev; l++) L[l].b[BL].off = take(L[l].b[BL].bytes());
+		for (int l = 0; l < nlev; l++)
+			for (int b = 0; b < 4; b++) L[l].b[b].rd_off = take((size_t)L[l].b[b].bw() * L[l].b[b].bh() * 4);
 		arena_bytes = off;
 	}
 

@@ -8,6 +8,7 @@
 #include <chrono>
 #include "ric_types.h"
 #include "entropy.h"
+#include "symbols.h"
 
 using namespace ric;
 
@@ -54,6 +55,42 @@ struct HostPyr {
 			}
 		}
 	}
+	// block records computed on the CPU with the same function the GPU runs
+	std::vector<std::vector<uint64_t>> recs;
+	void build_records() {
+		const SymTables& T = host_sym_tables();
+		recs.assign(3 * P.nlev, {});
+		for (int l = 0; l < P.nlev; l++)
+			for (int b = 0; b < 3; b++) {
+				Band& B = P.L[l].b[b];
+				std::vector<uint64_t>& R = recs[3 * l + b];
+				R.resize((size_t)B.bw() * B.bh());
+				const bool hp = l + 1 < P.nlev;
+				Band* Q = hp ? &P.L[l + 1].b[b] : nullptr;
+				for (size_t s = 0; s < R.size(); s++) {
+					int bx, by;
+					scan_block((int)s, B.dx, B.dy, bx, by);
+					const char* bp = arena.data() + B.off;
+					const char* pp = hp ? arena.data() + Q->off : nullptr;
+					const int pst = hp ? Q->pitch : 0, pdx = hp ? Q->dx : 0, pdy = hp ? Q->dy : 0;
+					const bool pint = hp ? Q->is_int : B.is_int;
+					if (!B.is_int && !pint)
+						R[s] = block_record<int16_t, int16_t>(T, (const int16_t*)bp, B.pitch, B.dx, B.dy, (const int16_t*)pp, pst, pdx, pdy, l == 0, bx, by);
+					else if (!B.is_int)
+						R[s] = block_record<int16_t, int32_t>(T, (const int16_t*)bp, B.pitch, B.dx, B.dy, (const int32_t*)pp, pst, pdx, pdy, l == 0, bx, by);
+					else
+						R[s] = block_record<int32_t, int32_t>(T, (const int32_t*)bp, B.pitch, B.dx, B.dy, (const int32_t*)pp, pst, pdx, pdy, l == 0, bx, by);
+				}
+			}
+	}
+	void encode_rec(Mux& m) {
+		pred_encode(m, view(P.coarsest_ll()));
+		for (int l = P.nlev - 1; l >= 0; l--) {
+			const int order[3] = {BV, BH, BD};
+			for (int k = 0; k < 3; k++)
+				tree_encode_records(m, recs[3 * l + order[k]].data(), view(P.L[l].b[order[k]]), l == 0);
+		}
+	}
 	void decode(Mux& m) {
 		pred_decode(m, view(P.coarsest_ll()));
 		for (int l = P.nlev - 1; l >= 0; l--) {
@@ -70,6 +107,29 @@ double now() { return std::chrono::duration<double>(std::chrono::steady_clock::n
 }  // namespace
 
 extern "C" {
+// as hc_encode, but through the block-record encoder (records built on the CPU)
+long hc_encode_rec(const int32_t* bands, long per_plane, int nplanes, int w, int h, int levels, int lc,
+                   uint8_t* out, long cap, double* secs, double* rec_secs)
+{
+	HostPyr hp(w, h, levels, lc);
+	Mux m;
+	m.init_encoder(out, cap, 0);
+	double t = 0, tr = 0;
+	for (int p = 0; p < nplanes; p++) {
+		hp.load(bands + p * per_plane);
+		double t0 = now();
+		hp.build_records();
+		double t1 = now();
+		hp.encode_rec(m);
+		tr += t1 - t0;
+		t += now() - t1;
+	}
+	uint8_t* e = m.end_coding();
+	if (secs) *secs = t;
+	if (rec_secs) *rec_secs = tr;
+	return m.overflow() ? -1 : (long)(e - out);
+}
+
 // bands: nplanes x (canonical stage-1 dump).  Returns the coder buffer length.
 long hc_encode(const int32_t* bands, long per_plane, int nplanes, int w, int h, int levels, int lc,
                uint8_t* out, long cap, double* secs)
