@@ -271,7 +271,7 @@ int decode_band(ric_wavelet* w, Mux& m)
 		for (int k = 0; k < 3; k++) {
 			BandView par;
 			if (l + 1 < P.nlev) par = view(w, P.L[l + 1].b[order[k]]);
-			tree_decode(m, view(w, P.L[l].b[order[k]]), par, l == 0, l > 0);
+			tree_decode_fast(m, view(w, P.L[l].b[order[k]]), par, l == 0, l > 0);
 		}
 	}
 	w->prof.host(S_HDEC, now_ms() - t0);

@@ -72,6 +72,20 @@ public:
 	void max_code(uint32_t value, uint32_t max);                // muxcodec.cpp:516-524
 	uint32_t max_decode(uint32_t max);                          // muxcodec.cpp:526-534
 
+	// decoder state, copied into registers by the band decoder (decoder.cpp)
+	struct DecState {
+		uint32_t range, low, code, nbits, buffer;
+		const uint8_t* p;
+		const uint8_t* limit;
+		bool ovf;
+	};
+	DecState dec_state() const { return {range_, low_, code_, nbits_, buffer_, p_, limit_, overflow_}; }
+	void set_dec_state(const DecState& d)
+	{
+		range_ = d.range; low_ = d.low; code_ = d.code; nbits_ = d.nbits; buffer_ = d.buffer;
+		p_ = const_cast<uint8_t*>(d.p); overflow_ = d.ovf;
+	}
+
 private:
 	void normalize_enc();
 	void normalize_dec();
@@ -123,6 +137,9 @@ void pred_decode(Mux& m, const BandView& b);
 // CBandCodec::tree, src/lib/bandcodec.cpp:484-589.  par.p == nullptr: no parent.
 void tree_encode(Mux& m, const BandView& b, const BandView& par, bool high, bool has_child);
 void tree_decode(Mux& m, const BandView& b, const BandView& par, bool high, bool has_child);
+// Register-resident decoder of one band (decoder.cpp), same semantics as
+// tree_decode.
+void tree_decode_fast(Mux& m, const BandView& b, const BandView& par, bool high, bool has_child);
 // Encoder over GPU block records (symbols.h): rec[s] for scan position s.
 void tree_encode_records(Mux& m, const uint64_t* rec, const BandView& b, bool high);
 

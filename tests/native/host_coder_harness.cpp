@@ -98,7 +98,7 @@ struct HostPyr {
 			for (int k = 0; k < 3; k++) {
 				BandView par;
 				if (l + 1 < P.nlev) par = view(P.L[l + 1].b[order[k]]);
-				tree_decode(m, view(P.L[l].b[order[k]]), par, l == 0, l > 0);
+				tree_decode_fast(m, view(P.L[l].b[order[k]]), par, l == 0, l > 0);
 			}
 		}
 	}
