@@ -302,7 +302,7 @@ static void pyr_inverse(pyr_t* p, int trans, int32_t* out)
 /* ------------------------------------------------------------------ mux */
 /* CMuxCodec, src/lib/muxcodec.h:66-277, src/lib/muxcodec.cpp */
 typedef struct {
-	uint8_t *p, *init, *last[4], *reserved;
+	uint8_t *p, *init, *last[4], *reserved, *end;   /* end: decoder read guard */
 	uint32_t range, low, code, outcount, nbits, buffer;
 	uint32_t nbtaboo[32], sumtaboo[32], ntaboo;
 } mux_t;
@@ -337,7 +337,17 @@ static void mux_dec_init(mux_t* m, uint8_t* buf)     /* initDecoder, muxcodec.cp
 	m->init = buf + 2; m->p = buf + 2;
 	m->code = m->low = (m->p[0] << 8) | m->p[1];
 	m->p += 2;
+	m->end = NULL;
 	mux_taboo(m, 2);
+}
+
+/* Decoder read guard: a desynchronised stream (the reference's maxDecode(0)
+ * case, muxcodec.cpp:526-534) can walk off the buffer; valid streams never get
+ * close.  The reference has no guard (it may crash there). */
+static inline uint8_t next_byte(mux_t* m)
+{
+	if (m->end && m->p >= m->end) return 0;
+	return *m->p++;
 }
 
 static void mux_empty(mux_t* m)                      /* emptyBuffer, muxcodec.cpp:536-548 */
@@ -381,9 +391,9 @@ static void mux_norm_dec(mux_t* m)                   /* normalize_dec, muxcodec.
 	do {
 		if (((m->code - m->low + m->range - 1) ^ (m->code - m->low)) >= 0x01000000u)
 			m->range = (m->low - m->code) & 4095u;
-		m->low = (m->low << 8) | *m->p;
-		m->code = (m->code << 8) | *m->p;
-		m->p++;
+		uint8_t b = next_byte(m);
+		m->low = (m->low << 8) | b;
+		m->code = (m->code << 8) | b;
 		m->range <<= 8;
 	} while (m->range <= 4096u);
 }
@@ -429,15 +439,16 @@ static inline void bits_code(mux_t* m, uint32_t bits, uint32_t len)  /* bitsCode
 
 static void mux_fill(mux_t* m, uint32_t len)                    /* fillBuffer, muxcodec.cpp:572-579 */
 {
+	if (len > 32) len = 32;
 	do {
 		m->nbits += 8;
-		m->buffer = (m->buffer << 8) | m->p[0];
-		m->p++;
+		m->buffer = (m->buffer << 8) | next_byte(m);
 	} while (m->nbits < len);
 }
 
 static inline uint32_t bits_decode(mux_t* m, uint32_t len)     /* bitsDecode, muxcodec.h:233-239 */
 {
+	if (len > 24) len = 24;                           /* desync guard only */
 	if (m->nbits < len) mux_fill(m, len);
 	m->nbits -= len;
 	return (m->buffer >> m->nbits) & ((1u << len) - 1);
@@ -532,6 +543,7 @@ static void enum_code(mux_t* m, uint32_t bits, uint32_t k, uint32_t nmax)
 
 static uint32_t enum_decode(mux_t* m, uint32_t k, uint32_t nmax)
 {
+	if (k == 0 || k >= nmax) return k ? (1u << nmax) - 1 : 0;   /* desync guard only */
 	int n = nmax - 1;
 	uint32_t bits = 0;
 	if (k > ((nmax + 1) >> 1)) { k = nmax - k; bits ^= (1u << nmax) - 1; }
@@ -540,6 +552,7 @@ static uint32_t enum_decode(mux_t* m, uint32_t k, uint32_t nmax)
 	uint32_t code = bits_decode(m, CNK_LEN[nmax - 1][k - 1] - 1);
 	if (code >= lost) code = ((code << 1) | bits_decode(m, 1)) - lost;
 	do {
+		if (n < 0) break;
 		if (code >= CNK[row][n]) { bits ^= 1u << n; code -= CNK[row][n]; row--; }
 		n--;
 	} while (row >= 0);
@@ -575,6 +588,7 @@ static uint32_t huff_decode(mux_t* m, const uint16_t* tab, int nsym)
 	}
 	if (s == nsym) { s = 0; len = tab[0] & 31; }  /* corrupt stream: any defined behaviour */
 	m->p -= (int)(m->nbits - len) >> 3;
+	if (m->end && m->p > m->end) m->p = m->end;
 	if ((int)m->nbits < len) m->buffer = m->p[-1];
 	m->nbits = (m->nbits - len) & 7;
 	return s;
@@ -662,7 +676,7 @@ static uint32_t geom_decode(geom_t* g, mux_t* m, int c)
 	uint32_t k = GEO_K[g->idx[c]], f = g->freq[c];
 	int s = GEO_SHIFT[g->idx[c]];
 	uint32_t l = 0;
-	while (get_bit(m, f)) { g->freq[c] -= g->freq[c] >> (3 + s); l++; }
+	while (get_bit(m, f)) { g->freq[c] -= g->freq[c] >> (3 + s); if (++l > (1u << 20)) break; }
 	if (k > 0) l = (l << k) | bits_decode(m, k);
 	g->freq[c] += (4096 - g->freq[c]) >> (3 + s);
 	if ((uint16_t)(g->freq[c] - GEO_THRES[s - 1]) > GEO_THRES[s] - GEO_THRES[s - 1]) geom_adj(g, c);
@@ -941,6 +955,7 @@ static void block_edge(int sh, int32_t* blk, int stride, mux_t* m, geom_t* g, in
 		}
 	} else {
 		if (high) k = max_decode(m, cnt - 1) + 1; else k = max_decode(m, cnt);
+		if (k > cnt) k = cnt;                    /* desync guard only */
 		if (high || k != 0) {
 			uint32_t sig = 0xFFFF;
 			if (k != cnt) sig = enum_decode(m, k, cnt);
@@ -1191,9 +1206,11 @@ long ricor_decode_planes(const uint8_t* in, long len, int nplanes, int w, int h,
 {
 	once();
 	size_t n = (size_t)w * h;
-	uint8_t* s = calloc((size_t)(len > 0 ? len : 0) + n * nplanes + 4096, 1);
+	size_t slen = (size_t)(len > 0 ? len : 0) + n * nplanes + 4096;
+	uint8_t* s = calloc(slen, 1);
 	memcpy(s, in, len);
 	mux_t m; mux_dec_init(&m, s);
+	m.end = s + slen - 8;
 	pyr_t p; pyr_init(&p, w, h, levels, lc); pyr_weights(&p, trans);
 	int32_t* x = malloc(sizeof(int32_t) * n);
 	for (int k = 0; k < nplanes; k++) {

@@ -250,7 +250,7 @@ int code_band(ric_wavelet* w, Mux& m, int quant, int lambda)
 		for (int k = 0; k < 3; k++) {
 			const Band& B = P.L[l].b[order[k]];
 			const uint64_t* rec = (const uint64_t*)(w->h_arena + P.rec_off[l][order[k]]);
-			tree_encode_records(m, rec, view(w, B), l == 0);
+			tree_encode_records_fast(m, rec, view(w, B), l == 0);
 		}
 	}
 	w->prof.host(S_HENC, now_ms() - t0);

@@ -1,0 +1,184 @@
+// encoder.cpp -- the serial .ric band encoder over GPU block records, with the
+// range-coder / raw-bit FIFO state held in registers (a local EncCore).
+// Restates CBandCodec::tree<encode> (src/lib/bandcodec.cpp:484-589), CBitCodec
+// / CGeomCodec code (src/lib/bitcodec.h:52-60, geomcodec.h:41-57) and CMuxCodec
+// codeBin / bitsCode / normalize_enc / flushBuffer (src/lib/muxcodec.h:156-231,
+// muxcodec.cpp:63-74, 536-570).  Output is byte-identical to entropy.cpp's
+// tree_encode_records (and to the reference).
+#include "entropy.h"
+#include "symbols.h"
+
+namespace ric {
+
+#include "huff_tables.inc"
+
+namespace {
+
+const uint16_t kBitThresE[11] = {2584, 1512, 745, 371, 185, 92, 46, 23, 12, 6, 3};
+const uint16_t kGeoThresE[11] = {1512, 2584, 3351, 3725, 3911, 4004, 4050, 4073, 4084, 4090, 4093};
+const uint8_t kGeoKE[25] = {0,0,0,0,0,0,0,0,0,0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,14};
+const uint8_t kGeoShiftE[25] = {10,9,8,7,6,5,4,3,2,1,1,1,1,1,1,1,1,1,1,1,1,1,1,1,1};
+
+#define RIC_AI __attribute__((always_inline)) inline
+
+struct EncCore {
+	Mux::EncState s;
+	explicit EncCore(const Mux::EncState& st) : s(st) {}
+
+	RIC_AI void put(uint8_t* slot, uint8_t v) { if (__builtin_expect(slot < s.limit, 1)) *slot = v; else s.ovf = true; }
+	__attribute__((noinline)) void norm()                 // normalize_enc, muxcodec.cpp:63-74
+	{
+		// flushBuffer<false>: every complete raw byte first, then reserve the partial one
+		while (s.ebits >= 8) {
+			s.ebits -= 8;
+			const uint8_t b = (uint8_t)(s.ebuf >> s.ebits);
+			if (!s.reserved) put(s.p++, b); else { put(s.reserved, b); s.reserved = nullptr; }
+		}
+		if (s.ebits > 0 && !s.reserved) s.reserved = s.p++;
+		do {
+			put(s.last[s.outcount++ & 3], (uint8_t)(s.low >> 24));
+			if (((s.low + s.range - 1) ^ s.low) >= 0x01000000u) s.range = (0u - s.low) & 4095u;
+			s.last[(s.outcount + 3) & 3] = s.p++;
+			s.range <<= 8;
+			s.low <<= 8;
+		} while (s.range <= 4096u);
+	}
+	__attribute__((noinline)) void drain()                // emptyBuffer, muxcodec.cpp:536-548
+	{
+		while (s.ebits >= 8) {
+			s.ebits -= 8;
+			const uint8_t b = (uint8_t)(s.ebuf >> s.ebits);
+			if (!s.reserved) put(s.p++, b); else { put(s.reserved, b); s.reserved = nullptr; }
+		}
+	}
+	RIC_AI void bin(uint32_t freq, uint32_t bit)           // codeBin, muxcodec.h:156-163
+	{
+		if (__builtin_expect(s.range <= 4096u, 0)) norm();
+		const uint32_t t = (s.range * freq) >> 12;
+		s.low += t & (0u - bit);
+		s.range = t + ((s.range - 2 * t) & (0u - bit));
+	}
+	RIC_AI void bits(uint32_t v, uint32_t len)             // bitsCode (64-bit FIFO, see entropy.h)
+	{
+		if (__builtin_expect(s.ebits + len > 64, 0)) drain();
+		s.ebuf = (s.ebuf << len) | v;
+		s.ebits += len;
+	}
+};
+
+struct BitE {                                             // CBitCodec::code
+	uint16_t freq[16];
+	uint8_t shift[16], mps[16];
+	BitE() { for (int i = 0; i < 16; i++) { freq[i] = 2048; shift[i] = 0; mps[i] = 0; } }
+	RIC_AI void code(EncCore& e, uint32_t sym, int c)
+	{
+		const uint32_t s = sym ^ mps[c];
+		e.bin(freq[c], s ^ 1);
+		const int sh = shift[c];
+		freq[c] = (uint16_t)(freq[c] + (s << (9 - sh)) - (freq[c] >> (3 + sh)));
+		if ((uint16_t)(freq[c] - kBitThresE[sh + 1]) > kBitThresE[sh] - kBitThresE[sh + 1]) {
+			if (freq[c] > kBitThresE[sh]) {
+				if (sh == 0) { mps[c] ^= 1; freq[c] = (uint16_t)(4096 - freq[c]); shift[c] = 1; }
+				else shift[c]--;
+			} else if (sh < 9) shift[c]++;
+		}
+	}
+};
+
+struct GeoE {                                             // CGeomCodec::code
+	uint16_t freq[16];
+	uint8_t idx[16];
+	explicit GeoE(const uint8_t* kinit)
+	{
+		for (int c = 0; c < 16; c++) {
+			idx[c] = kinit[c];
+			freq[c] = idx[c] >= 9 ? 2048 : (uint16_t)((kGeoThresE[idx[c] - 1] + kGeoThresE[idx[c]]) >> 1);
+		}
+	}
+	// magnitude - 1 then the raw sign bit (remainder and sign as one chunk)
+	RIC_AI void code_signed(EncCore& e, uint32_t sym, uint32_t sign, int c)
+	{
+		const uint32_t k = kGeoKE[idx[c]], f = freq[c];
+		const int s = kGeoShiftE[idx[c]];
+		for (uint32_t l = sym >> k; l > 0; l--) {
+			e.bin(f, 1);
+			freq[c] -= freq[c] >> (3 + s);
+		}
+		e.bin(f, 0);
+		e.bits(((sym & ((1u << k) - 1)) << 1) | sign, k + 1);
+		freq[c] += (4096 - freq[c]) >> (3 + s);
+		if ((uint16_t)(freq[c] - kGeoThresE[s - 1]) > kGeoThresE[s] - kGeoThresE[s - 1]) {
+			if (freq[c] < kGeoThresE[s - 1]) { if (idx[c] < 24) idx[c]++; }
+			else if (idx[c] > 0) idx[c]--;
+			if (idx[c] >= 9) freq[c] = 2048;
+		}
+	}
+};
+
+template <typename C, bool HIGH>
+void tree_rec_fast(Mux& m, const uint64_t* rec, const BandView& b)
+{
+	constexpr bool SH = sizeof(C) == 2;
+	static const uint8_t ginit[16] = {5,9,9,9,9,9,9,9,9,9,9,9,10,10,10,11};   // bandcodec.cpp:487
+	uint16_t kmean[16] = {2 << 10, 3 << 10, 4 << 10, 5 << 10, 8 << 10, 11 << 10, 13 << 10, 14 << 10,
+	                      15 << 10, 15 << 10, 15 << 10, 15 << 10, 15 << 10, 15 << 10, 15 << 10, 15 << 10};
+	EncCore e(m.enc_state());
+	GeoE g(ginit);
+	BitE tree, bord;
+	const C* band = (const C*)b.p;
+	const long st = b.pitch;
+	const int bw = (b.dx + 3) >> 2, bh = (b.dy + 3) >> 2, nfx = b.dx >> 2;
+	long s = 0;
+	for (int by = 0; by < bh; by++) {
+		const C* row = band + (long)by * 4 * st;
+		for (int p = 0; p < bw; p++, s++) {
+			const uint64_t r = rec[s];
+			if (BlockRec::prop(r)) continue;
+			const int bx = !(by & 1) ? p : (nfx < bw ? (p == 0 ? nfx : nfx - p) : nfx - 1 - p);
+			const C* blk = row + bx * 4;
+			const uint32_t ins = BlockRec::insig(r);
+			uint32_t mask = BlockRec::mask(r);
+			if (__builtin_expect(BlockRec::edge(r), 0)) {
+				bord.code(e, ins, 0);
+				if (ins) continue;
+				e.bits(BlockRec::raw(r), BlockRec::rawlen(r));
+				const int w = BlockRec::w(r), gc = BlockRec::gctx(r);
+				while (mask) {
+					const int i = __builtin_ctz(mask);
+					mask &= mask - 1;
+					const int v = blk[(i / w) * st + (i % w)];
+					g.code_signed(e, (uc<SH>(v) >> 1) - 1, v & 1, gc);
+				}
+			} else {
+				const int ctx = BlockRec::ctx(r);
+				tree.code(e, ins, ctx);
+				if (ins) continue;
+				const uint32_t k = BlockRec::k(r);
+				const int idx = (kmean[ctx] + (1 << 9)) >> 10;
+				const uint16_t h = HIGH ? kHuff_HIGH[idx][k - 1] : kHuff_LOW[idx][k];
+				const uint32_t rl = BlockRec::rawlen(r);
+				e.bits(((uint32_t)(h >> 5) << rl) | BlockRec::raw(r), (h & 31) + rl);
+				const int gc = (int)k - 1;
+				while (mask) {
+					const int i = __builtin_ctz(mask);
+					mask &= mask - 1;
+					const int v = blk[(i >> 2) * st + (i & 3)];
+					g.code_signed(e, (uc<SH>(v) >> 1) - 1, v & 1, gc);
+				}
+				const uint32_t kk = k - (HIGH ? 1 : 0);
+				kmean[ctx] = (uint16_t)(kmean[ctx] + (kk << 7) - (kmean[ctx] >> 3));
+			}
+		}
+	}
+	m.set_enc_state(e.s);
+}
+
+}  // namespace
+
+void tree_encode_records_fast(Mux& m, const uint64_t* rec, const BandView& b, bool high)
+{
+	if (b.is_int) { if (high) tree_rec_fast<int32_t, true>(m, rec, b); else tree_rec_fast<int32_t, false>(m, rec, b); }
+	else { if (high) tree_rec_fast<int16_t, true>(m, rec, b); else tree_rec_fast<int16_t, false>(m, rec, b); }
+}
+
+}  // namespace ric

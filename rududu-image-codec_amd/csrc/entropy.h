@@ -80,6 +80,24 @@ public:
 		bool ovf;
 	};
 	DecState dec_state() const { return {range_, low_, code_, nbits_, buffer_, p_, limit_, overflow_}; }
+	// encoder state, copied into registers by the record encoder (encoder.cpp)
+	struct EncState {
+		uint32_t range, low, outcount, ebits;
+		uint64_t ebuf;
+		uint8_t *p, *limit, *reserved;
+		uint8_t* last[4];
+		bool ovf;
+	};
+	EncState enc_state() const
+	{
+		return {range_, low_, outcount_, ebits_, ebuf_, p_, limit_, reserved_, {last_[0], last_[1], last_[2], last_[3]}, overflow_};
+	}
+	void set_enc_state(const EncState& e)
+	{
+		range_ = e.range; low_ = e.low; outcount_ = e.outcount; ebits_ = e.ebits; ebuf_ = e.ebuf;
+		p_ = e.p; reserved_ = e.reserved; overflow_ = e.ovf;
+		for (int i = 0; i < 4; i++) last_[i] = e.last[i];
+	}
 	void set_dec_state(const DecState& d)
 	{
 		range_ = d.range; low_ = d.low; code_ = d.code; nbits_ = d.nbits; buffer_ = d.buffer;
@@ -142,5 +160,7 @@ void tree_decode(Mux& m, const BandView& b, const BandView& par, bool high, bool
 void tree_decode_fast(Mux& m, const BandView& b, const BandView& par, bool high, bool has_child);
 // Encoder over GPU block records (symbols.h): rec[s] for scan position s.
 void tree_encode_records(Mux& m, const uint64_t* rec, const BandView& b, bool high);
+// Same, with the coder state in registers (encoder.cpp).
+void tree_encode_records_fast(Mux& m, const uint64_t* rec, const BandView& b, bool high);
 
 }  // namespace ric

@@ -91,7 +91,7 @@ struct Pyramid {
 			Level& Lv = L[nlev];
 			Lv.w = lw; Lv.h = lh;
 			Lv.is_int = lev <= lc;
-			Lv.in_is_int = nlev == 0 ? Lv.is_int : prev_int;
+			Lv.in_is_int = nlev == 0 ? 0 : prev_int;   // the image is always short (Transform<short>)
 			dims(Lv.b[BD], (lw + 1) >> 1, (lh + 1) >> 1, Lv.is_int);
 			dims(Lv.b[BH], lw >> 1, (lh + 1) >> 1, Lv.is_int);
 			dims(Lv.b[BV], (lw + 1) >> 1, lh >> 1, Lv.is_int);

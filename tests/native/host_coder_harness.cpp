@@ -88,7 +88,7 @@ struct HostPyr {
 		for (int l = P.nlev - 1; l >= 0; l--) {
 			const int order[3] = {BV, BH, BD};
 			for (int k = 0; k < 3; k++)
-				tree_encode_records(m, recs[3 * l + order[k]].data(), view(P.L[l].b[order[k]]), l == 0);
+				tree_encode_records_fast(m, recs[3 * l + order[k]].data(), view(P.L[l].b[order[k]]), l == 0);
 		}
 	}
 	void decode(Mux& m) {

@@ -1,0 +1,56 @@
+"""The clean-room oracle against the reference library compiled in place
+(oracle/_ref).  Skipped where the reference build is absent."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+REF = O.ref()
+pytestmark = pytest.mark.skipif(REF is None, reason="oracle/_ref not built (reference sources absent)")
+
+SIZES = [(8, 8), (16, 16), (17, 23), (33, 47), (64, 48), (100, 101), (129, 77), (255, 130), (1001, 603)]
+
+
+@pytest.mark.parametrize("w,h", SIZES)
+@pytest.mark.parametrize("t", [0, 1])
+@pytest.mark.parametrize("stage", [0, 1])
+def test_bands(w, h, t, stage):
+    pl = O.gray_plane(O.synth(w, h, 1, 3)[0], 9)
+    # the top level is always `short` in the reference callers (Transform<short> only);
+    # level_chg >= levels would make it int, which the reference mis-handles
+    for L, lc in [(5, 1), (3, -1), (4, 2)]:
+        a = O.port().bands(pl, L, lc, t, stage, 96, 36)
+        b = REF.bands(pl, L, lc, t, stage, 96, 36)
+        for x, y in zip(a, b):
+            assert np.array_equal(x, y)
+
+
+@pytest.mark.parametrize("q", [0, 1, 5, 9, 20, 31])
+@pytest.mark.parametrize("t", [0, 1])
+@pytest.mark.parametrize("w,h", [(64, 48), (129, 77), (200, 113)])
+def test_ric_gray(q, t, w, h):
+    pix = O.synth(w, h, 1, q)
+    a = O.port().encode_ric(pix, q, t)
+    assert a == REF.encode_ric(pix, q, t)
+    assert np.array_equal(O.port().decode_ric(a)[1], REF.decode_ric(a)[1])
+
+
+@pytest.mark.parametrize("q,t", [(0, 1), (9, 0), (31, 0), (3, 1)])
+def test_ric_rgb(q, t):
+    pix = O.synth(96, 72, 3, q)
+    a = O.port().encode_ric(pix, q, t)
+    assert a == REF.encode_ric(pix, q, t)
+    assert np.array_equal(O.port().decode_ric(a)[1], REF.decode_ric(a)[1])
+
+
+def test_dither_decode():
+    pix = O.synth(80, 60, 1, 2)
+    a = REF.encode_ric(pix, 12, 0)
+    assert np.array_equal(O.port().decode_ric(a, dither=True)[0], REF.decode_ric(a, dither=True)[0])
+
+
+def test_haar_even_sizes():
+    pix = O.synth(128, 96, 1, 5)     # every level even: the reference is deterministic
+    a = O.port().encode_ric(pix, 9, 2)
+    assert a == REF.encode_ric(pix, 9, 2)
+    assert np.array_equal(O.port().decode_ric(a)[1], REF.decode_ric(a)[1])

@@ -1,0 +1,82 @@
+"""Frame/tile sharding and the stream gather (rududu-image-codec_amd/shard.py):
+host logic plus a world_size-2 gloo run (the GPU runs use the same code with
+the nccl=RCCL backend)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import shard
+
+
+def test_frames_partition():
+    for world in (1, 2, 4, 8):
+        got = sorted(sum((shard.frames_of_rank(64, world, r) for r in range(world)), []))
+        assert got == list(range(64))
+        assert all(len(shard.frames_of_rank(64, world, r)) == 64 // world for r in range(world))
+
+
+def test_tiles_cover_image():
+    rects = shard.tile_rects(7680, 4320)
+    assert [(r[0], r[1]) for r in rects] == [(0, 0), (1, 0), (0, 1), (1, 1)]
+    cov = np.zeros((4320, 7680), np.int32)
+    for (_, _, x0, y0, w, h) in rects:
+        cov[y0:y0 + h, x0:x0 + w] += 1
+    assert (cov == 1).all()
+    assert rects[3][2:] == (3840, 2160, 3840, 2160)
+    odd = shard.tile_rects(1001, 603)
+    assert sum(r[4] * r[5] for r in odd) == 1001 * 603
+
+
+def test_tile_container_roundtrip():
+    streams = [bytes([i]) * (10 + i) for i in range(4)]
+    blob = shard.pack_tiles(7680, 4320, 2, 2, streams)
+    W, H, nx, ny, got = shard.unpack_tiles(blob)
+    assert (W, H, nx, ny) == (7680, 4320, 2, 2) and got == streams
+    with pytest.raises(ValueError):
+        shard.unpack_tiles(b"RUD2....")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "rududu-image-codec_amd"))
+    import torch.distributed as dist
+    import shard as S
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    frames = S.frames_of_rank(7, world, rank)
+    local = [(b"frame%d:" % f) * (f + 1) for f in frames]
+    res = S.gather_streams(local, dist)
+    q.put((rank, res))
+    dist.destroy_process_group()
+
+
+def test_gather_streams_gloo_world2():
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    out = dict(q.get(timeout=120) for _ in range(2))
+    for p in ps:
+        p.join(timeout=60)
+    assert out[1] is None
+    got = out[0]
+    assert [len(x) for x in got] == [4, 3]
+    flat = {}
+    for r, lst in enumerate(got):
+        for f, s in zip(shard.frames_of_rank(7, 2, r), lst):
+            flat[f] = s
+    assert all(flat[f] == (b"frame%d:" % f) * (f + 1) for f in range(7))
