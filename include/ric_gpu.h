@@ -73,6 +73,9 @@ int ric_transform_inv(ric_wavelet* w, int16_t* image, int stride, int trans, int
 int ric_code_band(ric_wavelet* w, ric_mux* m, int quant, int lambda);
 /* CWavelet2D::DecodeBand(CMuxCodec*) (src/lib/wavelet2d.h:38) */
 int ric_decode_band(ric_wavelet* w, ric_mux* m);
+/* CWavelet2D::TSUQ(int Quant, float Thres) (src/lib/wavelet2d.h:41): dead-zone
+ * quantiser on every band (the LL with Thres 0.5); *count = non-zeros. */
+int ric_tsuq(ric_wavelet* w, int quant, float thres, unsigned int* count);
 /* CWavelet2D::TSUQi(int Quant) (src/lib/wavelet2d.h:42) */
 int ric_tsuqi(ric_wavelet* w, int quant);
 /* band pyramid introspection, canonical order: levels finest->coarsest

@@ -52,14 +52,31 @@ def build(jobs=8, verbose=False):
     with ThreadPoolExecutor(jobs) as ex:
         objs = list(ex.map(lambda s: _compile(s, hdr), srcs))
     if os.path.exists(OUT) and os.path.getmtime(OUT) >= max(os.path.getmtime(o) for o in objs):
+        _build_cli()
         return OUT
     cmd = [os.path.join(ROCM, "bin", "hipcc"), "--offload-arch=" + ARCH, "-shared", "-fPIC"] + objs + ["-o", OUT]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError("link failed: %s\n%s" % (" ".join(cmd), r.stderr))
+    _build_cli()
     if verbose:
         print("built", OUT)
     return OUT
+
+
+def _build_cli():
+    """tools/ric_cli.cpp -> ./ric (the src/ric/ric.cpp counterpart, rpath to the .so)."""
+    src = os.path.join(HERE, "tools", "ric_cli.cpp")
+    exe = os.path.join(HERE, "ric")
+    deps = [src, OUT, os.path.join(REPO, "include", "rududu_gpu.hpp"), os.path.join(REPO, "include", "ric_gpu.h")]
+    if os.path.exists(exe) and os.path.getmtime(exe) >= max(os.path.getmtime(d) for d in deps):
+        return exe
+    cmd = ["g++", "-O2", "-std=c++17", "-Wall", "-I" + os.path.join(REPO, "include"), src, "-o", exe,
+           "-L" + HERE, "-lrududu_amd", "-Wl,-rpath,$ORIGIN"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("cli build failed: %s\n%s" % (" ".join(cmd), r.stderr))
+    return exe
 
 
 if __name__ == "__main__":

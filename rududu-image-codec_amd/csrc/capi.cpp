@@ -433,6 +433,35 @@ int ric_decode_band(ric_wavelet* w, ric_mux* m)
 	return decode_band(w, m->m);
 }
 
+// CWavelet2D::TSUQ (src/lib/wavelet2d.cpp:224-246): CBand::TSUQ on every band
+// (band.h:65-92, Thres for the high bands, 0.5 for the LL); returns the count.
+int ric_tsuq(ric_wavelet* w, int quant, float thres, unsigned int* count)
+{
+	if (!w) return RIC_E_ARG;
+	if (set_dev(w->device)) return RIC_E_HIP;
+	int rc = to_device(w);
+	if (rc) return rc;
+	unsigned int* d_count = nullptr;
+	HIPCHK(hipMallocAsync((void**)&d_count, sizeof(unsigned int), w->st));
+	HIPCHK(hipMemsetAsync(d_count, 0, sizeof(unsigned int), w->st));
+	Pyramid& P = w->P;
+	for (int i = 0; i < P.nbands(); i++) {
+		const Band& B = P.band(i);
+		const float th = i == 3 * P.nlev ? 0.5f : thres;
+		int Q = (int)((float)quant / B.weight);
+		if (Q == 0) Q = 1;
+		const int iQ = (1 << 16) / Q;
+		const int T0 = tr_any(!B.is_int, (int)(th * (float)Q));
+		launch_tsuq_band(B, iQ, T0, w->d_arena, d_count, w->st);
+	}
+	unsigned int h = 0;
+	HIPCHK(hipMemcpyAsync(&h, d_count, sizeof(unsigned int), hipMemcpyDeviceToHost, w->st));
+	HIPCHK(hipFreeAsync(d_count, w->st));
+	HIPCHK(hipStreamSynchronize(w->st));
+	if (count) *count = h;
+	return RIC_OK;
+}
+
 int ric_tsuqi(ric_wavelet* w, int quant)
 {
 	if (!w) return RIC_E_ARG;

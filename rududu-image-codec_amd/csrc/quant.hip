@@ -185,6 +185,23 @@ __global__ void k_quant_ll(T* p, int pitch, int dx, int dy, int iQ, int T0)
 	else *q = (T)tr<SH>((int)((uint32_t)v * (uint32_t)iQ + 32768u) >> 16);
 }
 
+// CBand::TSUQ (src/lib/band.h:65-92) on one band, with the Count accumulated
+template <typename T>
+__global__ void k_tsuq(T* p, int pitch, int dx, int dy, int iQ, int T0, unsigned int* count)
+{
+	constexpr bool SH = sizeof(T) == 2;
+	int i = blockIdx.x * blockDim.x + threadIdx.x;
+	unsigned nz = 0;
+	if (i < dx * dy) {
+		T* q = p + (long)(i / dx) * pitch + i % dx;
+		int v = *q;
+		if ((uint32_t)(v + T0) <= (uint32_t)(2 * T0)) *q = 0;
+		else { *q = (T)tr<SH>((int)((uint32_t)v * (uint32_t)iQ + 32768u) >> 16); nz = 1; }
+	}
+	unsigned long long b = __ballot(nz);
+	if ((threadIdx.x & 63) == 0 && b) atomicAdd(count, (unsigned)__popcll(b));
+}
+
 template <typename T>
 __global__ void k_dequant(T* p, int pitch, int dx, int dy, int q)
 {
@@ -234,6 +251,15 @@ void launch_quant_ll(const Pyramid& P, int Q, int iQ, int T0, char* arena, hipSt
 	dim3 grid((n + 255) / 256);
 	if (B.is_int) hipLaunchKernelGGL(k_quant_ll<int32_t>, grid, dim3(256), 0, st, (int32_t*)(arena + B.off), B.pitch, B.dx, B.dy, iQ, T0);
 	else hipLaunchKernelGGL(k_quant_ll<int16_t>, grid, dim3(256), 0, st, (int16_t*)(arena + B.off), B.pitch, B.dx, B.dy, iQ, T0);
+}
+
+void launch_tsuq_band(const Band& B, int iQ, int T0, char* arena, unsigned int* count, hipStream_t st)
+{
+	int n = B.dx * B.dy;
+	if (n == 0) return;
+	dim3 grid((n + 255) / 256);
+	if (B.is_int) hipLaunchKernelGGL(k_tsuq<int32_t>, grid, dim3(256), 0, st, (int32_t*)(arena + B.off), B.pitch, B.dx, B.dy, iQ, T0, count);
+	else hipLaunchKernelGGL(k_tsuq<int16_t>, grid, dim3(256), 0, st, (int16_t*)(arena + B.off), B.pitch, B.dx, B.dy, iQ, T0, count);
 }
 
 void launch_dequant_band(const Band& B, int q, char* arena, hipStream_t st)

@@ -27,6 +27,8 @@ void launch_quant_ll(const Pyramid& P, int Q, int iQ, int T, char* arena, hipStr
 // Zerotree block records of the D/H/V bands of level l (symbols.h), written
 // at P.rec_off[l][b]; needs every level quantised (parents are read).
 void launch_blocks_level(const Pyramid& P, int l, char* arena, hipStream_t st);
+// CBand::TSUQ on one band, adding its non-zero count to *count (device).
+void launch_tsuq_band(const Band& B, int iQ, int T0, char* arena, unsigned int* count, hipStream_t st);
 // CBand::TSUQi on one band (src/lib/band.h:94-107).
 void launch_dequant_band(const Band& B, int q, char* arena, hipStream_t st);
 
