@@ -71,6 +71,10 @@ int ric_transform(ric_wavelet* w, const int16_t* image, int stride, int trans, i
 int ric_transform_inv(ric_wavelet* w, int16_t* image, int stride, int trans, int image_on_device);
 /* CWavelet2D::CodeBand(CMuxCodec*, int Quant, int lambda) (src/lib/wavelet2d.h:39) */
 int ric_code_band(ric_wavelet* w, ric_mux* m, int quant, int lambda);
+/* The device half of CodeBand alone: buildTree (src/lib/bandcodec.cpp:239-319)
+ * on every level, the coarsest LL TSUQ and the zerotree block records, left in
+ * HBM (no copy, no coding).  Returns after the work completes. */
+int ric_quantize(ric_wavelet* w, int quant, int lambda);
 /* CWavelet2D::DecodeBand(CMuxCodec*) (src/lib/wavelet2d.h:38) */
 int ric_decode_band(ric_wavelet* w, ric_mux* m);
 /* CWavelet2D::TSUQ(int Quant, float Thres) (src/lib/wavelet2d.h:41): dead-zone

@@ -8,6 +8,7 @@
 #include <vector>
 #include <algorithm>
 #include <chrono>
+#include <mutex>
 
 #include "ric_gpu.h"
 #include "ric_types.h"
@@ -205,8 +206,9 @@ int inverse(ric_wavelet* w, int16_t* dimg, long stride, int trans)
 	return RIC_OK;
 }
 
-// CWavelet2D::CodeBand, src/lib/wavelet2d.cpp:83-177
-int code_band(ric_wavelet* w, Mux& m, int quant, int lambda)
+// The GPU half of CWavelet2D::CodeBand (src/lib/wavelet2d.cpp:83-177):
+// buildTree on every level, the LL TSUQ, and the zerotree block records.
+int quantize_gpu(ric_wavelet* w, int quant, int lambda)
 {
 	Pyramid& P = w->P;
 	// buildTree on every level, finest first (bandcodec.cpp:239-319)
@@ -240,6 +242,14 @@ int code_band(ric_wavelet* w, Mux& m, int quant, int lambda)
 	for (int l = 0; l < P.nlev; l++) launch_blocks_level(P, l, w->d_arena, w->st);
 	w->prof.end(S_QUANT, w->st);
 	HIPCHK(hipGetLastError());
+	w->host_valid = false;
+	return RIC_OK;
+}
+
+// The host half: bands + records to the pinned mirror, then the serial coder.
+int code_band_host(ric_wavelet* w, Mux& m)
+{
+	Pyramid& P = w->P;
 	int rc = to_host(w, true);
 	if (rc) return rc;
 	// serial part: LL DPCM, then coarse -> fine, V, H, D (wavelet2d.cpp:119-159)
@@ -298,6 +308,29 @@ int tsuqi(ric_wavelet* w, int quant)
 	HIPCHK(hipGetLastError());
 	return RIC_OK;
 }
+
+// CWavelet2D::CodeBand, src/lib/wavelet2d.cpp:83-177
+int code_band(ric_wavelet* w, Mux& m, int quant, int lambda)
+{
+	int rc = quantize_gpu(w, quant, lambda);
+	return rc ? rc : code_band_host(w, m);
+}
+
+// Exclusive GPU sections: the codec's device stages (pixel conversion, DWT,
+// quantiser, records; dequantiser, inverse DWT) of concurrent codecs on one
+// device run one at a time, each at full chip width, while the host coder
+// threads overlap them.  Kernel timings stay uncontended.  RIC_GPU_SHARED=1
+// lets sections of different codecs overlap instead.
+std::mutex g_gpu_mu[64];
+const bool g_gpu_shared = [] { const char* e = getenv("RIC_GPU_SHARED"); return e && atoi(e) != 0; }();
+
+struct GpuSection {
+	std::unique_lock<std::mutex> lk;
+	explicit GpuSection(int device)
+	{
+		if (!g_gpu_shared) lk = std::unique_lock<std::mutex>(g_gpu_mu[device & 63]);
+	}
+};
 
 int ensure_img(ric_wavelet* w)
 {
@@ -424,6 +457,16 @@ int ric_code_band(ric_wavelet* w, ric_mux* m, int quant, int lambda)
 	int rc = code_band(w, m->m, quant, lambda);
 	if (rc) return rc;
 	return m->m.overflow() ? RIC_E_CAPACITY : RIC_OK;
+}
+
+int ric_quantize(ric_wavelet* w, int quant, int lambda)
+{
+	if (!w) return RIC_E_ARG;
+	if (set_dev(w->device)) return RIC_E_HIP;
+	int rc = quantize_gpu(w, quant, lambda);
+	if (rc) return rc;
+	HIPCHK(hipStreamSynchronize(w->st));
+	return RIC_OK;
 }
 
 int ric_decode_band(ric_wavelet* w, ric_mux* m)
@@ -619,19 +662,26 @@ int ric_codec_encode(ric_codec* c, const uint8_t* pix, int on_device, int q, int
 		HIPCHK(hipMemcpyAsync(c->d_pix, pix, npix, hipMemcpyHostToDevice, w->st));
 		dpix = c->d_pix;
 	}
-	w->prof.begin(S_PIXIN, w->st);
-	launch_pix_in(dpix, c->d_planes, c->w, c->h, c->pitch, c->channels, q, w->st);
-	w->prof.end(S_PIXIN, w->st);
-	HIPCHK(hipGetLastError());
 	Mux m;
 	m.init_encoder(c->stream.data(), c->stream.size(), 0);
 	w->P.set_weight(trans);
 	const long plane = c->pitch * c->h;
 	for (int p = 0; p < c->channels; p++) {
 		const int boost = p ? 8 : 0;                // C_Q_BOOST for chroma (ric.cpp:164-168)
-		int rc = forward(w, c->d_planes + p * plane, c->pitch, trans);
-		if (rc) return rc;
-		rc = code_band(w, m, q ? ric_quants(q + 20 + boost) : 0, q ? ric_quants(q + 13 + boost) : 0);
+		{
+			GpuSection gs(c->device);
+			if (p == 0) {
+				w->prof.begin(S_PIXIN, w->st);
+				launch_pix_in(dpix, c->d_planes, c->w, c->h, c->pitch, c->channels, q, w->st);
+				w->prof.end(S_PIXIN, w->st);
+				HIPCHK(hipGetLastError());
+			}
+			int rc = forward(w, c->d_planes + p * plane, c->pitch, trans);
+			if (!rc) rc = quantize_gpu(w, q ? ric_quants(q + 20 + boost) : 0, q ? ric_quants(q + 13 + boost) : 0);
+			if (rc) return rc;
+			HIPCHK(hipStreamSynchronize(w->st));
+		}
+		int rc = code_band_host(w, m);
 		if (rc) return rc;
 	}
 	uint8_t* e = m.end_coding();
@@ -671,9 +721,13 @@ int ric_codec_decode(ric_codec* c, const uint8_t* ric, size_t len, int dither,
 		const int boost = p ? 8 : 0;
 		rc = decode_band(w, m);
 		if (rc && rc != RIC_E_STREAM) return rc;
+		rc = to_device(w);
+		if (rc) return rc;
+		GpuSection gs(c->device);
 		if (q) { rc = tsuqi(w, ric_quants(q + 20 + boost)); if (rc) return rc; }
 		rc = inverse(w, c->d_planes + p * plane, c->pitch, trans);
 		if (rc) return rc;
+		HIPCHK(hipStreamSynchronize(w->st));
 	}
 	if (dither && q && c->channels == 1) {
 		// dither() is a serial error diffusion (src/ric/ric.cpp:51-74): host side
@@ -714,10 +768,14 @@ int ric_codec_decode(ric_codec* c, const uint8_t* ric, size_t len, int dither,
 	}
 	uint8_t* dpix = on_device ? pix_out : (pix_out ? c->d_pix : nullptr);
 	int16_t* dpl = on_device ? planes_out : (planes_out ? c->d_out : nullptr);
-	w->prof.begin(S_PIXOUT, w->st);
-	launch_pix_out(c->d_planes, c->pitch, c->w, c->h, c->channels, q, dpix, dpl, w->st);
-	w->prof.end(S_PIXOUT, w->st);
-	HIPCHK(hipGetLastError());
+	{
+		GpuSection gs(c->device);
+		w->prof.begin(S_PIXOUT, w->st);
+		launch_pix_out(c->d_planes, c->pitch, c->w, c->h, c->channels, q, dpix, dpl, w->st);
+		w->prof.end(S_PIXOUT, w->st);
+		HIPCHK(hipGetLastError());
+		HIPCHK(hipStreamSynchronize(w->st));
+	}
 	if (!on_device) {
 		if (pix_out) HIPCHK(hipMemcpyAsync(pix_out, c->d_pix, npix, hipMemcpyDeviceToHost, w->st));
 		if (planes_out) HIPCHK(hipMemcpyAsync(planes_out, c->d_out, npix * 2, hipMemcpyDeviceToHost, w->st));
