@@ -63,7 +63,10 @@ int ric_wavelet_sync(ric_wavelet* w);
 int ric_set_weight(ric_wavelet* w, int trans, float base_weight);
 /* CWavelet2D::Transform<short>(short* pImage, int Stride, trans t)
  * (src/lib/wavelet2d.h:33).  image_on_device: pImage is a device pointer.
- * The caller's image is only read (the reference uses it as scratch). */
+ * The caller's image is only read (the reference uses it as scratch).
+ * A host image is copied to the device at once and its transform deferred to
+ * the next call on this object, so that Transform followed by CodeBand runs
+ * as one fused forward+quantiser pass; any other call runs it first. */
 int ric_transform(ric_wavelet* w, const int16_t* image, int stride, int trans, int image_on_device);
 /* CWavelet2D::TransformI<short>(short* pImageEnd, int Stride, trans t)
  * (src/lib/wavelet2d.h:34).  Takes the image START (the reference takes the
@@ -75,6 +78,11 @@ int ric_code_band(ric_wavelet* w, ric_mux* m, int quant, int lambda);
  * on every level, the coarsest LL TSUQ and the zerotree block records, left in
  * HBM (no copy, no coding).  Returns after the work completes. */
 int ric_quantize(ric_wavelet* w, int quant, int lambda);
+/* Transform followed by the device half of CodeBand, as one fused pass over
+ * the pyramid (the 9/7 short levels transform and quantise in one kernel, the
+ * unquantised bands never reach HBM).  Synchronous. */
+int ric_transform_quantize(ric_wavelet* w, const int16_t* image, int stride, int trans, int image_on_device,
+                           int quant, int lambda);
 /* CWavelet2D::DecodeBand(CMuxCodec*) (src/lib/wavelet2d.h:38) */
 int ric_decode_band(ric_wavelet* w, ric_mux* m);
 /* CWavelet2D::TSUQ(int Quant, float Thres) (src/lib/wavelet2d.h:41): dead-zone

@@ -104,7 +104,15 @@ struct ric_wavelet {
 	size_t img_pitch = 0;             // elements
 	hipStream_t st = nullptr;
 	bool own_stream = false;
+	// second stream for the border-frame kernels of the fused forward levels,
+	// forked from / joined back to st by events
+	hipStream_t st2 = nullptr;
+	hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 	bool host_valid = false;          // bands live on the host (after a decode)
+	// A Transform of a host image is deferred until the next call, so that a
+	// CodeBand right after it runs as one fused forward+quantiser pass.
+	bool pend = false;
+	int pend_trans = 0;
 };
 
 struct ric_mux {
@@ -206,8 +214,39 @@ int inverse(ric_wavelet* w, int16_t* dimg, long stride, int trans)
 	return RIC_OK;
 }
 
-// The GPU half of CWavelet2D::CodeBand (src/lib/wavelet2d.cpp:83-177):
-// buildTree on every level, the LL TSUQ, and the zerotree block records.
+// buildTree parameters of level l (src/lib/bandcodec.cpp:243-247, float32 as
+// the reference); qin carries CodeBand's per-level C-typed Quant.
+QuantParams level_qp(const Pyramid& P, int l, int& qin, int lambda)
+{
+	const bool sh = !P.L[l].is_int;
+	qin = tr_any(sh, qin);
+	QuantParams qp;
+	for (int b = 0; b < 3; b++) {
+		const Band& B = P.L[l].b[b];
+		int lbda = (int)((float)lambda / B.weight);
+		int Q = tr_any(sh, (int16_t)(int)((float)qin / B.weight));
+		if (Q == 0) Q = 1;
+		qp.Q[b] = Q;
+		qp.iQ[b] = (1 << 16) / Q;
+		make_thres(sh, qp.thres[b], Q, lbda);
+	}
+	return qp;
+}
+
+// CBand::TSUQ on the coarsest LL with Thres 0.5 (band.h:65-92)
+void quant_ll(ric_wavelet* w, int quant)
+{
+	Band& B = w->P.coarsest_ll();
+	int Q = (int)((float)quant / B.weight);
+	if (Q == 0) Q = 1;
+	int iQ = (1 << 16) / Q;
+	int T0 = tr_any(!B.is_int, (int)(0.5f * (float)Q));
+	launch_quant_ll(w->P, Q, iQ, T0, w->d_arena, w->st);
+}
+
+// The GPU half of CWavelet2D::CodeBand (src/lib/wavelet2d.cpp:83-177) on a
+// pyramid already transformed: buildTree on every level, the LL TSUQ, and the
+// zerotree block records.
 int quantize_gpu(ric_wavelet* w, int quant, int lambda)
 {
 	Pyramid& P = w->P;
@@ -215,35 +254,67 @@ int quantize_gpu(ric_wavelet* w, int quant, int lambda)
 	int qin = quant;
 	w->prof.begin(S_QUANT, w->st);
 	for (int l = 0; l < P.nlev; l++) {
-		const bool sh = !P.L[l].is_int;
-		qin = tr_any(sh, qin);
-		QuantParams qp;
-		for (int b = 0; b < 3; b++) {
-			const Band& B = P.L[l].b[b];
-			int lbda = (int)((float)lambda / B.weight);
-			int Q = tr_any(sh, (int16_t)(int)((float)qin / B.weight));
-			if (Q == 0) Q = 1;
-			qp.Q[b] = Q;
-			qp.iQ[b] = (1 << 16) / Q;
-			make_thres(sh, qp.thres[b], Q, lbda);
-		}
+		QuantParams qp = level_qp(P, l, qin, lambda);
 		launch_quant_level(P, l, qp, w->d_arena, w->st);
 	}
-	// CBand::TSUQ on the coarsest LL with Thres 0.5 (band.h:65-92)
-	{
-		Band& B = P.coarsest_ll();
-		int Q = (int)((float)quant / B.weight);
-		if (Q == 0) Q = 1;
-		int iQ = (1 << 16) / Q;
-		int T0 = tr_any(!B.is_int, (int)(0.5f * (float)Q));
-		launch_quant_ll(P, Q, iQ, T0, w->d_arena, w->st);
-	}
+	quant_ll(w, quant);
 	// zerotree symbolisation of every level (parents must be quantised first)
-	for (int l = 0; l < P.nlev; l++) launch_blocks_level(P, l, w->d_arena, w->st);
+	for (int l = 0; l < P.nlev; l++) launch_blocks_level(P, l, true, true, w->d_arena, w->st);
 	w->prof.end(S_QUANT, w->st);
 	HIPCHK(hipGetLastError());
 	w->host_valid = false;
 	return RIC_OK;
+}
+
+// Transform + the GPU half of CodeBand in one pass over the pyramid: every 9/7
+// short level runs the fused forward+quantiser (dwt.hip k_fwdq), the others the
+// separate forward level, quantiser and record kernels.
+int encode_gpu(ric_wavelet* w, const int16_t* dimg, long stride, int trans, int quant, int lambda)
+{
+	Pyramid& P = w->P;
+	bool fused[kMaxLevels] = {};
+	int qin = quant;
+	w->prof.begin(S_FWD, w->st);
+	for (int l = 0; l < P.nlev; l++) {
+		const void* src;
+		long sp;
+		int vec8, vec16;
+		if (l == 0) {
+			src = dimg; sp = stride;
+			vec8 = (stride % 4 == 0) && ((uintptr_t)dimg % 8 == 0);
+			vec16 = (stride % 8 == 0) && ((uintptr_t)dimg % 16 == 0);
+		} else {
+			const Band& LL = P.L[l - 1].b[BL];
+			src = w->d_arena + LL.off; sp = LL.pitch; vec8 = vec16 = 1;
+		}
+		QuantParams qp = level_qp(P, l, qin, lambda);
+		fused[l] = fwdq_supported(P.L[l], trans, qp);
+		if (l == 0) w->prof.begin(S_FWD0, w->st);
+		if (fused[l]) {
+			launch_fwdq_level(P, l, src, sp, vec8, vec16, qp, w->d_arena, w->st, w->st2, w->ev_fork, w->ev_join);
+		} else {
+			launch_fwd_level(P.L[l], src, sp, w->d_arena, trans, vec8, w->st);
+			launch_quant_level(P, l, qp, w->d_arena, w->st);
+		}
+		if (l == 0) w->prof.end(S_FWD0, w->st);
+	}
+	quant_ll(w, quant);
+	// records of the unfused levels, parent info below the unfused levels
+	for (int l = 0; l < P.nlev; l++)
+		launch_blocks_level(P, l, !fused[l], l + 1 < P.nlev && !fused[l + 1], w->d_arena, w->st);
+	w->prof.end(S_FWD, w->st);
+	HIPCHK(hipGetLastError());
+	w->host_valid = false;
+	w->pend = false;
+	return RIC_OK;
+}
+
+// run a deferred Transform (see ric_wavelet::pend) before anything else
+int flush_pending(ric_wavelet* w)
+{
+	if (!w->pend) return RIC_OK;
+	w->pend = false;
+	return forward(w, w->d_img, (long)w->img_pitch, w->pend_trans);
 }
 
 // The host half: bands + records to the pinned mirror, then the serial coder.
@@ -260,7 +331,8 @@ int code_band_host(ric_wavelet* w, Mux& m)
 		for (int k = 0; k < 3; k++) {
 			const Band& B = P.L[l].b[order[k]];
 			const uint64_t* rec = (const uint64_t*)(w->h_arena + P.rec_off[l][order[k]]);
-			tree_encode_records_fast(m, rec, view(w, B), l == 0);
+			const uint8_t* pin = l + 1 < P.nlev ? (const uint8_t*)(w->h_arena + P.pin_off[l][order[k]]) : nullptr;
+			tree_encode_records_fast(m, rec, pin, view(w, B), l == 0);
 		}
 	}
 	w->prof.host(S_HENC, now_ms() - t0);
@@ -312,7 +384,8 @@ int tsuqi(ric_wavelet* w, int quant)
 // CWavelet2D::CodeBand, src/lib/wavelet2d.cpp:83-177
 int code_band(ric_wavelet* w, Mux& m, int quant, int lambda)
 {
-	int rc = quantize_gpu(w, quant, lambda);
+	int rc = w->pend ? encode_gpu(w, w->d_img, (long)w->img_pitch, w->pend_trans, quant, lambda)
+	                 : quantize_gpu(w, quant, lambda);
 	return rc ? rc : code_band_host(w, m);
 }
 
@@ -369,6 +442,9 @@ int ric_wavelet_create(ric_wavelet** out, int x, int y, int level, int level_chg
 	if (hip_fail(hipMalloc(&w->d_arena, w->P.arena_bytes), "hipMalloc arena") ||
 	    hip_fail(hipHostMalloc(&w->h_arena, w->P.arena_bytes, 0), "hipHostMalloc arena") ||
 	    hip_fail(hipStreamCreateWithFlags(&w->st, hipStreamNonBlocking), "hipStreamCreate") ||
+	    hip_fail(hipStreamCreateWithFlags(&w->st2, hipStreamNonBlocking), "hipStreamCreate") ||
+	    hip_fail(hipEventCreateWithFlags(&w->ev_fork, hipEventDisableTiming), "hipEventCreate") ||
+	    hip_fail(hipEventCreateWithFlags(&w->ev_join, hipEventDisableTiming), "hipEventCreate") ||
 	    hip_fail(hipMemsetAsync(w->d_arena, 0, w->P.arena_bytes, w->st), "hipMemset arena") ||
 	    hip_fail(hipStreamSynchronize(w->st), "hipStreamSynchronize")) {
 		ric_wavelet_destroy(w);
@@ -390,6 +466,9 @@ void ric_wavelet_destroy(ric_wavelet* w)
 	if (w->d_img) (void)hipFree(w->d_img);
 	if (w->h_arena) (void)hipHostFree(w->h_arena);
 	if (w->own_stream && w->st) (void)hipStreamDestroy(w->st);
+	if (w->st2) { (void)hipStreamSynchronize(w->st2); (void)hipStreamDestroy(w->st2); }
+	if (w->ev_fork) (void)hipEventDestroy(w->ev_fork);
+	if (w->ev_join) (void)hipEventDestroy(w->ev_join);
 	delete w;
 }
 
@@ -397,6 +476,7 @@ int ric_wavelet_set_stream(ric_wavelet* w, void* s)
 {
 	if (!w) return RIC_E_ARG;
 	if (set_dev(w->device)) return RIC_E_HIP;
+	if (flush_pending(w)) return RIC_E_HIP;
 	HIPCHK(hipStreamSynchronize(w->st));
 	if (w->own_stream) (void)hipStreamDestroy(w->st);
 	if (s) { w->st = (hipStream_t)s; w->own_stream = false; }
@@ -408,6 +488,7 @@ int ric_wavelet_sync(ric_wavelet* w)
 {
 	if (!w) return RIC_E_ARG;
 	if (set_dev(w->device)) return RIC_E_HIP;
+	if (flush_pending(w)) return RIC_E_HIP;
 	HIPCHK(hipStreamSynchronize(w->st));
 	return RIC_OK;
 }
@@ -428,8 +509,13 @@ int ric_transform(ric_wavelet* w, const int16_t* image, int stride, int trans, i
 		if (rc) return rc;
 		HIPCHK(hipMemcpy2DAsync(w->d_img, w->img_pitch * 2, image, (size_t)stride * 2, (size_t)w->P.w * 2,
 		                        w->P.h, hipMemcpyHostToDevice, w->st));
-		return forward(w, w->d_img, (long)w->img_pitch, trans);
+		// deferred: a CodeBand next runs it fused with the quantiser (encode_gpu)
+		w->pend = true;
+		w->pend_trans = trans;
+		w->host_valid = false;
+		return RIC_OK;
 	}
+	w->pend = false;   // superseded: this transform rewrites every band
 	return forward(w, image, stride, trans);
 }
 
@@ -437,6 +523,7 @@ int ric_transform_inv(ric_wavelet* w, int16_t* image, int stride, int trans, int
 {
 	if (!w || !image || stride < w->P.w || trans < 0 || trans > 2) return RIC_E_ARG;
 	if (set_dev(w->device)) return RIC_E_HIP;
+	if (flush_pending(w)) return RIC_E_HIP;
 	if (!on_device) {
 		int rc = ensure_img(w);
 		if (rc) return rc;
@@ -463,9 +550,32 @@ int ric_quantize(ric_wavelet* w, int quant, int lambda)
 {
 	if (!w) return RIC_E_ARG;
 	if (set_dev(w->device)) return RIC_E_HIP;
-	int rc = quantize_gpu(w, quant, lambda);
+	int rc = w->pend ? encode_gpu(w, w->d_img, (long)w->img_pitch, w->pend_trans, quant, lambda)
+	                 : quantize_gpu(w, quant, lambda);
 	if (rc) return rc;
 	HIPCHK(hipStreamSynchronize(w->st));
+	return RIC_OK;
+}
+
+int ric_transform_quantize(ric_wavelet* w, const int16_t* image, int stride, int trans, int on_device,
+                           int quant, int lambda)
+{
+	if (!w || !image || stride < w->P.w || trans < 0 || trans > 2) return RIC_E_ARG;
+	if (set_dev(w->device)) return RIC_E_HIP;
+	w->pend = false;
+	const int16_t* src = image;
+	long sp = stride;
+	if (!on_device) {
+		int rc = ensure_img(w);
+		if (rc) return rc;
+		HIPCHK(hipMemcpy2DAsync(w->d_img, w->img_pitch * 2, image, (size_t)stride * 2, (size_t)w->P.w * 2,
+		                        w->P.h, hipMemcpyHostToDevice, w->st));
+		src = w->d_img; sp = (long)w->img_pitch;
+	}
+	int rc = encode_gpu(w, src, sp, trans, quant, lambda);
+	if (rc) return rc;
+	HIPCHK(hipStreamSynchronize(w->st));
+	w->prof.harvest();
 	return RIC_OK;
 }
 
@@ -473,6 +583,7 @@ int ric_decode_band(ric_wavelet* w, ric_mux* m)
 {
 	if (!w || !m || m->encoder) return RIC_E_ARG;
 	if (set_dev(w->device)) return RIC_E_HIP;
+	w->pend = false;   // every band is rewritten
 	return decode_band(w, m->m);
 }
 
@@ -482,6 +593,7 @@ int ric_tsuq(ric_wavelet* w, int quant, float thres, unsigned int* count)
 {
 	if (!w) return RIC_E_ARG;
 	if (set_dev(w->device)) return RIC_E_HIP;
+	if (flush_pending(w)) return RIC_E_HIP;
 	int rc = to_device(w);
 	if (rc) return rc;
 	unsigned int* d_count = nullptr;
@@ -509,6 +621,7 @@ int ric_tsuqi(ric_wavelet* w, int quant)
 {
 	if (!w) return RIC_E_ARG;
 	if (set_dev(w->device)) return RIC_E_HIP;
+	if (flush_pending(w)) return RIC_E_HIP;
 	return tsuqi(w, quant);
 }
 
@@ -529,6 +642,7 @@ int ric_band_read(ric_wavelet* w, int index, int32_t* out)
 {
 	if (!w || !out || index < 0 || index >= w->P.nbands()) return RIC_E_ARG;
 	if (set_dev(w->device)) return RIC_E_HIP;
+	if (flush_pending(w)) return RIC_E_HIP;
 	const Band& B = w->P.band(index);
 	if (!w->host_valid) {
 		HIPCHK(hipMemcpyAsync(w->h_arena + B.off, w->d_arena + B.off, B.bytes(), hipMemcpyDeviceToHost, w->st));
@@ -546,6 +660,7 @@ int ric_band_write(ric_wavelet* w, int index, const int32_t* in)
 {
 	if (!w || !in || index < 0 || index >= w->P.nbands()) return RIC_E_ARG;
 	if (set_dev(w->device)) return RIC_E_HIP;
+	if (flush_pending(w)) return RIC_E_HIP;
 	int rc = to_device(w);
 	if (rc) return rc;
 	const Band& B = w->P.band(index);
@@ -676,8 +791,8 @@ int ric_codec_encode(ric_codec* c, const uint8_t* pix, int on_device, int q, int
 				w->prof.end(S_PIXIN, w->st);
 				HIPCHK(hipGetLastError());
 			}
-			int rc = forward(w, c->d_planes + p * plane, c->pitch, trans);
-			if (!rc) rc = quantize_gpu(w, q ? ric_quants(q + 20 + boost) : 0, q ? ric_quants(q + 13 + boost) : 0);
+			int rc = encode_gpu(w, c->d_planes + p * plane, c->pitch, trans,
+			                    q ? ric_quants(q + 20 + boost) : 0, q ? ric_quants(q + 13 + boost) : 0);
 			if (rc) return rc;
 			HIPCHK(hipStreamSynchronize(w->st));
 		}

@@ -19,6 +19,8 @@
 #include <cstdlib>
 #include "ric_types.h"
 #include "ric_kernels.h"
+#include "quant_block.h"
+#include "symbols.h"
 
 namespace ric {
 
@@ -303,10 +305,7 @@ __device__ __forceinline__ void store_band2(T* __restrict__ row, int bx, int dx,
 // both the row steps (neighbours via one DPP shift + one alignbit) and the
 // column steps (elementwise between rows) are 2-wide, and the de-interleaved
 // band words D/H/V/L are E/O of even/odd rows as they stand.
-typedef short v2s __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ v2s as_v2(uint32_t u) { return __builtin_bit_cast(v2s, u); }
-__device__ __forceinline__ uint32_t as_u32(v2s v) { return __builtin_bit_cast(uint32_t, v); }
+// v2s, as_v2, as_u32: quant_block.h
 // (a & m) | (b & ~m): per-16-bit-half select
 __device__ __forceinline__ v2s sel(uint32_t m, v2s a, v2s b) { return as_v2((as_u32(a) & m) | (as_u32(b) & ~m)); }
 // (lm, c1): the odd left neighbours of E = (c0, c2); lm = left lane's c3
@@ -721,6 +720,582 @@ __global__ void __launch_bounds__(256) k_fwd(FwdArgs<TI, TO> a)
 	}
 }
 
+// ------------------------------------------- fused forward level + quantiser
+// k_fwdq: one 9/7 short->short forward level fused with the band's whole
+// device-side CodeBand work, so the unquantised bands never go back to HBM:
+//   * CWavelet2D::Transform97 of the level (src/lib/wavelet2d.cpp:407-492);
+//   * CBandCodec::buildTree's tsuqBlock + pRD + INSIGNIF marker on every 4x4
+//     block of D, H, V (src/lib/bandcodec.cpp:159-319; the children's pRD are
+//     the finer level's, already final because levels run finest first);
+//   * the block-local zerotree record of every block, and the parent info of
+//     the FINER level's blocks, whose parent this level is (symbols.h).
+// The LL band (next level's input) is written unquantised.
+//
+// Geometry: one wave owns a 512-column strip (8 columns per lane, 16-byte
+// row loads; lanes 0 and 63 are halo, so 496 output columns = 62 blocks of
+// every band, one block column per lane) and a segment of S input rows
+// (S/8 block rows).  Interior waves ("fast") keep everything in registers:
+// the packed 16-bit lifting of fwd97p_seg on 8 columns (4 packed words per
+// row), a 4-band-row buffer per band, and the quantiser on the buffer once a
+// block row is complete.  Waves touching an image border ("edge") run the
+// checked 4-column lifting (fwd97p_seg<S, false>) over their two 248-column
+// halves, then quantise their own blocks from the just-written bands (the
+// blocks of one lane were written by lanes of the same wave: a workgroup-scope
+// fence orders it).
+constexpr int kFqStrip = (kLanes - 2) * 8;   // 496 output columns per wave
+
+__constant__ SymTables kSymDevF __attribute__((aligned(16))) = RIC_SYM_TABLES_INIT;
+__constant__ EnumSplit kEnumDevF __attribute__((aligned(16))) = make_enum_split();
+
+// format tables staged in LDS once per workgroup
+struct FqTables {
+	SymTables T;
+	EnumSplit E;
+};
+
+struct FqArgs {
+	const int16_t* src; long sp;
+	int W, H, nseg, vec8, vec16, nofast, high;
+	int16_t* d[4]; long p[4];          // D, H, V, L
+	int dx[3], dy[3], bw[3], bh[3];
+	uint32_t* rd[3];                   // this level's pRD (raster, stride bw)
+	const uint32_t* crd[3]; int cbw[3];   // the finer level's pRD, or null
+	uint64_t* rec[3];                  // this level's block-local records
+	uint8_t* cpin[3]; int cpw[3], cph[3];  // the finer level's parent info, or null
+	int Q[3], iQ[3];
+	int thres[3][16];
+};
+
+struct PRow8 { v2s q[4]; };            // (c0,c2) (c4,c6) | (c1,c3) (c5,c7)
+
+__device__ __forceinline__ PRow8 prow8_from(const uint4& u)
+{
+	PRow8 r;
+	r.q[0] = as_v2(__builtin_amdgcn_perm(u.y, u.x, 0x05040100u));
+	r.q[2] = as_v2(__builtin_amdgcn_perm(u.y, u.x, 0x07060302u));
+	r.q[1] = as_v2(__builtin_amdgcn_perm(u.w, u.z, 0x05040100u));
+	r.q[3] = as_v2(__builtin_amdgcn_perm(u.w, u.z, 0x07060302u));
+	return r;
+}
+// the odd left neighbours of the evens: (lm, c1), (c3, c5)
+__device__ __forceinline__ void left_odd8(const PRow8& r, v2s& l0, v2s& l1)
+{
+	l0 = as_v2(__builtin_amdgcn_alignbit(as_u32(r.q[2]), (uint32_t)from_left((int)as_u32(r.q[3])), 16));
+	l1 = as_v2(__builtin_amdgcn_alignbit(as_u32(r.q[3]), as_u32(r.q[2]), 16));
+}
+// the even right neighbours of the odds: (c2, c4), (c6, rn)
+__device__ __forceinline__ void right_even8(const PRow8& r, v2s& r0, v2s& r1)
+{
+	r0 = as_v2(__builtin_amdgcn_alignbit(as_u32(r.q[1]), as_u32(r.q[0]), 16));
+	r1 = as_v2(__builtin_amdgcn_alignbit((uint32_t)from_right((int)as_u32(r.q[0])), as_u32(r.q[1]), 16));
+}
+
+// TransLine97 (src/lib/wavelet2d.cpp:320-359) on two interior rows at once
+__device__ __forceinline__ void row_fwd97p8x2(PRow8& r, PRow8& s)
+{
+	v2s a0, a1, b0, b1, t;
+	left_odd8(r, a0, a1); left_odd8(s, b0, b1);                   // P1 (even)
+	t = a0 + r.q[2]; r.q[0] -= t + (t >> 1);
+	t = b0 + s.q[2]; s.q[0] -= t + (t >> 1);
+	t = a1 + r.q[3]; r.q[1] -= t + (t >> 1);
+	t = b1 + s.q[3]; s.q[1] -= t + (t >> 1);
+	right_even8(r, a0, a1); right_even8(s, b0, b1);               // U1 (odd)
+	r.q[2] -= avg16(r.q[0], a0); s.q[2] -= avg16(s.q[0], b0);
+	r.q[3] -= avg16(r.q[1], a1); s.q[3] -= avg16(s.q[1], b1);
+	left_odd8(r, a0, a1); left_odd8(s, b0, b1);                   // P2 (even)
+	r.q[0] += mult08p(a0 + r.q[2]); s.q[0] += mult08p(b0 + s.q[2]);
+	r.q[1] += mult08p(a1 + r.q[3]); s.q[1] += mult08p(b1 + s.q[3]);
+	right_even8(r, a0, a1); right_even8(s, b0, b1);               // U2 (odd)
+	t = r.q[0] + a0; r.q[2] += (t >> 1) - (t >> 5);
+	t = s.q[0] + b0; s.q[2] += (t >> 1) - (t >> 5);
+	t = r.q[1] + a1; r.q[3] += (t >> 1) - (t >> 5);
+	t = s.q[1] + b1; s.q[3] += (t >> 1) - (t >> 5);
+}
+
+// Children of block (kx, ky) at the finer level: their parent info from this
+// block's final values (symbols.h parent_info, computed on the parent side).
+__device__ __forceinline__ void fq_child_pin(const FqArgs& a, int b, const int (&v)[16], bool full, int kx, int ky)
+{
+	uint8_t* cp = a.cpin[b];
+	if (!cp) return;
+	const uint32_t prop = (full && v[0] == kInsignif) ? 0x80u : 0u;
+#pragma unroll
+	for (int q = 0; q < 4; q++) {
+		const int qx = q & 1, qy = q >> 1;
+		const int cx = 2 * kx + qx, cy = 2 * ky + qy;
+		const int o = 8 * qy + 2 * qx;
+		if (cx < a.cpw[b] && cy < a.cph[b])
+			cp[(long)cy * a.cpw[b] + cx] = (uint8_t)(pin_ctx_of<true>(v[o], v[o + 1], v[o + 4], v[o + 5]) | prop);
+	}
+}
+
+// children pRD sum exactly as k_quant_level (u32 sum, then widened)
+__device__ __forceinline__ uint32_t fq_dist(const FqArgs& a, int b, int cnt, int kx, int ky)
+{
+	uint64_t d = (uint64_t)cnt;
+	if (a.crd[b]) {
+		const uint32_t* c0 = a.crd[b] + (long)(2 * ky) * a.cbw[b] + 2 * kx;
+		const uint32_t* c1 = c0 + a.cbw[b];
+		d += (uint32_t)(c0[0] + c0[1] + c1[0] + c1[1]);
+	}
+	return d > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)d;
+}
+
+// parent info of the 4 children of a full block held as packed words
+__device__ __forceinline__ void fq_child_pin_pk(const FqArgs& a, int b, const uint32_t (&w)[8], bool insig, int kx, int ky)
+{
+	uint8_t* cp = a.cpin[b];
+	if (!cp) return;
+	const uint32_t prop = insig ? 0x80u : 0u;
+#pragma unroll
+	for (int q = 0; q < 4; q++) {
+		const int qx = q & 1, qy = q >> 1;
+		const int cx = 2 * kx + qx, cy = 2 * ky + qy;
+		// maxLen<2> over the quadrant, max from 0 (markers are negative)
+		const v2s m2 = __builtin_elementwise_max(__builtin_elementwise_max(as_v2(w[4 * qy + qx]), as_v2(w[4 * qy + 2 + qx])),
+		                                         (v2s){0, 0});
+		const int mx = m2.x > m2.y ? m2.x : m2.y;
+		if (cx < a.cpw[b] && cy < a.cph[b])
+			cp[(long)cy * a.cpw[b] + cx] = (uint8_t)(((uint32_t)bitlen((uint32_t)mx >> 1) & 31) | prop);
+	}
+}
+
+// one full block from the register buffer (4 band rows of 4 shorts = 8
+// packed words, row r = words 2r, 2r + 1)
+__device__ __forceinline__ void fq_block_regs(const FqArgs& a, const int* thr, const uint32_t* tpk, const FqTables& F,
+                                              int b, const uint2 (&buf)[4], int kx, int ky, bool out_lane)
+{
+	uint32_t w[8];
+#pragma unroll
+	for (int r = 0; r < 4; r++) { w[2 * r] = buf[r].x; w[2 * r + 1] = buf[r].y; }
+	const int cnt = tsuq_full_pk(w, a.Q[b], a.iQ[b], thr[0], tpk);   // levels are fused only when pk_ok
+	const uint32_t dist = fq_dist(a, b, cnt, kx, ky);
+	if (dist == 0) w[0] = (w[0] & 0xFFFF0000u) | 0x8000u;   // INSIGNIF_BLOCK
+	if (!out_lane) return;
+	const long pb = a.p[b];
+	int16_t* base = a.d[b] + (long)(4 * ky) * pb + 4 * kx;
+#pragma unroll
+	for (int r = 0; r < 4; r++) *reinterpret_cast<uint2*>(base + r * pb) = make_uint2(w[2 * r], w[2 * r + 1]);
+	const long bi = (long)ky * a.bw[b] + kx;
+	a.rd[b][bi] = dist;
+	// significance mask: bit i = coefficient i != 0
+	uint32_t acc = 0;
+#pragma unroll
+	for (int j = 0; j < 8; j++) acc |= as_w(__builtin_elementwise_min(as_v2u(w[j]), (v2u){1, 1})) << (2 * j);
+	const uint32_t mask = (acc & 0x5555u) | ((acc >> 15) & 0xAAAAu);
+	const bool insig = (w[0] & 0xFFFFu) == 0x8000u;
+	a.rec[b][bi] = block_local_mask<true>(F.T, &F.E, mask, insig, a.high != 0);
+	fq_child_pin_pk(a, b, w, insig, kx, ky);
+}
+
+// The blocks of one block row (D, H, V) read back from the bands in HBM, full
+// or partial (edge waves).  All loads are issued before any block is
+// processed, so a block row costs one memory round trip.  Full blocks use the
+// packed quantiser (the level is fused only when pk_ok), partial ones the
+// edge tsuqBlock.
+__device__ __forceinline__ void fq_row_global(const FqArgs& a, const int (*thr)[16], const uint32_t (*tpk)[17 * 8],
+                                              const FqTables& F, int kx, int ky)
+{
+	uint32_t w[3][8];
+	uint32_t csum[3];
+	bool ok[3], full[3];
+	int wdt[3], hgt[3];
+#pragma unroll
+	for (int b = 0; b < 3; b++) {
+		ok[b] = kx < a.bw[b] && ky < a.bh[b];
+		wdt[b] = ok[b] ? min(4, a.dx[b] - 4 * kx) : 0;
+		hgt[b] = ok[b] ? min(4, a.dy[b] - 4 * ky) : 0;
+		full[b] = wdt[b] == 4 && hgt[b] == 4;
+		const long pb = a.p[b];
+		const int16_t* base = a.d[b] + (long)(4 * ky) * pb + 4 * kx;
+		if (full[b]) {
+#pragma unroll
+			for (int r = 0; r < 4; r++) {
+				const uint2 u = *reinterpret_cast<const uint2*>(base + r * pb);
+				w[b][2 * r] = u.x; w[b][2 * r + 1] = u.y;
+			}
+		} else {
+#pragma unroll
+			for (int j = 0; j < 8; j++) {
+				const int i0 = 2 * j, i1 = 2 * j + 1;
+				const uint32_t lo = ((i0 >> 2) < hgt[b] && (i0 & 3) < wdt[b]) ? (uint16_t)base[(i0 >> 2) * pb + (i0 & 3)] : 0u;
+				const uint32_t hi = ((i1 >> 2) < hgt[b] && (i1 & 3) < wdt[b]) ? (uint16_t)base[(i1 >> 2) * pb + (i1 & 3)] : 0u;
+				w[b][j] = lo | (hi << 16);
+			}
+		}
+		csum[b] = 0;
+		if (full[b] && a.crd[b]) {
+			const uint32_t* c0 = a.crd[b] + (long)(2 * ky) * a.cbw[b] + 2 * kx;
+			const uint32_t* c1 = c0 + a.cbw[b];
+			csum[b] = (uint32_t)(c0[0] + c0[1] + c1[0] + c1[1]);
+		}
+	}
+#pragma unroll
+	for (int b = 0; b < 3; b++) {
+		if (!ok[b]) continue;
+		const long pb = a.p[b];
+		int16_t* base = a.d[b] + (long)(4 * ky) * pb + 4 * kx;
+		const long bi = (long)ky * a.bw[b] + kx;
+		if (full[b]) {
+			const uint64_t d = (uint64_t)tsuq_full_pk(w[b], a.Q[b], a.iQ[b], thr[b][0], tpk[b]) + csum[b];
+			const uint32_t dist = d > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)d;
+			if (dist == 0) w[b][0] = (w[b][0] & 0xFFFF0000u) | 0x8000u;
+#pragma unroll
+			for (int r = 0; r < 4; r++) *reinterpret_cast<uint2*>(base + r * pb) = make_uint2(w[b][2 * r], w[b][2 * r + 1]);
+			a.rd[b][bi] = dist;
+			uint32_t acc = 0;
+#pragma unroll
+			for (int j = 0; j < 8; j++) acc |= as_w(__builtin_elementwise_min(as_v2u(w[b][j]), (v2u){1, 1})) << (2 * j);
+			const uint32_t mask = (acc & 0x5555u) | ((acc >> 15) & 0xAAAAu);
+			const bool insig = (w[b][0] & 0xFFFFu) == 0x8000u;
+			a.rec[b][bi] = block_local_mask<true>(F.T, &F.E, mask, insig, a.high != 0);
+			fq_child_pin_pk(a, b, w[b], insig, kx, ky);
+		} else {
+			// edge tsuqBlock, src/lib/bandcodec.cpp:215-237 (children ignored)
+			int v[16];
+#pragma unroll
+			for (int j = 0; j < 8; j++) { v[2 * j] = (int16_t)(w[b][j] & 0xffff); v[2 * j + 1] = (int)w[b][j] >> 16; }
+			const uint32_t dist = (uint32_t)tsuq_edge<true>(v, wdt[b], hgt[b], a.Q[b], a.iQ[b]);
+			if (dist == 0) v[0] = kInsignif;
+#pragma unroll
+			for (int i = 0; i < 16; i++)
+				if ((i >> 2) < hgt[b] && (i & 3) < wdt[b]) base[(i >> 2) * pb + (i & 3)] = (int16_t)v[i];
+			a.rd[b][bi] = dist;
+			a.rec[b][bi] = block_local_edge(F.T, v, wdt[b], hgt[b], a.high != 0);
+			fq_child_pin(a, b, v, false, kx, ky);
+		}
+	}
+}
+
+// Image-border flags of one wave (fq_seg<S, true>).  Needs W % 8 == 0 and
+// H % 8 == 0: column W-1 is then the last odd column of some lane, and every
+// block the wave quantises is full.
+struct FqBorder {
+	uint32_t eL0;      // 0x0000FFFF on the lane whose word q0 low half is column 0
+	uint32_t oR3;      // 0xFFFF0000 on the lane whose word q3 high half is column W-1
+	bool top;          // y0 == 0: rows above the image, boundary formulas at e == 0, 2
+	bool bottom;       // y0 + S >= H: the segment ends at H, tail formulas after the loop
+	bool ld;           // this lane's 8 columns lie inside the image (loads allowed)
+};
+
+// TransLine97 with the left/right boundary formulas (src/lib/wavelet2d.cpp:
+// 326-358: x0 -= 3 x1 at column 0, 2 mult08 at column 0 for P2, the odd last
+// column from its left neighbour only), two rows at once
+__device__ __forceinline__ void row_fwd97p8x2_edge(PRow8& r, PRow8& s, const FqBorder& m)
+{
+	v2s a0, a1, b0, b1, t, u;
+	left_odd8(r, a0, a1); left_odd8(s, b0, b1);                   // P1 (even)
+	t = a0 + r.q[2]; t = t + (t >> 1); r.q[0] -= sel(m.eL0, mul3(r.q[2]), t);
+	u = b0 + s.q[2]; u = u + (u >> 1); s.q[0] -= sel(m.eL0, mul3(s.q[2]), u);
+	t = a1 + r.q[3]; r.q[1] -= t + (t >> 1);
+	u = b1 + s.q[3]; s.q[1] -= u + (u >> 1);
+	right_even8(r, a0, a1); right_even8(s, b0, b1);               // U1 (odd)
+	r.q[2] -= avg16(r.q[0], a0); s.q[2] -= avg16(s.q[0], b0);
+	r.q[3] -= sel(m.oR3, r.q[1] >> 3, avg16(r.q[1], a1));
+	s.q[3] -= sel(m.oR3, s.q[1] >> 3, avg16(s.q[1], b1));
+	left_odd8(r, a0, a1); left_odd8(s, b0, b1);                   // P2 (even)
+	t = mult08p(sel(m.eL0, r.q[2], a0 + r.q[2])); r.q[0] += sel(m.eL0, t + t, t);
+	u = mult08p(sel(m.eL0, s.q[2], b0 + s.q[2])); s.q[0] += sel(m.eL0, u + u, u);
+	r.q[1] += mult08p(a1 + r.q[3]); s.q[1] += mult08p(b1 + s.q[3]);
+	right_even8(r, a0, a1); right_even8(s, b0, b1);               // U2 (odd)
+	t = r.q[0] + a0; r.q[2] += (t >> 1) - (t >> 5);
+	u = s.q[0] + b0; s.q[2] += (u >> 1) - (u >> 5);
+	t = r.q[1] + a1; r.q[3] += sel(m.oR3, r.q[1] - (r.q[1] >> 4), (t >> 1) - (t >> 5));
+	u = s.q[1] + b1; s.q[3] += sel(m.oR3, s.q[1] - (s.q[1] >> 4), (u >> 1) - (u >> 5));
+}
+
+// One wave's segment: the forward 9/7 of rows [y0, y0 + S) of a 496-column
+// strip and the quantiser, records and parent info of the block rows they
+// make, all in registers.  EDGE: the wave touches an image border (m).
+template <int S, bool EDGE>
+__device__ __forceinline__ void fq_seg(const FqArgs& a, const int (*thr)[16], const uint32_t (*tpk)[17 * 8],
+                                       const FqTables& F, int x, int lane, int y0, int kx, const FqBorder& m)
+{
+	const bool out_lane = lane >= 1 && lane <= kLanes - 2 && (!EDGE || x < a.W);
+	int16_t* pL = a.d[BL] + (long)(y0 >> 1) * a.p[BL] + (x >> 1);
+	// input rows y0-4 .. y0+S+3 through a ring of PF row pairs (fwd97p_seg);
+	// PF = 4 pairs = one block row of output, so the buffer slot of an emitted
+	// pair is the unrolled index k
+	constexpr int NP = (S + 8) / 2, PF = 4;
+	static_assert(NP % PF == 0, "segment rows");
+	// bottom segment: pairs e = y0-4 .. H-2 only, then the tail formulas
+	const int nit = (EDGE && m.bottom) ? (a.H - y0) / 8 + 1 : NP / PF;   // loop iterations
+	const int kend = (EDGE && m.bottom) ? 2 : PF;                          // pairs of the last one
+	uint4 ring[2 * PF];
+	const int16_t* rp = a.src + (long)(y0 - 4) * a.sp + x;
+	int yl = y0 - 4;
+	auto load_next = [&](uint4& dst) {
+		if (!EDGE || (m.ld && yl >= 0 && yl < a.H)) dst = *reinterpret_cast<const uint4*>(rp);
+		else dst = make_uint4(0, 0, 0, 0);
+		rp += a.sp; yl++;
+	};
+#pragma unroll
+	for (int j = 0; j < 2 * PF; j++) load_next(ring[j]);
+	const v2s z = {0, 0};
+	PRow8 w0, w1, w2, w3, w4, w5;
+#pragma unroll
+	for (int q = 0; q < 4; q++) { w0.q[q] = z; w1.q[q] = z; w2.q[q] = z; w3.q[q] = z; }
+	uint2 bD[4], bH[4], bV[4];
+	auto emit = [&](int k) {                    // rows e-4 (D, H) and e-3 (V, L) are final
+		bD[k] = make_uint2(as_u32(w0.q[0]), as_u32(w0.q[1]));
+		bH[k] = make_uint2(as_u32(w0.q[2]), as_u32(w0.q[3]));
+		bV[k] = make_uint2(as_u32(w1.q[0]), as_u32(w1.q[1]));
+		if (out_lane) *reinterpret_cast<uint2*>(pL) = make_uint2(as_u32(w1.q[2]), as_u32(w1.q[3]));
+		pL += a.p[BL];
+	};
+	auto quant_row = [&](int ky) {
+		// one block at a time: the scheduler would otherwise interleave the
+		// three independent quantisers and spill
+		__builtin_amdgcn_sched_barrier(0);
+		fq_block_regs(a, thr[BD], tpk[BD], F, BD, bD, kx, ky, out_lane);
+		__builtin_amdgcn_sched_barrier(0);
+		fq_block_regs(a, thr[BH], tpk[BH], F, BH, bH, kx, ky, out_lane);
+		__builtin_amdgcn_sched_barrier(0);
+		fq_block_regs(a, thr[BV], tpk[BV], F, BV, bV, kx, ky, out_lane);
+		__builtin_amdgcn_sched_barrier(0);
+	};
+#pragma unroll 1
+	for (int it = 0; it < nit; it++) {
+		const bool last = it + 1 == nit;
+#pragma unroll
+		for (int k = 0; k < PF; k++) {
+			if (EDGE && last && k >= kend) break;
+			const int e = y0 - 4 + 2 * (it * PF + k);   // the pair's even row
+			w4 = prow8_from(ring[2 * k]);
+			w5 = prow8_from(ring[2 * k + 1]);
+			if (!last) { load_next(ring[2 * k]); load_next(ring[2 * k + 1]); }
+			if (EDGE && e < 0) continue;                 // above the image (top segment)
+			if (EDGE) row_fwd97p8x2_edge(w4, w5, m);
+			else row_fwd97p8x2(w4, w5);
+			// P1 at e, U1 at e-1, P2 at e-2, U2 at e-3 (src/lib/wavelet2d.cpp:425-454)
+			if (EDGE && e == 0) {
+#pragma unroll
+				for (int q = 0; q < 4; q++) w4.q[q] -= mul3(w5.q[q]);
+			} else {
+#pragma unroll
+				for (int q = 0; q < 4; q++) { v2s t = w3.q[q] + w5.q[q]; w4.q[q] -= t + (t >> 1); }
+			}
+			if (!EDGE || e >= 1) {
+#pragma unroll
+				for (int q = 0; q < 4; q++) w3.q[q] -= avg16(w2.q[q], w4.q[q]);
+			}
+			if (EDGE && e == 2) {
+#pragma unroll
+				for (int q = 0; q < 4; q++) { v2s t = mult08p(w3.q[q]); w2.q[q] += t + t; }
+			} else if (!EDGE || e >= 4) {
+#pragma unroll
+				for (int q = 0; q < 4; q++) w2.q[q] += mult08p(w1.q[q] + w3.q[q]);
+			}
+			if (!EDGE || e >= 4) {
+#pragma unroll
+				for (int q = 0; q < 4; q++) { v2s t = w0.q[q] + w2.q[q]; w1.q[q] += (t >> 1) - (t >> 5); }
+			}
+			if (it >= 1) emit(k);
+			w0 = w2; w1 = w3; w2 = w4; w3 = w5;
+		}
+		if (EDGE && last && m.bottom) {
+			// even H: the window holds rows H-4 .. H-1 (src/lib/wavelet2d.cpp:476-491)
+#pragma unroll
+			for (int q = 0; q < 4; q++) {
+				w3.q[q] -= w2.q[q] >> 3;
+				w2.q[q] += mult08p(w1.q[q] + w3.q[q]);
+				const v2s t = w0.q[q] + w2.q[q];
+				w1.q[q] += (t >> 1) - (t >> 5);
+				w3.q[q] += w2.q[q] - (w2.q[q] >> 4);
+			}
+			emit(2);
+			w0 = w2; w1 = w3;
+			emit(3);
+		}
+		if (it >= 1) quant_row((y0 >> 3) + it - 1);   // a block row is complete
+	}
+}
+
+template <int S>
+__device__ __forceinline__ void fq_edge(const FqArgs& a, const int (*thr)[16], const uint32_t (*tpk)[17 * 8],
+                                        const FqTables& F, int lane, int y0, int strip)
+{
+	FwdArgs<int16_t, int16_t> f;
+	f.src = a.src; f.sp = a.sp; f.W = a.W; f.H = a.H;
+#pragma unroll
+	for (int b = 0; b < 4; b++) { f.d[b] = a.d[b]; f.p[b] = a.p[b]; }
+	f.nseg = a.nseg; f.vec = a.vec8; f.nofast = 1;
+	for (int h = 0; h < 2; h++) {
+		const int X0 = strip * kFqStrip + h * kStripValid - kCols;
+		if (X0 + kCols >= a.W) break;
+		fwd97p_seg<S, false>(f, X0 + lane * kCols, lane, y0);
+	}
+	// the blocks of this lane were written by lanes of this wave
+	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+	if (lane < 1 || lane > kLanes - 2) return;
+	const int kx = strip * (kFqStrip / 8) + lane - 1;
+	for (int ky = y0 >> 3; ky < (y0 + S) >> 3; ky++) fq_row_global(a, thr, tpk, F, kx, ky);
+}
+
+// The level is split into an interior rectangle of "fast" waves (strips
+// [fs0, fs1), segments [fg0, fg1) of S rows) and the border frame around it,
+// run as two kernels on forked streams so the frame's latency-bound waves
+// overlap the interior's streaming ones.
+struct FqGrid {
+	int fs0, fs1, fg0, fg1, S;         // interior rectangle (S-row segments)
+	int nstrip;
+	int se_rows;                       // frame segment height
+	int nseg_e;                        // frame segments per full-height strip
+	int tseg, bseg0;                   // frame segments above / from here below the interior
+	int n_lr, nlr_strips, lr_strip[3]; // full-height frame strips (lr_all: every strip)
+	int lr_all;
+	int border;                        // the interior kernel covers the whole level
+	int n_tb, ntb;                     // top+bottom units of the interior strips
+};
+
+__device__ __forceinline__ void fq_stage_tables(const FqArgs& a, int (*s_thres)[16], FqTables& s_F, uint32_t (*s_tpk)[17 * 8])
+{
+	if (threadIdx.x < 48) s_thres[threadIdx.x / 16][threadIdx.x % 16] = a.thres[threadIdx.x / 16][threadIdx.x % 16];
+	{
+		for (int i = threadIdx.x; i < 3 * 17 * 8; i += blockDim.x) {
+			const int b = i / (17 * 8), c = (i >> 3) % 17, p = i & 7;
+			const uint32_t lo = c + p < 16 ? (uint32_t)a.thres[b][c + p] & 0xFFFFu : 0xFFFFu;
+			const uint32_t hi = c + p + 8 < 16 ? (uint32_t)a.thres[b][c + p + 8] & 0xFFFFu : 0xFFFFu;
+			s_tpk[b][i % (17 * 8)] = lo | (hi << 16);
+		}
+	}
+	static_assert(sizeof(SymTables) % 4 == 0 && sizeof(EnumSplit) % 4 == 0, "table words");
+	const uint32_t* sw = reinterpret_cast<const uint32_t*>(&kSymDevF);
+	uint32_t* dw = reinterpret_cast<uint32_t*>(&s_F.T);
+	for (int i = threadIdx.x; i < (int)(sizeof(SymTables) / 4); i += blockDim.x) dw[i] = sw[i];
+	sw = reinterpret_cast<const uint32_t*>(&kEnumDevF);
+	dw = reinterpret_cast<uint32_t*>(&s_F.E);
+	for (int i = threadIdx.x; i < (int)(sizeof(EnumSplit) / 4); i += blockDim.x) dw[i] = sw[i];
+}
+
+// interior (or, in border mode, every wave of the level): grid
+// (fs1 - fs0, ceil((fg1 - fg0) / 4)), one wave per segment
+template <int S>
+__global__ void __launch_bounds__(256, 3) k_fwdq_fast(FqArgs a, FqGrid g)
+{
+	__shared__ int s_thres[3][16];
+	__shared__ FqTables s_F __attribute__((aligned(16)));
+	__shared__ uint32_t s_tpk[3][17 * 8];
+	fq_stage_tables(a, s_thres, s_F, s_tpk);
+	__syncthreads();
+	const int lane = threadIdx.x & 63;
+	const int seg = g.fg0 + blockIdx.y * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+	if (seg >= g.fg1) return;
+	const int strip = g.fs0 + blockIdx.x;
+	const int X0 = strip * kFqStrip - 8, x = X0 + lane * 8, y0 = seg * S;
+	const int kx = strip * (kFqStrip / 8) + lane - 1;
+	FqBorder m;
+	m.top = y0 == 0;
+	m.bottom = y0 + S >= a.H;
+	if (g.border && (X0 < 0 || X0 + kLanes * 8 >= a.W || m.top || m.bottom)) {
+		m.eL0 = x == 0 ? 0x0000FFFFu : 0u;
+		m.oR3 = x + 7 == a.W - 1 ? 0xFFFF0000u : 0u;
+		m.ld = x >= 0 && x < a.W;
+		fq_seg<S, true>(a, s_thres, s_tpk, s_F, x, lane, y0, kx, m);
+	} else {
+		fq_seg<S, false>(a, s_thres, s_tpk, s_F, x, lane, y0, kx, m);
+	}
+}
+
+// frame: one wave per (strip, SE-row segment) unit outside the interior
+template <int SE>
+__global__ void __launch_bounds__(256) k_fwdq_edge(FqArgs a, FqGrid g)
+{
+	__shared__ int s_thres[3][16];
+	__shared__ FqTables s_F __attribute__((aligned(16)));
+	__shared__ uint32_t s_tpk[3][17 * 8];
+	fq_stage_tables(a, s_thres, s_F, s_tpk);
+	__syncthreads();
+	const int lane = threadIdx.x & 63;
+	const int u = blockIdx.x * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+	int strip, seg;
+	if (u < g.n_lr) {
+		const int k = u / g.nseg_e;
+		strip = g.lr_all ? k : k == 0 ? g.lr_strip[0] : k == 1 ? g.lr_strip[1] : g.lr_strip[2];
+		seg = u - k * g.nseg_e;
+	} else if (u < g.n_lr + g.n_tb) {
+		const int v = u - g.n_lr, k = v / g.ntb, r = v - k * g.ntb;
+		strip = g.fs0 + k;
+		seg = r < g.tseg ? r : g.bseg0 + (r - g.tseg);
+	} else {
+		return;
+	}
+	fq_edge<SE>(a, s_thres, s_tpk, s_F, lane, seg * SE, strip);
+}
+
+int fq_seg_rows(int H)
+{
+	static const int forced = [] { const char* e = getenv("RIC_FQ_S"); return e ? atoi(e) : 0; }();
+	if (forced == 16 || forced == 32) return forced;
+	return H >= 4096 ? 32 : 16;
+}
+
+constexpr int kFqEdgeRows = 8;
+
+FqGrid fq_grid(const FqArgs& a, int S)
+{
+	FqGrid g = {};
+	g.S = S;
+	g.nstrip = (a.W + kFqStrip - 1) / kFqStrip;
+	// interior strips: the whole 512-column wave (halo lanes included) inside
+	// the image, clear of column W-1; interior segments: halo rows inside and
+	// clear of the top/bottom boundary formulas
+	g.border = a.vec16 && a.nofast != 1 && a.W % 8 == 0 && a.H % 8 == 0;
+	if (g.border) {
+		// border mode: fq_seg<S, true> handles the image borders in registers
+		g.fs0 = 0; g.fs1 = g.nstrip;
+		g.fg0 = 0; g.fg1 = (a.H + S - 1) / S;
+		g.nseg_e = 0; g.tseg = g.bseg0 = 0; g.nlr_strips = 0; g.lr_all = 0; g.n_lr = g.ntb = g.n_tb = 0;
+		return g;
+	}
+	g.fs0 = 1; g.fs1 = 1;
+	while (g.fs1 * kFqStrip - 8 + kLanes * 8 < a.W) g.fs1++;
+	g.fg0 = (8 + S - 1) / S; g.fg1 = g.fg0;
+	while ((g.fg1 + 1) * S + 4 < a.H) g.fg1++;
+	if (!a.vec16 || a.nofast == 1 || g.fs1 <= g.fs0 || g.fg1 <= g.fg0) { g.fs0 = g.fs1 = 0; g.fg0 = g.fg1 = 0; }
+	g.se_rows = kFqEdgeRows;
+	g.nseg_e = (a.H + kFqEdgeRows - 1) / kFqEdgeRows;
+	const bool interior = g.fs1 > g.fs0;
+	g.tseg = interior ? g.fg0 * S / kFqEdgeRows : 0;
+	g.bseg0 = interior ? g.fg1 * S / kFqEdgeRows : 0;
+	g.nlr_strips = 0;
+	g.lr_all = !interior;
+	if (interior) {
+		for (int s = 0; s < g.nstrip; s++)
+			if (s < g.fs0 || s >= g.fs1) g.lr_strip[g.nlr_strips++] = s;   // at most 3 (fs0 = 1)
+	} else {
+		g.nlr_strips = g.nstrip;
+	}
+	g.n_lr = g.nlr_strips * g.nseg_e;
+	g.ntb = interior ? g.tseg + (g.nseg_e - g.bseg0) : 0;
+	g.n_tb = interior ? (g.fs1 - g.fs0) * g.ntb : 0;
+	return g;
+}
+
+template <int S>
+void fq_launch_s(FqArgs& a, hipStream_t st, hipStream_t st2, hipEvent_t fork, hipEvent_t join)
+{
+	a.nseg = (a.H + S - 1) / S;
+	const FqGrid g = fq_grid(a, S);
+	const int nedge = g.n_lr + g.n_tb;
+	const bool interior = g.fs1 > g.fs0;
+	if (interior && nedge > 0 && st2) {
+		(void)hipEventRecord(fork, st);
+		(void)hipStreamWaitEvent(st2, fork, 0);
+	}
+	hipStream_t se = (interior && st2) ? st2 : st;
+	if (nedge > 0 && a.nofast != 2)
+		hipLaunchKernelGGL(k_fwdq_edge<kFqEdgeRows>, dim3((nedge + kWavesPerBlock - 1) / kWavesPerBlock), dim3(256), 0, se, a, g);
+	if (interior)
+		hipLaunchKernelGGL(k_fwdq_fast<S>, dim3(g.fs1 - g.fs0, (g.fg1 - g.fg0 + kWavesPerBlock - 1) / kWavesPerBlock),
+		                   dim3(256), 0, st, a, g);
+	if (interior && nedge > 0 && st2) {
+		(void)hipEventRecord(join, st2);
+		(void)hipStreamWaitEvent(st, join, 0);
+	}
+}
+
 // ---------------------------------------------------------- inverse level
 template <typename TB, typename TL, typename TO>
 struct InvArgs {
@@ -1108,6 +1683,42 @@ void launch_fwd_level(const Level& L, const void* src, long sp, char* arena, int
 	if (trans == CDF97) fwd_dispatch<CDF97>(L, src, sp, arena, vec, st);
 	else if (trans == CDF53) fwd_dispatch<CDF53>(L, src, sp, arena, vec, st);
 	else fwd_dispatch<HAAR>(L, src, sp, arena, vec, st);
+}
+
+bool fwdq_supported(const Level& L, int trans, const QuantParams& qp)
+{
+	static const bool off = [] { const char* e = getenv("RIC_NOFUSE"); return e && atoi(e) != 0; }();
+	return !off && trans == CDF97 && !L.in_is_int && !L.is_int && pk_ok(qp.thres[0]) && pk_ok(qp.thres[1]) &&
+	       pk_ok(qp.thres[2]);
+}
+
+void launch_fwdq_level(const Pyramid& P, int l, const void* src, long sp, int vec8, int vec16, const QuantParams& qp,
+                       char* arena, hipStream_t st, hipStream_t st2, hipEvent_t fork, hipEvent_t join)
+{
+	const Level& L = P.L[l];
+	FqArgs a;
+	a.src = (const int16_t*)src; a.sp = sp; a.W = L.w; a.H = L.h;
+	a.vec8 = vec8; a.vec16 = vec16; a.nofast = dbg_nofast(); a.high = l == 0;
+	for (int b = 0; b < 4; b++) { a.d[b] = (int16_t*)(arena + L.b[b].off); a.p[b] = L.b[b].pitch; }
+	for (int b = 0; b < 3; b++) {
+		const Band& B = L.b[b];
+		a.dx[b] = B.dx; a.dy[b] = B.dy; a.bw[b] = B.bw(); a.bh[b] = B.bh();
+		a.rd[b] = (uint32_t*)(arena + B.rd_off);
+		a.rec[b] = (uint64_t*)(arena + P.rec_off[l][b]);
+		if (l > 0) {
+			const Band& C = P.L[l - 1].b[b];
+			a.crd[b] = (const uint32_t*)(arena + C.rd_off); a.cbw[b] = C.bw();
+			a.cpin[b] = (uint8_t*)(arena + P.pin_off[l - 1][b]); a.cpw[b] = C.bw(); a.cph[b] = C.bh();
+		} else {
+			a.crd[b] = nullptr; a.cbw[b] = 0;
+			a.cpin[b] = nullptr; a.cpw[b] = 0; a.cph[b] = 0;
+		}
+		a.Q[b] = qp.Q[b]; a.iQ[b] = qp.iQ[b];
+		for (int i = 0; i < 16; i++) a.thres[b][i] = qp.thres[b][i];
+	}
+	const int S = fq_seg_rows(L.h);
+	if (S == 32) fq_launch_s<32>(a, st, st2, fork, join);
+	else fq_launch_s<16>(a, st, st2, fork, join);
 }
 
 void launch_inv_level(const Level& L, const Band& lls, char* arena, void* out, long po, int out_is_int,

@@ -3,8 +3,7 @@
 // Restates CBandCodec::tree<encode> (src/lib/bandcodec.cpp:484-589), CBitCodec
 // / CGeomCodec code (src/lib/bitcodec.h:52-60, geomcodec.h:41-57) and CMuxCodec
 // codeBin / bitsCode / normalize_enc / flushBuffer (src/lib/muxcodec.h:156-231,
-// muxcodec.cpp:63-74, 536-570).  Output is byte-identical to entropy.cpp's
-// tree_encode_records (and to the reference).
+// muxcodec.cpp:63-74, 536-570).  Output is byte-identical to the reference's tree<encode>.
 #include "entropy.h"
 #include "symbols.h"
 
@@ -115,8 +114,8 @@ struct GeoE {                                             // CGeomCodec::code
 	}
 };
 
-template <typename C, bool HIGH>
-void tree_rec_fast(Mux& m, const uint64_t* rec, const BandView& b)
+template <typename C, bool HIGH, bool PAR>
+void tree_rec_fast(Mux& m, const uint64_t* rec, const uint8_t* pin, const BandView& b)
 {
 	constexpr bool SH = sizeof(C) == 2;
 	static const uint8_t ginit[16] = {5,9,9,9,9,9,9,9,9,9,9,9,10,10,10,11};   // bandcodec.cpp:487
@@ -128,13 +127,13 @@ void tree_rec_fast(Mux& m, const uint64_t* rec, const BandView& b)
 	const C* band = (const C*)b.p;
 	const long st = b.pitch;
 	const int bw = (b.dx + 3) >> 2, bh = (b.dy + 3) >> 2, nfx = b.dx >> 2;
-	long s = 0;
 	for (int by = 0; by < bh; by++) {
 		const C* row = band + (long)by * 4 * st;
-		for (int p = 0; p < bw; p++, s++) {
-			const uint64_t r = rec[s];
-			if (BlockRec::prop(r)) continue;
+		const long rb = (long)by * bw;
+		for (int p = 0; p < bw; p++) {
+			// serpentine scan (bandcodec.cpp:509-523); records are in raster order
 			const int bx = !(by & 1) ? p : (nfx < bw ? (p == 0 ? nfx : nfx - p) : nfx - 1 - p);
+			const uint64_t r = rec[rb + bx];
 			const C* blk = row + bx * 4;
 			const uint32_t ins = BlockRec::insig(r);
 			uint32_t mask = BlockRec::mask(r);
@@ -150,7 +149,12 @@ void tree_rec_fast(Mux& m, const uint64_t* rec, const BandView& b)
 					g.code_signed(e, (uc<SH>(v) >> 1) - 1, v & 1, gc);
 				}
 			} else {
-				const int ctx = BlockRec::ctx(r);
+				int ctx = 15;
+				if (PAR) {
+					const uint32_t pi = pin[rb + bx];
+					if (BlockRec::pin_prop(pi)) continue;
+					ctx = (int)BlockRec::pin_ctx(pi);
+				}
 				tree.code(e, ins, ctx);
 				if (ins) continue;
 				const uint32_t k = BlockRec::k(r);
@@ -173,12 +177,19 @@ void tree_rec_fast(Mux& m, const uint64_t* rec, const BandView& b)
 	m.set_enc_state(e.s);
 }
 
+template <typename C, bool HIGH>
+void tree_rec_disp(Mux& m, const uint64_t* rec, const uint8_t* pin, const BandView& b)
+{
+	if (pin) tree_rec_fast<C, HIGH, true>(m, rec, pin, b);
+	else tree_rec_fast<C, HIGH, false>(m, rec, pin, b);
+}
+
 }  // namespace
 
-void tree_encode_records_fast(Mux& m, const uint64_t* rec, const BandView& b, bool high)
+void tree_encode_records_fast(Mux& m, const uint64_t* rec, const uint8_t* pin, const BandView& b, bool high)
 {
-	if (b.is_int) { if (high) tree_rec_fast<int32_t, true>(m, rec, b); else tree_rec_fast<int32_t, false>(m, rec, b); }
-	else { if (high) tree_rec_fast<int16_t, true>(m, rec, b); else tree_rec_fast<int16_t, false>(m, rec, b); }
+	if (b.is_int) { if (high) tree_rec_disp<int32_t, true>(m, rec, pin, b); else tree_rec_disp<int32_t, false>(m, rec, pin, b); }
+	else { if (high) tree_rec_disp<int16_t, true>(m, rec, pin, b); else tree_rec_disp<int16_t, false>(m, rec, pin, b); }
 }
 
 }  // namespace ric

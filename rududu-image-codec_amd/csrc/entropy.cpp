@@ -651,72 +651,7 @@ void tree_dispatch(Mux& m, const BandView& b, const BandView& par, bool high, bo
 	}
 }
 
-// CBandCodec::tree<encode> over the GPU block records (symbols.h).  Only the
-// adaptive state and the coder run here: tree/border bins, the Huffman table
-// choice from k_mean, the geometric codes of the coefficients.
-template <typename C, bool HIGH>
-void tree_rec_t(Mux& m, const uint64_t* rec, const BandView& b)
-{
-	constexpr bool SH = is_short<C>();
-	static const uint8_t ginit[16] = {5,9,9,9,9,9,9,9,9,9,9,9,10,10,10,11};   // bandcodec.cpp:487
-	uint16_t kmean[16] = {2 << 10, 3 << 10, 4 << 10, 5 << 10, 8 << 10, 11 << 10, 13 << 10, 14 << 10,
-	                      15 << 10, 15 << 10, 15 << 10, 15 << 10, 15 << 10, 15 << 10, 15 << 10, 15 << 10};
-	GeomModel g; g.init(ginit);
-	BitModel tree, bord; tree.init(); bord.init();
-	const C* band = (const C*)b.p;
-	const long st = b.pitch;
-	const int bw = (b.dx + 3) >> 2, bh = (b.dy + 3) >> 2, nfx = b.dx >> 2;
-	long s = 0;
-	for (int by = 0; by < bh; by++) {
-		const C* row = band + (long)by * 4 * st;
-		for (int p = 0; p < bw; p++, s++) {
-			const uint64_t r = rec[s];
-			if (BlockRec::prop(r)) continue;
-			const int bx = !(by & 1) ? p : (nfx < bw ? (p == 0 ? nfx : nfx - p) : nfx - 1 - p);
-			const C* blk = row + bx * 4;
-			const uint32_t ins = BlockRec::insig(r);
-			uint32_t mask = BlockRec::mask(r);
-			if (BlockRec::edge(r)) {
-				bord.code(m, ins, 0);
-				if (ins) continue;
-				m.bits_code(BlockRec::raw(r), BlockRec::rawlen(r));
-				const int w = BlockRec::w(r), gc = BlockRec::gctx(r);
-				while (mask) {
-					const int i = __builtin_ctz(mask);
-					mask &= mask - 1;
-					const int v = blk[(i / w) * st + (i % w)];
-					g.code_signed(m, (uc<SH>(v) >> 1) - 1, v & 1, gc);
-				}
-			} else {
-				const int ctx = BlockRec::ctx(r);
-				tree.code(m, ins, ctx);
-				if (ins) continue;
-				const uint32_t k = BlockRec::k(r);
-				const int idx = (kmean[ctx] + (1 << 9)) >> 10;
-				const uint16_t e = HIGH ? kHuff_HIGH[idx][k - 1] : kHuff_LOW[idx][k];
-				const uint32_t rl = BlockRec::rawlen(r);
-				m.bits_code(((uint32_t)(e >> 5) << rl) | BlockRec::raw(r), (e & 31) + rl);
-				const int gc = (int)k - 1;
-				while (mask) {
-					const int i = __builtin_ctz(mask);
-					mask &= mask - 1;
-					const int v = blk[(i >> 2) * st + (i & 3)];
-					g.code_signed(m, (uc<SH>(v) >> 1) - 1, v & 1, gc);
-				}
-				const uint32_t kk = k - (HIGH ? 1 : 0);
-				kmean[ctx] = (uint16_t)(kmean[ctx] + (kk << 7) - (kmean[ctx] >> 3));
-			}
-		}
-	}
-}
-
 }  // namespace
-
-void tree_encode_records(Mux& m, const uint64_t* rec, const BandView& b, bool high)
-{
-	if (b.is_int) { if (high) tree_rec_t<int32_t, true>(m, rec, b); else tree_rec_t<int32_t, false>(m, rec, b); }
-	else { if (high) tree_rec_t<int16_t, true>(m, rec, b); else tree_rec_t<int16_t, false>(m, rec, b); }
-}
 
 void pred_encode(Mux& m, const BandView& b)
 {

@@ -158,9 +158,9 @@ void tree_decode(Mux& m, const BandView& b, const BandView& par, bool high, bool
 // Register-resident decoder of one band (decoder.cpp), same semantics as
 // tree_decode.
 void tree_decode_fast(Mux& m, const BandView& b, const BandView& par, bool high, bool has_child);
-// Encoder over GPU block records (symbols.h): rec[s] for scan position s.
-void tree_encode_records(Mux& m, const uint64_t* rec, const BandView& b, bool high);
-// Same, with the coder state in registers (encoder.cpp).
-void tree_encode_records_fast(Mux& m, const uint64_t* rec, const BandView& b, bool high);
+// Encoder over GPU block records (symbols.h), coder state in registers
+// (encoder.cpp): rec / pin in raster block order; pin == nullptr for a band
+// without a parent (the coarsest level).
+void tree_encode_records_fast(Mux& m, const uint64_t* rec, const uint8_t* pin, const BandView& b, bool high);
 
 }  // namespace ric

@@ -3,16 +3,14 @@
 //
 // k_quant_level restates CBandCodec::buildTree / tsuqBlock / makeThres
 // (src/lib/bandcodec.cpp:149-319) for the D, H and V bands of one level: one
-// lane per 4x4 block, the 16 coefficients held in registers.  The reference's
-// stable insertion sort of the RD candidates followed by the suffix
-// thresholding (bandcodec.cpp:115-127, 188-198) becomes a 16-key bitonic
-// network on packed (key << 4 | 15 - index) words: a candidate survives iff its
-// packed key is >= the smallest packed key whose sorted rank r fails
-// `key < rd_thres[r + cnt]`.  Levels run finest -> coarsest because a parent's
-// significance adds its four children's pRD (bandcodec.cpp:267-269).
+// lane per 4x4 block, the 16 coefficients held in registers (quant_block.h).
+// Levels run finest -> coarsest because a parent's significance adds its four
+// children's pRD (bandcodec.cpp:267-269).  It serves the levels the fused
+// forward+quantiser (dwt.hip k_fwdq) does not cover.
 #include <hip/hip_runtime.h>
 #include "ric_types.h"
 #include "ric_kernels.h"
+#include "quant_block.h"
 
 namespace ric {
 
@@ -28,36 +26,6 @@ struct QArgs {
 	int Q[3], iQ[3];
 	int thres[3][16];
 };
-
-template <bool SH>
-__device__ __forceinline__ int quant_mag(int v, int iQ)
-{
-	// (tmp * iQuant + (1 << 15)) >> 16 with x86 wrap-around semantics
-	int tmp = (int)(uc<SH>(v) >> 1);
-	int q = (int)((uint32_t)tmp * (uint32_t)iQ + 32768u) >> 16;
-	return tr<SH>((q << 1) | (v & 1));
-}
-
-__device__ __forceinline__ void sort16_desc(uint32_t (&s)[16])
-{
-#pragma unroll
-	for (int k = 2; k <= 16; k <<= 1) {
-#pragma unroll
-		for (int j = k >> 1; j > 0; j >>= 1) {
-#pragma unroll
-			for (int i = 0; i < 16; i++) {
-				int l = i ^ j;
-				if (l > i) {
-					uint32_t a = s[i], b = s[l];
-					bool desc = (i & k) == 0;
-					uint32_t hi = a > b ? a : b, lo = a > b ? b : a;
-					s[i] = desc ? hi : lo;
-					s[l] = desc ? lo : hi;
-				}
-			}
-		}
-	}
-}
 
 template <typename T>
 __global__ void __launch_bounds__(256) k_quant_level(QArgs a, int nblk)
@@ -92,48 +60,7 @@ __global__ void __launch_bounds__(256) k_quant_level(QArgs a, int nblk)
 				v[4 * r + 0] = u.x; v[4 * r + 1] = u.y; v[4 * r + 2] = u.z; v[4 * r + 3] = u.w;
 			}
 		}
-		const int T0 = tr<SH>(Q >> 1);
-		const uint32_t th0 = uc<SH>(s_thres[b][0]);
-		int cnt = 0, ncand = 0;
-		uint32_t key[16];
-#pragma unroll
-		for (int i = 0; i < 16; i++) {
-			key[i] = 0;
-			int x = v[i];
-			if ((uint32_t)(x + T0) <= (uint32_t)(2 * T0)) { v[i] = 0; continue; }
-			x = tr<SH>(s2u_(x));
-			if (uc<SH>(x) < th0) {
-				v[i] = x;
-				key[i] = (uc<SH>(x) << 4) | (uint32_t)(15 - i);
-				ncand++;
-			} else {
-				cnt++;
-				v[i] = quant_mag<SH>(x, iQ);
-			}
-		}
-		if (ncand) {
-			uint32_t s[16];
-#pragma unroll
-			for (int i = 0; i < 16; i++) s[i] = key[i];
-			sort16_desc(s);
-			uint32_t thr = 0xFFFFFFFFu;
-#pragma unroll
-			for (int r = 0; r < 16; r++) {
-				if (r < ncand) {
-					int kv = tr<SH>((int)(s[r] >> 4));
-					if (!(kv < s_thres[b][r + cnt])) thr = s[r];
-				}
-			}
-			int surv = 0;
-#pragma unroll
-			for (int i = 0; i < 16; i++) {
-				if (key[i]) {
-					if (key[i] >= thr) { v[i] = tr<SH>(2 | (v[i] & 1)); surv++; }
-					else v[i] = 0;
-				}
-			}
-			cnt += surv;
-		}
+		int cnt = tsuq_full<SH>(v, Q, iQ, s_thres[b]);
 		uint64_t d = (uint64_t)cnt;
 		if (a.crd[b]) {
 			const uint32_t* c0 = a.crd[b] + (long)(2 * ky) * a.cbw[b];
@@ -156,17 +83,12 @@ __global__ void __launch_bounds__(256) k_quant_level(QArgs a, int nblk)
 	} else {
 		// edge tsuqBlock, src/lib/bandcodec.cpp:215-237 (children ignored)
 		int wdt = min(4, dx - x0), hgt = min(4, dy - y0);
-		const int T0 = tr<SH>((Q + ((Q - (Q >> 2)) >> 1)) >> 1);
-		int cnt = 0;
+		int v[16];
+#pragma unroll
+		for (int i = 0; i < 16; i++) v[i] = ((i >> 2) < hgt && (i & 3) < wdt) ? (int)base[(long)(i >> 2) * pitch + (i & 3)] : 0;
+		int cnt = tsuq_edge<SH>(v, wdt, hgt, Q, iQ);
 		for (int r = 0; r < hgt; r++)
-			for (int c = 0; c < wdt; c++) {
-				T* p = base + (long)r * pitch + c;
-				int x = *p;
-				if ((uint32_t)(x + T0) <= (uint32_t)(2 * T0)) { *p = 0; continue; }
-				x = tr<SH>(s2u_(x));
-				cnt++;
-				*p = (T)quant_mag<SH>(x, iQ);
-			}
+			for (int c = 0; c < wdt; c++) base[(long)r * pitch + c] = (T)v[4 * r + c];
 		dist = (uint32_t)cnt;
 		if (dist == 0) *base = (T)kInsignif;
 	}

@@ -9,6 +9,16 @@ namespace ric {
 // level's D/H/V/L bands in the arena.  vec: src rows are 8/16-byte aligned.
 void launch_fwd_level(const Level& L, const void* src, long sp, char* arena, int trans, int vec,
                       hipStream_t st);
+// Fused forward level + quantiser + block records (dwt.hip k_fwdq): the 9/7
+// short->short levels.  Writes level l's quantised D/H/V bands, pRD, block-local
+// records, its unquantised LL, and (l > 0) the parent info of level l-1.
+struct QuantParams;
+// 9/7 short->short levels whose rd thresholds suit the packed quantiser
+bool fwdq_supported(const Level& L, int trans, const QuantParams& qp);
+// The border frame runs on st2 (forked from st by `fork`, joined back by
+// `join`), concurrently with the interior on st; st2 == nullptr: all on st.
+void launch_fwdq_level(const Pyramid& P, int l, const void* src, long sp, int vec8, int vec16, const QuantParams& qp,
+                       char* arena, hipStream_t st, hipStream_t st2, hipEvent_t fork, hipEvent_t join);
 // Inverse level: D/H/V bands + lls (the level's LL) -> out (pitch po elements),
 // typed int32 if out_is_int else int16.
 void launch_inv_level(const Level& L, const Band& lls, char* arena, void* out, long po,
@@ -26,7 +36,9 @@ void launch_quant_level(const Pyramid& P, int l, const QuantParams& qp, char* ar
 void launch_quant_ll(const Pyramid& P, int Q, int iQ, int T, char* arena, hipStream_t st);
 // Zerotree block records of the D/H/V bands of level l (symbols.h), written
 // at P.rec_off[l][b]; needs every level quantised (parents are read).
-void launch_blocks_level(const Pyramid& P, int l, char* arena, hipStream_t st);
+// do_rec: the block-local records of level l; do_pin: the parent info of
+// level l's blocks, read from level l+1's quantised bands.
+void launch_blocks_level(const Pyramid& P, int l, bool do_rec, bool do_pin, char* arena, hipStream_t st);
 // CBand::TSUQ on one band, adding its non-zero count to *count (device).
 void launch_tsuq_band(const Band& B, int iQ, int T0, char* arena, unsigned int* count, hipStream_t st);
 // CBand::TSUQi on one band (src/lib/band.h:94-107).

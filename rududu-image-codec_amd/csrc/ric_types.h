@@ -12,6 +12,12 @@
 #define RIC_HD inline
 #endif
 
+#if defined(__clang__)
+#define RIC_UNROLL _Pragma("unroll")
+#else
+#define RIC_UNROLL _Pragma("GCC unroll 16")
+#endif
+
 namespace ric {
 
 constexpr int kMaxLevels = 16;
@@ -37,6 +43,7 @@ RIC_HD int s2u(int s) { int u = (int)(0u - (2u * (uint32_t)s + 1u)); return u ^ 
 RIC_HD int u2s(int u) { return (u >> 1) ^ -(u & 1); }
 RIC_HD int s2u_(int s) { int m = s >> 31; return (int)(2u * (uint32_t)s + (uint32_t)m) ^ (m * 2); }
 RIC_HD int u2s_(int u) { int m = -(u & 1); return ((u >> 1) + m) ^ m; }
+RIC_HD uint32_t popc32(uint32_t m) { return (uint32_t)__builtin_popcount(m); }
 RIC_HD int bitlen(uint32_t v) { return v ? 32 - __builtin_clz(v) : 0; }
 
 // One band of the pyramid in the device/host arenas.
@@ -64,7 +71,8 @@ struct Level {
 // CWavelet2D::Init geometry (src/lib/wavelet2d.cpp:69-81, src/lib/band.cpp:51-65).
 // Arena layout (one allocation on the device, a pinned mirror on the host):
 //   region A [0, a_end):     the coded bands (D/H/V of every level + coarsest LL)
-//   region B [a_end, b_end): per-block zerotree records of the 3*nlev high bands
+//   region B [a_end, b_end): per-block zerotree records + parent info of the
+//                            3*nlev high bands
 //   region C [b_end, end):   device-only scratch: intermediate LL planes, pRD
 // Encode copies A+B to the host, decode copies A back to the device.
 struct Pyramid {
@@ -72,7 +80,8 @@ struct Pyramid {
 	int w = 0, h = 0, levels = 0, lc = 0;
 	Level L[kMaxLevels];
 	size_t arena_bytes = 0, a_end = 0, b_end = 0;
-	size_t rec_off[kMaxLevels][3] = {};
+	size_t rec_off[kMaxLevels][3] = {};   // u64 block records (symbols.h), raster order
+	size_t pin_off[kMaxLevels][3] = {};   // u8 parent info per block (symbols.h), raster order
 
 	void build(int w_, int h_, int levels_, int lc_)
 	{
@@ -109,6 +118,8 @@ struct Pyramid {
 		a_end = off;
 		for (int l = 0; l < nlev; l++)
 			for (int b = 0; b < 3; b++) rec_off[l][b] = take((size_t)L[l].b[b].bw() * L[l].b[b].bh() * 8);
+		for (int l = 0; l < nlev; l++)
+			for (int b = 0; b < 3; b++) pin_off[l][b] = take((size_t)L[l].b[b].bw() * L[l].b[b].bh());
 		b_end = off;
 		for (int l = 0; l + 1 < nlev; l++) L[l].b[BL].off = take(L[l].b[BL].bytes());
 		for (int l = 0; l < nlev; l++)

@@ -4,8 +4,9 @@
   python scripts/kbench.py [--iters N] [--width W --height H] [--codec]
 
 Times the device stages in isolation with the library's HIP-event stage
-timers: forward DWT (level 0 and all levels) + quantiser/records
-(ric_quantize), then, with --codec, one full encode+decode per iteration on a
+timers: the fused forward DWT + quantiser + records (ric_transform_quantize;
+"fwd_l0" = the level-0 kernel, "fwd" = the whole device encode, "quant" =
+nothing unless RIC_NOFUSE=1 splits it off), then, with --codec, one full encode+decode per iteration on a
 single codec (stage breakdown incl. the host coder).  Used for kernel tuning
 and under rocprofv3; bench.py is the contract benchmark.
 """
@@ -43,8 +44,7 @@ def main():
     for i in range(a.warmup + a.iters):
         if i == a.warmup:
             w.prof_enable(True)
-        w.Transform(img, W, 0, on_device=True)
-        w.Quantize(q, lam)
+        w.TransformQuantize(img, W, 0, q, lam, on_device=True)
         w.prof_read()
     st = w.prof_read()
     out["wavelet_ms"] = {k: round(v[0] / v[1], 4) for k, v in st.items() if v[1]}

@@ -55,31 +55,37 @@ struct HostPyr {
 			}
 		}
 	}
-	// block records computed on the CPU with the same function the GPU runs
+	// block records + parent info computed on the CPU with the same functions
+	// the GPU runs (symbols.h), raster block order
 	std::vector<std::vector<uint64_t>> recs;
+	std::vector<std::vector<uint8_t>> pins;
+	template <typename P>
+	void pin_band(std::vector<uint8_t>& R, const Band& B, const Band& Q) {
+		const P* pp = (const P*)(arena.data() + Q.off);
+		for (int by = 0; by < B.bh(); by++)
+			for (int bx = 0; bx < B.bw(); bx++)
+				R[(size_t)by * B.bw() + bx] = (uint8_t)parent_info<P>(pp, Q.pitch, Q.dx, Q.dy, bx, by);
+	}
 	void build_records() {
 		const SymTables& T = host_sym_tables();
 		recs.assign(3 * P.nlev, {});
+		pins.assign(3 * P.nlev, {});
 		for (int l = 0; l < P.nlev; l++)
 			for (int b = 0; b < 3; b++) {
 				Band& B = P.L[l].b[b];
 				std::vector<uint64_t>& R = recs[3 * l + b];
 				R.resize((size_t)B.bw() * B.bh());
-				const bool hp = l + 1 < P.nlev;
-				Band* Q = hp ? &P.L[l + 1].b[b] : nullptr;
-				for (size_t s = 0; s < R.size(); s++) {
-					int bx, by;
-					scan_block((int)s, B.dx, B.dy, bx, by);
-					const char* bp = arena.data() + B.off;
-					const char* pp = hp ? arena.data() + Q->off : nullptr;
-					const int pst = hp ? Q->pitch : 0, pdx = hp ? Q->dx : 0, pdy = hp ? Q->dy : 0;
-					const bool pint = hp ? Q->is_int : B.is_int;
-					if (!B.is_int && !pint)
-						R[s] = block_record<int16_t, int16_t>(T, (const int16_t*)bp, B.pitch, B.dx, B.dy, (const int16_t*)pp, pst, pdx, pdy, l == 0, bx, by);
-					else if (!B.is_int)
-						R[s] = block_record<int16_t, int32_t>(T, (const int16_t*)bp, B.pitch, B.dx, B.dy, (const int32_t*)pp, pst, pdx, pdy, l == 0, bx, by);
-					else
-						R[s] = block_record<int32_t, int32_t>(T, (const int32_t*)bp, B.pitch, B.dx, B.dy, (const int32_t*)pp, pst, pdx, pdy, l == 0, bx, by);
+				const char* bp = arena.data() + B.off;
+				for (int by = 0; by < B.bh(); by++)
+					for (int bx = 0; bx < B.bw(); bx++)
+						R[(size_t)by * B.bw() + bx] = B.is_int
+							? block_local<int32_t>(T, (const int32_t*)bp, B.pitch, B.dx, B.dy, l == 0, bx, by)
+							: block_local<int16_t>(T, (const int16_t*)bp, B.pitch, B.dx, B.dy, l == 0, bx, by);
+				if (l + 1 < P.nlev) {
+					Band& Q = P.L[l + 1].b[b];
+					pins[3 * l + b].resize(R.size());
+					if (Q.is_int) pin_band<int32_t>(pins[3 * l + b], B, Q);
+					else pin_band<int16_t>(pins[3 * l + b], B, Q);
 				}
 			}
 	}
@@ -88,7 +94,9 @@ struct HostPyr {
 		for (int l = P.nlev - 1; l >= 0; l--) {
 			const int order[3] = {BV, BH, BD};
 			for (int k = 0; k < 3; k++)
-				tree_encode_records_fast(m, recs[3 * l + order[k]].data(), view(P.L[l].b[order[k]]), l == 0);
+				tree_encode_records_fast(m, recs[3 * l + order[k]].data(),
+				                         l + 1 < P.nlev ? pins[3 * l + order[k]].data() : nullptr,
+				                         view(P.L[l].b[order[k]]), l == 0);
 		}
 	}
 	void decode(Mux& m) {
