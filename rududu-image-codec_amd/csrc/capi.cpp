@@ -104,10 +104,6 @@ struct ric_wavelet {
 	size_t img_pitch = 0;             // elements
 	hipStream_t st = nullptr;
 	bool own_stream = false;
-	// second stream for the border-frame kernels of the fused forward levels,
-	// forked from / joined back to st by events
-	hipStream_t st2 = nullptr;
-	hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 	bool host_valid = false;          // bands live on the host (after a decode)
 	// A Transform of a host image is deferred until the next call, so that a
 	// CodeBand right after it runs as one fused forward+quantiser pass.
@@ -233,14 +229,19 @@ QuantParams level_qp(const Pyramid& P, int l, int& qin, int lambda)
 	return qp;
 }
 
-// CBand::TSUQ on the coarsest LL with Thres 0.5 (band.h:65-92)
-void quant_ll(ric_wavelet* w, int quant)
+// CBand::TSUQ on the coarsest LL with Thres 0.5 (band.h:65-92): parameters
+void ll_params(ric_wavelet* w, int quant, int& Q, int& iQ, int& T0)
 {
 	Band& B = w->P.coarsest_ll();
-	int Q = (int)((float)quant / B.weight);
+	Q = (int)((float)quant / B.weight);
 	if (Q == 0) Q = 1;
-	int iQ = (1 << 16) / Q;
-	int T0 = tr_any(!B.is_int, (int)(0.5f * (float)Q));
+	iQ = (1 << 16) / Q;
+	T0 = tr_any(!B.is_int, (int)(0.5f * (float)Q));
+}
+void quant_ll(ric_wavelet* w, int quant)
+{
+	int Q, iQ, T0;
+	ll_params(w, quant, Q, iQ, T0);
 	launch_quant_ll(w->P, Q, iQ, T0, w->d_arena, w->st);
 }
 
@@ -273,6 +274,7 @@ int encode_gpu(ric_wavelet* w, const int16_t* dimg, long stride, int trans, int 
 {
 	Pyramid& P = w->P;
 	bool fused[kMaxLevels] = {};
+	bool ll_done = false;
 	int qin = quant;
 	w->prof.begin(S_FWD, w->st);
 	for (int l = 0; l < P.nlev; l++) {
@@ -288,17 +290,23 @@ int encode_gpu(ric_wavelet* w, const int16_t* dimg, long stride, int trans, int 
 			src = w->d_arena + LL.off; sp = LL.pitch; vec8 = vec16 = 1;
 		}
 		QuantParams qp = level_qp(P, l, qin, lambda);
-		fused[l] = fwdq_supported(P.L[l], trans, qp);
+		const int mode = fwdq_mode(P.L[l], trans, qp, vec16);
+		fused[l] = mode != FQ_NONE;
 		if (l == 0) w->prof.begin(S_FWD0, w->st);
-		if (fused[l]) {
-			launch_fwdq_level(P, l, src, sp, vec8, vec16, qp, w->d_arena, w->st, w->st2, w->ev_fork, w->ev_join);
+		if (mode == FQ_PACKED) {
+			launch_fwdq_level(P, l, src, sp, vec8, vec16, qp, w->d_arena, w->st);
+		} else if (mode == FQ_GENERIC) {
+			const bool coarsest = l + 1 == P.nlev;
+			int llQ = 0, lliQ = 0, llT0 = 0;
+			if (coarsest) { ll_params(w, quant, llQ, lliQ, llT0); ll_done = true; }
+			launch_fwdq_gen_level(P, l, src, sp, vec8, qp, coarsest, lliQ, llT0, w->d_arena, w->st);
 		} else {
 			launch_fwd_level(P.L[l], src, sp, w->d_arena, trans, vec8, w->st);
 			launch_quant_level(P, l, qp, w->d_arena, w->st);
 		}
 		if (l == 0) w->prof.end(S_FWD0, w->st);
 	}
-	quant_ll(w, quant);
+	if (!ll_done) quant_ll(w, quant);
 	// records of the unfused levels, parent info below the unfused levels
 	for (int l = 0; l < P.nlev; l++)
 		launch_blocks_level(P, l, !fused[l], l + 1 < P.nlev && !fused[l + 1], w->d_arena, w->st);
@@ -442,9 +450,6 @@ int ric_wavelet_create(ric_wavelet** out, int x, int y, int level, int level_chg
 	if (hip_fail(hipMalloc(&w->d_arena, w->P.arena_bytes), "hipMalloc arena") ||
 	    hip_fail(hipHostMalloc(&w->h_arena, w->P.arena_bytes, 0), "hipHostMalloc arena") ||
 	    hip_fail(hipStreamCreateWithFlags(&w->st, hipStreamNonBlocking), "hipStreamCreate") ||
-	    hip_fail(hipStreamCreateWithFlags(&w->st2, hipStreamNonBlocking), "hipStreamCreate") ||
-	    hip_fail(hipEventCreateWithFlags(&w->ev_fork, hipEventDisableTiming), "hipEventCreate") ||
-	    hip_fail(hipEventCreateWithFlags(&w->ev_join, hipEventDisableTiming), "hipEventCreate") ||
 	    hip_fail(hipMemsetAsync(w->d_arena, 0, w->P.arena_bytes, w->st), "hipMemset arena") ||
 	    hip_fail(hipStreamSynchronize(w->st), "hipStreamSynchronize")) {
 		ric_wavelet_destroy(w);
@@ -466,9 +471,6 @@ void ric_wavelet_destroy(ric_wavelet* w)
 	if (w->d_img) (void)hipFree(w->d_img);
 	if (w->h_arena) (void)hipHostFree(w->h_arena);
 	if (w->own_stream && w->st) (void)hipStreamDestroy(w->st);
-	if (w->st2) { (void)hipStreamSynchronize(w->st2); (void)hipStreamDestroy(w->st2); }
-	if (w->ev_fork) (void)hipEventDestroy(w->ev_fork);
-	if (w->ev_join) (void)hipEventDestroy(w->ev_join);
 	delete w;
 }
 

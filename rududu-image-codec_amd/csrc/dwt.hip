@@ -31,21 +31,21 @@ constexpr int kCols = 4;                          // columns per lane
 constexpr int kStripValid = (kLanes - 2) * kCols; // 248 valid output columns per wave
 constexpr int kWavesPerBlock = 4;
 
+// Bounds-checked loads are branch-free -- clamped addresses, then a select:
+// a divergent vector-or-scalar branch makes the compiler drain every load at
+// the join, one memory round trip per row.
+// (the empty asm pins the load: otherwise it is sunk back under the condition)
+__device__ __forceinline__ int pinned(int v) { asm("" : "+v"(v)); return v; }
+
 template <typename T>
 __device__ __forceinline__ void load4(const T* __restrict__ row, int x, int W, bool vec, int (&c)[4])
 {
-	if (vec && x >= 0 && x + 3 < W) {
-		if constexpr (sizeof(T) == 2) {
-			uint2 u = *reinterpret_cast<const uint2*>(row + x);
-			c[0] = (int16_t)(u.x & 0xffff); c[1] = (int16_t)(u.x >> 16);
-			c[2] = (int16_t)(u.y & 0xffff); c[3] = (int16_t)(u.y >> 16);
-		} else {
-			int4 u = *reinterpret_cast<const int4*>(row + x);
-			c[0] = u.x; c[1] = u.y; c[2] = u.z; c[3] = u.w;
-		}
-	} else {
+	(void)vec;
 #pragma unroll
-		for (int j = 0; j < 4; j++) c[j] = (x + j >= 0 && x + j < W) ? (int)row[x + j] : 0;
+	for (int j = 0; j < 4; j++) {
+		const int xj = x + j;
+		const int v = pinned((int)row[min(max(xj, 0), W - 1)]);
+		c[j] = (xj >= 0 && xj < W) ? v : 0;
 	}
 }
 
@@ -67,19 +67,10 @@ __device__ __forceinline__ void store2(T* __restrict__ row, int bx, int dx, int 
 template <typename T>
 __device__ __forceinline__ void load2(const T* __restrict__ row, int bx, int dx, int& a, int& b)
 {
-	if (bx < 0) { a = b = 0; return; }     // halo lane left of the image
-	if (bx + 1 < dx) {
-		if constexpr (sizeof(T) == 2) {
-			uint32_t u = *reinterpret_cast<const uint32_t*>(row + bx);
-			a = (int16_t)(u & 0xffff); b = (int16_t)(u >> 16);
-		} else {
-			int2 u = *reinterpret_cast<const int2*>(row + bx);
-			a = u.x; b = u.y;
-		}
-	} else {
-		a = bx < dx ? (int)row[bx] : 0;
-		b = 0;
-	}
+	const int hi = dx > 0 ? dx - 1 : 0;
+	const int v0 = pinned((int)row[min(max(bx, 0), hi)]), v1 = pinned((int)row[min(max(bx + 1, 0), hi)]);
+	a = (bx >= 0 && bx < dx) ? v0 : 0;
+	b = (bx + 1 >= 0 && bx + 1 < dx) ? v1 : 0;
 }
 
 // Neighbour exchange across lanes with DPP wave shifts (GFX9 wave_shr:1 /
@@ -531,8 +522,9 @@ __device__ __forceinline__ void fwd_seg(const FwdArgs<TI, TO>& a, int x, int lan
 #pragma unroll
 		for (int i = 0; i < R; i++) {
 			const int y = y0 - 4 + i;
-			if (FAST || (y >= 0 && y < H)) raw[i] = load_row4<TI, EDGE>(a.src + (long)y * a.sp, x, W, a.vec != 0);
-			else raw[i] = RT{};
+			const int yc = FAST ? y : min(max(y, 0), H - 1);      // rows outside the image read as 0
+			const RT r = load_row4<TI, EDGE>(a.src + (long)yc * a.sp, x, W, a.vec != 0);
+			raw[i] = (FAST || (y >= 0 && y < H)) ? r : RT{};
 		}
 		int w0[4] = {0, 0, 0, 0}, w1[4] = {0, 0, 0, 0}, w2[4] = {0, 0, 0, 0};
 		int w3[4] = {0, 0, 0, 0}, w4[4], w5[4] = {0, 0, 0, 0};
@@ -635,8 +627,13 @@ __device__ __forceinline__ void fwd97p_seg(const FwdArgs<int16_t, int16_t>& a, i
 	const int16_t* rp = a.src + (long)(y0 - 4) * a.sp;   // wave-uniform row pointer
 	int yl = y0 - 4;
 	auto load_next = [&](uint2& dst) {
-		if (FAST || (yl >= 0 && yl < H)) dst = load_row4<int16_t, EDGE>(rp, x, W, a.vec != 0);
-		else dst = make_uint2(0, 0);
+		if (FAST) {
+			dst = load_row4<int16_t, false>(rp, x, W, true);
+		} else {
+			// rows outside the image read as 0 (clamped row, then a select)
+			const uint2 r = load_row4<int16_t, true>(a.src + (long)min(max(yl, 0), H - 1) * a.sp, x, W, a.vec != 0);
+			dst = (yl >= 0 && yl < H) ? r : make_uint2(0, 0);
+		}
 		rp += a.sp; yl++;
 	};
 #pragma unroll
@@ -888,85 +885,6 @@ __device__ __forceinline__ void fq_block_regs(const FqArgs& a, const int* thr, c
 	fq_child_pin_pk(a, b, w, insig, kx, ky);
 }
 
-// The blocks of one block row (D, H, V) read back from the bands in HBM, full
-// or partial (edge waves).  All loads are issued before any block is
-// processed, so a block row costs one memory round trip.  Full blocks use the
-// packed quantiser (the level is fused only when pk_ok), partial ones the
-// edge tsuqBlock.
-__device__ __forceinline__ void fq_row_global(const FqArgs& a, const int (*thr)[16], const uint32_t (*tpk)[17 * 8],
-                                              const FqTables& F, int kx, int ky)
-{
-	uint32_t w[3][8];
-	uint32_t csum[3];
-	bool ok[3], full[3];
-	int wdt[3], hgt[3];
-#pragma unroll
-	for (int b = 0; b < 3; b++) {
-		ok[b] = kx < a.bw[b] && ky < a.bh[b];
-		wdt[b] = ok[b] ? min(4, a.dx[b] - 4 * kx) : 0;
-		hgt[b] = ok[b] ? min(4, a.dy[b] - 4 * ky) : 0;
-		full[b] = wdt[b] == 4 && hgt[b] == 4;
-		const long pb = a.p[b];
-		const int16_t* base = a.d[b] + (long)(4 * ky) * pb + 4 * kx;
-		if (full[b]) {
-#pragma unroll
-			for (int r = 0; r < 4; r++) {
-				const uint2 u = *reinterpret_cast<const uint2*>(base + r * pb);
-				w[b][2 * r] = u.x; w[b][2 * r + 1] = u.y;
-			}
-		} else {
-#pragma unroll
-			for (int j = 0; j < 8; j++) {
-				const int i0 = 2 * j, i1 = 2 * j + 1;
-				const uint32_t lo = ((i0 >> 2) < hgt[b] && (i0 & 3) < wdt[b]) ? (uint16_t)base[(i0 >> 2) * pb + (i0 & 3)] : 0u;
-				const uint32_t hi = ((i1 >> 2) < hgt[b] && (i1 & 3) < wdt[b]) ? (uint16_t)base[(i1 >> 2) * pb + (i1 & 3)] : 0u;
-				w[b][j] = lo | (hi << 16);
-			}
-		}
-		csum[b] = 0;
-		if (full[b] && a.crd[b]) {
-			const uint32_t* c0 = a.crd[b] + (long)(2 * ky) * a.cbw[b] + 2 * kx;
-			const uint32_t* c1 = c0 + a.cbw[b];
-			csum[b] = (uint32_t)(c0[0] + c0[1] + c1[0] + c1[1]);
-		}
-	}
-#pragma unroll
-	for (int b = 0; b < 3; b++) {
-		if (!ok[b]) continue;
-		const long pb = a.p[b];
-		int16_t* base = a.d[b] + (long)(4 * ky) * pb + 4 * kx;
-		const long bi = (long)ky * a.bw[b] + kx;
-		if (full[b]) {
-			const uint64_t d = (uint64_t)tsuq_full_pk(w[b], a.Q[b], a.iQ[b], thr[b][0], tpk[b]) + csum[b];
-			const uint32_t dist = d > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)d;
-			if (dist == 0) w[b][0] = (w[b][0] & 0xFFFF0000u) | 0x8000u;
-#pragma unroll
-			for (int r = 0; r < 4; r++) *reinterpret_cast<uint2*>(base + r * pb) = make_uint2(w[b][2 * r], w[b][2 * r + 1]);
-			a.rd[b][bi] = dist;
-			uint32_t acc = 0;
-#pragma unroll
-			for (int j = 0; j < 8; j++) acc |= as_w(__builtin_elementwise_min(as_v2u(w[b][j]), (v2u){1, 1})) << (2 * j);
-			const uint32_t mask = (acc & 0x5555u) | ((acc >> 15) & 0xAAAAu);
-			const bool insig = (w[b][0] & 0xFFFFu) == 0x8000u;
-			a.rec[b][bi] = block_local_mask<true>(F.T, &F.E, mask, insig, a.high != 0);
-			fq_child_pin_pk(a, b, w[b], insig, kx, ky);
-		} else {
-			// edge tsuqBlock, src/lib/bandcodec.cpp:215-237 (children ignored)
-			int v[16];
-#pragma unroll
-			for (int j = 0; j < 8; j++) { v[2 * j] = (int16_t)(w[b][j] & 0xffff); v[2 * j + 1] = (int)w[b][j] >> 16; }
-			const uint32_t dist = (uint32_t)tsuq_edge<true>(v, wdt[b], hgt[b], a.Q[b], a.iQ[b]);
-			if (dist == 0) v[0] = kInsignif;
-#pragma unroll
-			for (int i = 0; i < 16; i++)
-				if ((i >> 2) < hgt[b] && (i & 3) < wdt[b]) base[(i >> 2) * pb + (i & 3)] = (int16_t)v[i];
-			a.rd[b][bi] = dist;
-			a.rec[b][bi] = block_local_edge(F.T, v, wdt[b], hgt[b], a.high != 0);
-			fq_child_pin(a, b, v, false, kx, ky);
-		}
-	}
-}
-
 // Image-border flags of one wave (fq_seg<S, true>).  Needs W % 8 == 0 and
 // H % 8 == 0: column W-1 is then the last odd column of some lane, and every
 // block the wave quantises is full.
@@ -1007,40 +925,68 @@ __device__ __forceinline__ void row_fwd97p8x2_edge(PRow8& r, PRow8& s, const FqB
 // One wave's segment: the forward 9/7 of rows [y0, y0 + S) of a 496-column
 // strip and the quantiser, records and parent info of the block rows they
 // make, all in registers.  EDGE: the wave touches an image border (m).
-template <int S, bool EDGE>
+// PC (producer-consumer mode, k_fwdq_pc): this wave only lifts; each
+// completed block row goes to the LDS double buffer `pcbuf` and every loop
+// iteration ends in a workgroup barrier that the consumer waves match.
+template <bool EDGE, bool PC = false>
 __device__ __forceinline__ void fq_seg(const FqArgs& a, const int (*thr)[16], const uint32_t (*tpk)[17 * 8],
-                                       const FqTables& F, int x, int lane, int y0, int kx, const FqBorder& m)
+                                       const FqTables& F, int x, int lane, int y0, int kx, const FqBorder& m, int S,
+                                       uint2 (*pcbuf)[3][4][kLanes] = nullptr, int dbg = 0)
 {
 	const bool out_lane = lane >= 1 && lane <= kLanes - 2 && (!EDGE || x < a.W);
 	int16_t* pL = a.d[BL] + (long)(y0 >> 1) * a.p[BL] + (x >> 1);
 	// input rows y0-4 .. y0+S+3 through a ring of PF row pairs (fwd97p_seg);
 	// PF = 4 pairs = one block row of output, so the buffer slot of an emitted
 	// pair is the unrolled index k
-	constexpr int NP = (S + 8) / 2, PF = 4;
-	static_assert(NP % PF == 0, "segment rows");
-	// bottom segment: pairs e = y0-4 .. H-2 only, then the tail formulas
-	const int nit = (EDGE && m.bottom) ? (a.H - y0) / 8 + 1 : NP / PF;   // loop iterations
+	constexpr int PF = 4;
+	// S (a multiple of 8) rows: S / 8 + 1 iterations of PF row pairs; bottom
+	// segment: pairs e = y0-4 .. H-2 only, then the tail formulas
+	const int nit = (EDGE && m.bottom) ? (a.H - y0) / 8 + 1 : S / 8 + 1;   // loop iterations
 	const int kend = (EDGE && m.bottom) ? 2 : PF;                          // pairs of the last one
-	uint4 ring[2 * PF];
+	// prefetch depth in loop iterations (8 rows each): the producer of the
+	// PC form has the registers for two
+	constexpr int DEPTH = PC ? 2 : 1;
+	uint4 ring[DEPTH][2 * PF];
 	const int16_t* rp = a.src + (long)(y0 - 4) * a.sp + x;
 	int yl = y0 - 4;
+	// border waves: clamped row / column, then a select (no divergent branch,
+	// which would drain every load at the join)
+	const int xcl = EDGE ? min(max(x, 0), a.W - 8) : x;
 	auto load_next = [&](uint4& dst) {
-		if (!EDGE || (m.ld && yl >= 0 && yl < a.H)) dst = *reinterpret_cast<const uint4*>(rp);
-		else dst = make_uint4(0, 0, 0, 0);
+		if (dbg & 8) {                            // timing experiment: no input loads
+			dst = make_uint4(yl, x, yl ^ x, 7);
+		} else if (!EDGE) {
+			dst = *reinterpret_cast<const uint4*>(rp);
+		} else {
+			uint4 u = *reinterpret_cast<const uint4*>(a.src + (long)min(max(yl, 0), a.H - 1) * a.sp + xcl);
+			asm("" : "+v"(u.x), "+v"(u.y), "+v"(u.z), "+v"(u.w));
+			dst = (m.ld && yl >= 0 && yl < a.H) ? u : make_uint4(0, 0, 0, 0);
+		}
 		rp += a.sp; yl++;
 	};
 #pragma unroll
-	for (int j = 0; j < 2 * PF; j++) load_next(ring[j]);
+	for (int d = 0; d < DEPTH; d++) {
+#pragma unroll
+		for (int j = 0; j < 2 * PF; j++)
+			if (d == 0 || d < nit) load_next(ring[d][j]);
+	}
 	const v2s z = {0, 0};
 	PRow8 w0, w1, w2, w3, w4, w5;
 #pragma unroll
 	for (int q = 0; q < 4; q++) { w0.q[q] = z; w1.q[q] = z; w2.q[q] = z; w3.q[q] = z; }
 	uint2 bD[4], bH[4], bV[4];
+	int cur = 0;                                // PC: the LDS buffer being filled
 	auto emit = [&](int k) {                    // rows e-4 (D, H) and e-3 (V, L) are final
-		bD[k] = make_uint2(as_u32(w0.q[0]), as_u32(w0.q[1]));
-		bH[k] = make_uint2(as_u32(w0.q[2]), as_u32(w0.q[3]));
-		bV[k] = make_uint2(as_u32(w1.q[0]), as_u32(w1.q[1]));
-		if (out_lane) *reinterpret_cast<uint2*>(pL) = make_uint2(as_u32(w1.q[2]), as_u32(w1.q[3]));
+		const uint2 vd = make_uint2(as_u32(w0.q[0]), as_u32(w0.q[1]));
+		const uint2 vh = make_uint2(as_u32(w0.q[2]), as_u32(w0.q[3]));
+		const uint2 vv = make_uint2(as_u32(w1.q[0]), as_u32(w1.q[1]));
+		if constexpr (PC) {
+			if (!(dbg & 16)) { pcbuf[cur][BD][k][lane] = vd; pcbuf[cur][BH][k][lane] = vh; pcbuf[cur][BV][k][lane] = vv; }
+			else if (vd.x == 0x7FFF1234u) pcbuf[cur][BD][k][lane] = vh;   // (keep the values live)
+		} else {
+			bD[k] = vd; bH[k] = vh; bV[k] = vv;
+		}
+		if (out_lane && !(dbg & 16)) *reinterpret_cast<uint2*>(pL) = make_uint2(as_u32(w1.q[2]), as_u32(w1.q[3]));
 		pL += a.p[BL];
 	};
 	auto quant_row = [&](int ky) {
@@ -1054,16 +1000,17 @@ __device__ __forceinline__ void fq_seg(const FqArgs& a, const int (*thr)[16], co
 		fq_block_regs(a, thr[BV], tpk[BV], F, BV, bV, kx, ky, out_lane);
 		__builtin_amdgcn_sched_barrier(0);
 	};
-#pragma unroll 1
-	for (int it = 0; it < nit; it++) {
+	auto iteration = [&](int it, uint4 (&rg)[2 * PF]) {
 		const bool last = it + 1 == nit;
+		const bool refill = it + DEPTH < nit;
+		cur = it & 1;
 #pragma unroll
 		for (int k = 0; k < PF; k++) {
 			if (EDGE && last && k >= kend) break;
 			const int e = y0 - 4 + 2 * (it * PF + k);   // the pair's even row
-			w4 = prow8_from(ring[2 * k]);
-			w5 = prow8_from(ring[2 * k + 1]);
-			if (!last) { load_next(ring[2 * k]); load_next(ring[2 * k + 1]); }
+			w4 = prow8_from(rg[2 * k]);
+			w5 = prow8_from(rg[2 * k + 1]);
+			if (refill) { load_next(rg[2 * k]); load_next(rg[2 * k + 1]); }
 			if (EDGE && e < 0) continue;                 // above the image (top segment)
 			if (EDGE) row_fwd97p8x2_edge(w4, w5, m);
 			else row_fwd97p8x2(w4, w5);
@@ -1107,58 +1054,31 @@ __device__ __forceinline__ void fq_seg(const FqArgs& a, const int (*thr)[16], co
 			w0 = w2; w1 = w3;
 			emit(3);
 		}
-		if (it >= 1) quant_row((y0 >> 3) + it - 1);   // a block row is complete
+		if constexpr (PC) __syncthreads();           // the consumers take the block row
+		else if (it >= 1) quant_row((y0 >> 3) + it - 1);   // a block row is complete
+	};
+	if constexpr (DEPTH == 1) {
+#pragma unroll 1
+		for (int it = 0; it < nit; it++) iteration(it, ring[0]);
+	} else {
+#pragma unroll 1
+		for (int it = 0; it < nit; it += 2) {
+			iteration(it, ring[0]);
+			if (it + 1 < nit) iteration(it + 1, ring[1]);
+		}
 	}
 }
 
-template <int S>
-__device__ __forceinline__ void fq_edge(const FqArgs& a, const int (*thr)[16], const uint32_t (*tpk)[17 * 8],
-                                        const FqTables& F, int lane, int y0, int strip)
-{
-	FwdArgs<int16_t, int16_t> f;
-	f.src = a.src; f.sp = a.sp; f.W = a.W; f.H = a.H;
-#pragma unroll
-	for (int b = 0; b < 4; b++) { f.d[b] = a.d[b]; f.p[b] = a.p[b]; }
-	f.nseg = a.nseg; f.vec = a.vec8; f.nofast = 1;
-	for (int h = 0; h < 2; h++) {
-		const int X0 = strip * kFqStrip + h * kStripValid - kCols;
-		if (X0 + kCols >= a.W) break;
-		fwd97p_seg<S, false>(f, X0 + lane * kCols, lane, y0);
-	}
-	// the blocks of this lane were written by lanes of this wave
-	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-	if (lane < 1 || lane > kLanes - 2) return;
-	const int kx = strip * (kFqStrip / 8) + lane - 1;
-	for (int ky = y0 >> 3; ky < (y0 + S) >> 3; ky++) fq_row_global(a, thr, tpk, F, kx, ky);
-}
-
-// The level is split into an interior rectangle of "fast" waves (strips
-// [fs0, fs1), segments [fg0, fg1) of S rows) and the border frame around it,
-// run as two kernels on forked streams so the frame's latency-bound waves
-// overlap the interior's streaming ones.
-struct FqGrid {
-	int fs0, fs1, fg0, fg1, S;         // interior rectangle (S-row segments)
-	int nstrip;
-	int se_rows;                       // frame segment height
-	int nseg_e;                        // frame segments per full-height strip
-	int tseg, bseg0;                   // frame segments above / from here below the interior
-	int n_lr, nlr_strips, lr_strip[3]; // full-height frame strips (lr_all: every strip)
-	int lr_all;
-	int border;                        // the interior kernel covers the whole level
-	int n_tb, ntb;                     // top+bottom units of the interior strips
-};
-
+// A packed level covers whole 496 x S tiles: one wave per (strip, segment),
+// the waves on the image border (fq_seg<S, true>) included.
 __device__ __forceinline__ void fq_stage_tables(const FqArgs& a, int (*s_thres)[16], FqTables& s_F, uint32_t (*s_tpk)[17 * 8])
 {
 	if (threadIdx.x < 48) s_thres[threadIdx.x / 16][threadIdx.x % 16] = a.thres[threadIdx.x / 16][threadIdx.x % 16];
-	{
-		for (int i = threadIdx.x; i < 3 * 17 * 8; i += blockDim.x) {
-			const int b = i / (17 * 8), c = (i >> 3) % 17, p = i & 7;
-			const uint32_t lo = c + p < 16 ? (uint32_t)a.thres[b][c + p] & 0xFFFFu : 0xFFFFu;
-			const uint32_t hi = c + p + 8 < 16 ? (uint32_t)a.thres[b][c + p + 8] & 0xFFFFu : 0xFFFFu;
-			s_tpk[b][i % (17 * 8)] = lo | (hi << 16);
-		}
+	for (int i = threadIdx.x; i < 3 * 17 * 8; i += blockDim.x) {
+		const int b = i / (17 * 8), c = (i >> 3) % 17, p = i & 7;
+		const uint32_t lo = c + p < 16 ? (uint32_t)a.thres[b][c + p] & 0xFFFFu : 0xFFFFu;
+		const uint32_t hi = c + p + 8 < 16 ? (uint32_t)a.thres[b][c + p + 8] & 0xFFFFu : 0xFFFFu;
+		s_tpk[b][i % (17 * 8)] = lo | (hi << 16);
 	}
 	static_assert(sizeof(SymTables) % 4 == 0 && sizeof(EnumSplit) % 4 == 0, "table words");
 	const uint32_t* sw = reinterpret_cast<const uint32_t*>(&kSymDevF);
@@ -1169,10 +1089,9 @@ __device__ __forceinline__ void fq_stage_tables(const FqArgs& a, int (*s_thres)[
 	for (int i = threadIdx.x; i < (int)(sizeof(EnumSplit) / 4); i += blockDim.x) dw[i] = sw[i];
 }
 
-// interior (or, in border mode, every wave of the level): grid
-// (fs1 - fs0, ceil((fg1 - fg0) / 4)), one wave per segment
+// grid (ceil(W / 496), ceil(nseg / 4)), one wave per segment
 template <int S>
-__global__ void __launch_bounds__(256, 3) k_fwdq_fast(FqArgs a, FqGrid g)
+__global__ void __launch_bounds__(256, 3) k_fwdq_fast(FqArgs a)
 {
 	__shared__ int s_thres[3][16];
 	__shared__ FqTables s_F __attribute__((aligned(16)));
@@ -1180,27 +1099,191 @@ __global__ void __launch_bounds__(256, 3) k_fwdq_fast(FqArgs a, FqGrid g)
 	fq_stage_tables(a, s_thres, s_F, s_tpk);
 	__syncthreads();
 	const int lane = threadIdx.x & 63;
-	const int seg = g.fg0 + blockIdx.y * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-	if (seg >= g.fg1) return;
-	const int strip = g.fs0 + blockIdx.x;
+	const int seg = blockIdx.y * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+	if (seg >= a.nseg) return;
+	const int strip = blockIdx.x;
 	const int X0 = strip * kFqStrip - 8, x = X0 + lane * 8, y0 = seg * S;
 	const int kx = strip * (kFqStrip / 8) + lane - 1;
 	FqBorder m;
 	m.top = y0 == 0;
 	m.bottom = y0 + S >= a.H;
-	if (g.border && (X0 < 0 || X0 + kLanes * 8 >= a.W || m.top || m.bottom)) {
+	if (X0 < 0 || X0 + kLanes * 8 >= a.W || m.top || m.bottom) {
 		m.eL0 = x == 0 ? 0x0000FFFFu : 0u;
 		m.oR3 = x + 7 == a.W - 1 ? 0xFFFF0000u : 0u;
 		m.ld = x >= 0 && x < a.W;
-		fq_seg<S, true>(a, s_thres, s_tpk, s_F, x, lane, y0, kx, m);
+		fq_seg<true>(a, s_thres, s_tpk, s_F, x, lane, y0, kx, m, S);
 	} else {
-		fq_seg<S, false>(a, s_thres, s_tpk, s_F, x, lane, y0, kx, m);
+		fq_seg<false>(a, s_thres, s_tpk, s_F, x, lane, y0, kx, m, S);
 	}
 }
 
-// frame: one wave per (strip, SE-row segment) unit outside the interior
-template <int SE>
-__global__ void __launch_bounds__(256) k_fwdq_edge(FqArgs a, FqGrid g)
+// Producer-consumer form: one workgroup per segment, wave 0 lifts (fq_seg in
+// PC mode), waves 1-3 quantise the D, H and V blocks of the block row the
+// producer finished one iteration earlier (LDS double buffer, one barrier per
+// iteration).  The lifting chain and the three quantisers of a segment run on
+// four SIMDs at once, and each wave needs fewer registers.
+// S is a runtime multiple of 8, chosen so that the level is about one round
+// of resident workgroups.  The producer role rotates over the four waves with
+// the workgroup index, so the lifting chains of the workgroups on a CU spread
+// over its four SIMDs.
+__global__ void __launch_bounds__(256, 4) k_fwdq_pc(FqArgs a, int S, int dbg)
+{
+	__shared__ int s_thres[3][16];
+	__shared__ FqTables s_F __attribute__((aligned(16)));
+	__shared__ uint32_t s_tpk[3][17 * 8];
+	__shared__ uint2 s_buf[2][3][4][kLanes];
+	fq_stage_tables(a, s_thres, s_F, s_tpk);
+	__syncthreads();
+	const int lane = threadIdx.x & 63;
+	const int strip = (dbg & 4) ? 1 : blockIdx.x, seg = (dbg & 4) ? 2 : blockIdx.y;
+	const int wave = (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) + blockIdx.x + blockIdx.y) & 3;   // role
+	const int X0 = strip * kFqStrip - 8, x = X0 + lane * 8, y0 = seg * S;
+	const int kx = strip * (kFqStrip / 8) + lane - 1;
+	FqBorder m;
+	m.top = y0 == 0;
+	m.bottom = y0 + S >= a.H;
+	const bool edge = X0 < 0 || X0 + kLanes * 8 >= a.W || m.top || m.bottom;
+	const int nit = m.bottom ? (a.H - y0) / 8 + 1 : S / 8 + 1;
+	if (wave == 0) {
+		if (edge) {
+			m.eL0 = x == 0 ? 0x0000FFFFu : 0u;
+			m.oR3 = x + 7 == a.W - 1 ? 0xFFFF0000u : 0u;
+			m.ld = x >= 0 && x < a.W;
+			fq_seg<true, true>(a, s_thres, s_tpk, s_F, x, lane, y0, kx, m, S, s_buf, dbg);
+		} else {
+			fq_seg<false, true>(a, s_thres, s_tpk, s_F, x, lane, y0, kx, m, S, s_buf, dbg);
+		}
+	} else {
+		const int b = wave - 1;
+		const bool out_lane = lane >= 1 && lane <= kLanes - 2 && x < a.W;
+#pragma unroll 1
+		for (int it = 0; it < nit; it++) {
+			__syncthreads();                     // matches the producer's iteration `it`
+			if (it == 0 || (dbg & 3) == 2) continue;     // dbg 2: timing of the lifting alone
+			uint2 buf[4];
+#pragma unroll
+			for (int r = 0; r < 4; r++) buf[r] = s_buf[it & 1][b][r][lane];
+			fq_block_regs(a, s_thres[b], s_tpk[b], s_F, b, buf, kx, (y0 >> 3) + it - 1, out_lane);
+		}
+	}
+}
+
+int fq_seg_rows(int H)
+{
+	static const int forced = [] { const char* e = getenv("RIC_FQ_S"); return e ? atoi(e) : 0; }();
+	if (forced == 8 || forced == 16 || forced == 32) return forced;
+	return H >= 4096 ? 32 : 16;
+}
+
+int fq_pc()
+{
+	static const int v = [] { const char* e = getenv("RIC_FQ_PC"); return e ? atoi(e) : 1; }();
+	return v;
+}
+
+template <int S>
+void fq_launch_s(FqArgs& a, hipStream_t st)
+{
+	a.nseg = (a.H + S - 1) / S;
+	const int nstrip = (a.W + kFqStrip - 1) / kFqStrip;
+	dim3 grid(nstrip, (a.nseg + kWavesPerBlock - 1) / kWavesPerBlock);
+	hipLaunchKernelGGL(k_fwdq_fast<S>, grid, dim3(256), 0, st, a);
+}
+
+// segment height of the producer-consumer form: about one round of resident
+// workgroups (kPcResident per CU) over the level, at least 8 rows
+constexpr int kPcResident = 4 * 256;
+int pc_seg_rows(int W, int H)
+{
+	static const int forced = [] { const char* e = getenv("RIC_FQ_S"); return e ? atoi(e) : 0; }();
+	if (forced >= 8 && forced % 8 == 0) return forced;
+	const int nstrip = (W + kFqStrip - 1) / kFqStrip;
+	const int want = (kPcResident + nstrip - 1) / nstrip;            // segments per strip
+	const int s = ((H + want - 1) / want + 7) / 8 * 8;
+	return s < 8 ? 8 : s;
+}
+
+void fq_launch_pc(FqArgs& a, hipStream_t st)
+{
+	const int S = pc_seg_rows(a.W, a.H);
+	a.nseg = (a.H + S - 1) / S;
+	const int nstrip = (a.W + kFqStrip - 1) / kFqStrip;
+	static const int onewg = [] { const char* e = getenv("RIC_FQ_ONEWG"); return e ? atoi(e) : 0; }();
+	// RIC_FQ_ONEWG=1: one interior workgroup only (latency of one segment; results invalid)
+	if (onewg) hipLaunchKernelGGL(k_fwdq_pc, dim3(1, 1), dim3(256), 0, st, a, S, fq_pc() | 4);
+	else hipLaunchKernelGGL(k_fwdq_pc, dim3(nstrip, a.nseg), dim3(256), 0, st, a, S, fq_pc());
+}
+
+// ------------------------------ generic fused forward level + quantiser
+// k_fwdq_gen: the same fusion as k_fwdq_fast for the 9/7 levels the packed
+// kernel does not take (int bands -- the coarsest level under ric's
+// level_chg --, image sizes that are not multiples of 8, rd thresholds
+// outside the packed range).  Geometry of k_fwd (4 columns per lane, 248
+// output columns per wave) with 8-row segments, so even a small level has
+// hundreds of waves: the wave lifts its segment with fwd_seg (checked path),
+// then quantises the 31 x 3 blocks it produced, read back from HBM (they were
+// written by lanes of this same wave: a workgroup-scope fence orders it), two
+// blocks per lane.  On the coarsest level it also runs the LL TSUQ
+// (src/lib/band.h:65-92) on the LL samples it wrote.
+constexpr int kGenRows = 8;
+constexpr int kGenBlocks = kStripValid / 8;   // 31 block columns per wave
+
+struct GenLL {
+	int on, iQ, T0;
+};
+
+template <typename TO>
+__device__ __forceinline__ void gen_block(const FqArgs& a, const int* thr, const FqTables& F, const TO* const* d, int b,
+                                          int kx, int ky)
+{
+	constexpr bool SH = sizeof(TO) == 2;
+	const int x0 = 4 * kx, y0 = 4 * ky, dx = a.dx[b], dy = a.dy[b];
+	const int wdt = min(4, dx - x0), hgt = min(4, dy - y0);
+	const bool full = wdt == 4 && hgt == 4;
+	const long pb = a.p[b];
+	TO* base = const_cast<TO*>(d[b]) + (long)y0 * pb + x0;
+	// clamped addresses: all 16 loads issue back to back, no divergent branch
+	int v[16];
+#pragma unroll
+	for (int i = 0; i < 16; i++) {
+		const int r = min(i >> 2, hgt - 1), c = min(i & 3, wdt - 1);
+		const int x = pinned((int)base[r * pb + c]);
+		v[i] = ((i >> 2) < hgt && (i & 3) < wdt) ? x : 0;
+	}
+	uint32_t csum = 0;   // children pRD (u32 sum, as k_quant_level)
+	if (full && a.crd[b]) {
+		const uint32_t* c0 = a.crd[b] + (long)(2 * ky) * a.cbw[b] + 2 * kx;
+		const uint32_t* c1 = c0 + a.cbw[b];
+		csum = c0[0] + c0[1] + c1[0] + c1[1];
+	}
+	uint32_t dist;
+	if (full) {
+		const uint64_t dd = (uint64_t)tsuq_full<SH>(v, a.Q[b], a.iQ[b], thr) + csum;
+		dist = dd > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)dd;
+	} else {
+		dist = (uint32_t)tsuq_edge<SH>(v, wdt, hgt, a.Q[b], a.iQ[b]);   // children ignored
+	}
+	if (dist == 0) v[0] = kInsignif;
+#pragma unroll
+	for (int i = 0; i < 16; i++)
+		if ((i >> 2) < hgt && (i & 3) < wdt) base[(i >> 2) * pb + (i & 3)] = (TO)v[i];
+	const long bi = (long)ky * a.bw[b] + kx;
+	a.rd[b][bi] = dist;
+	a.rec[b][bi] = full ? block_local_full(F.T, F.E, v, a.high != 0) : block_local_edge(F.T, v, wdt, hgt, a.high != 0);
+	uint8_t* cp = a.cpin[b];
+	if (cp) {
+		const uint32_t prop = (full && v[0] == kInsignif) ? 0x80u : 0u;
+#pragma unroll
+		for (int q = 0; q < 4; q++) {
+			const int qx = q & 1, qy = q >> 1, cx = 2 * kx + qx, cy = 2 * ky + qy, o = 8 * qy + 2 * qx;
+			if (cx < a.cpw[b] && cy < a.cph[b])
+				cp[(long)cy * a.cpw[b] + cx] = (uint8_t)(pin_ctx_of<SH>(v[o], v[o + 1], v[o + 4], v[o + 5]) | prop);
+		}
+	}
+}
+
+template <typename TI, typename TO>
+__global__ void __launch_bounds__(256) k_fwdq_gen(FqArgs a, GenLL ll, int nseg)
 {
 	__shared__ int s_thres[3][16];
 	__shared__ FqTables s_F __attribute__((aligned(16)));
@@ -1208,91 +1291,49 @@ __global__ void __launch_bounds__(256) k_fwdq_edge(FqArgs a, FqGrid g)
 	fq_stage_tables(a, s_thres, s_F, s_tpk);
 	__syncthreads();
 	const int lane = threadIdx.x & 63;
-	const int u = blockIdx.x * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-	int strip, seg;
-	if (u < g.n_lr) {
-		const int k = u / g.nseg_e;
-		strip = g.lr_all ? k : k == 0 ? g.lr_strip[0] : k == 1 ? g.lr_strip[1] : g.lr_strip[2];
-		seg = u - k * g.nseg_e;
-	} else if (u < g.n_lr + g.n_tb) {
-		const int v = u - g.n_lr, k = v / g.ntb, r = v - k * g.ntb;
-		strip = g.fs0 + k;
-		seg = r < g.tseg ? r : g.bseg0 + (r - g.tseg);
-	} else {
-		return;
+	const int seg = blockIdx.y * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+	if (seg >= nseg) return;
+	const int strip = blockIdx.x;
+	const int y0 = seg * kGenRows;
+	FwdArgs<TI, TO> f;
+	f.src = reinterpret_cast<const TI*>(a.src); f.sp = a.sp; f.W = a.W; f.H = a.H;
+#pragma unroll
+	for (int b = 0; b < 4; b++) { f.d[b] = reinterpret_cast<TO*>(a.d[b]); f.p[b] = a.p[b]; }
+	f.nseg = nseg; f.vec = a.vec8; f.nofast = 1;
+	const int X0 = strip * kStripValid - kCols;
+	fwd_seg<CDF97, TI, TO, kGenRows, false>(f, X0 + lane * kCols, lane, y0);
+	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+	const TO* d[3] = {f.d[0], f.d[1], f.d[2]};
+	const int ky = y0 >> 3;
+	for (int i = lane; i < 3 * kGenBlocks; i += kLanes) {
+		const int b = i / kGenBlocks, kx = strip * kGenBlocks + (i - b * kGenBlocks);
+		if (kx < a.bw[b] && ky < a.bh[b]) gen_block<TO>(a, s_thres[b], s_F, d, b, kx, ky);
 	}
-	fq_edge<SE>(a, s_thres, s_tpk, s_F, lane, seg * SE, strip);
-}
-
-int fq_seg_rows(int H)
-{
-	static const int forced = [] { const char* e = getenv("RIC_FQ_S"); return e ? atoi(e) : 0; }();
-	if (forced == 16 || forced == 32) return forced;
-	return H >= 4096 ? 32 : 16;
-}
-
-constexpr int kFqEdgeRows = 8;
-
-FqGrid fq_grid(const FqArgs& a, int S)
-{
-	FqGrid g = {};
-	g.S = S;
-	g.nstrip = (a.W + kFqStrip - 1) / kFqStrip;
-	// interior strips: the whole 512-column wave (halo lanes included) inside
-	// the image, clear of column W-1; interior segments: halo rows inside and
-	// clear of the top/bottom boundary formulas
-	g.border = a.vec16 && a.nofast != 1 && a.W % 8 == 0 && a.H % 8 == 0;
-	if (g.border) {
-		// border mode: fq_seg<S, true> handles the image borders in registers
-		g.fs0 = 0; g.fs1 = g.nstrip;
-		g.fg0 = 0; g.fg1 = (a.H + S - 1) / S;
-		g.nseg_e = 0; g.tseg = g.bseg0 = 0; g.nlr_strips = 0; g.lr_all = 0; g.n_lr = g.ntb = g.n_tb = 0;
-		return g;
-	}
-	g.fs0 = 1; g.fs1 = 1;
-	while (g.fs1 * kFqStrip - 8 + kLanes * 8 < a.W) g.fs1++;
-	g.fg0 = (8 + S - 1) / S; g.fg1 = g.fg0;
-	while ((g.fg1 + 1) * S + 4 < a.H) g.fg1++;
-	if (!a.vec16 || a.nofast == 1 || g.fs1 <= g.fs0 || g.fg1 <= g.fg0) { g.fs0 = g.fs1 = 0; g.fg0 = g.fg1 = 0; }
-	g.se_rows = kFqEdgeRows;
-	g.nseg_e = (a.H + kFqEdgeRows - 1) / kFqEdgeRows;
-	const bool interior = g.fs1 > g.fs0;
-	g.tseg = interior ? g.fg0 * S / kFqEdgeRows : 0;
-	g.bseg0 = interior ? g.fg1 * S / kFqEdgeRows : 0;
-	g.nlr_strips = 0;
-	g.lr_all = !interior;
-	if (interior) {
-		for (int s = 0; s < g.nstrip; s++)
-			if (s < g.fs0 || s >= g.fs1) g.lr_strip[g.nlr_strips++] = s;   // at most 3 (fs0 = 1)
-	} else {
-		g.nlr_strips = g.nstrip;
-	}
-	g.n_lr = g.nlr_strips * g.nseg_e;
-	g.ntb = interior ? g.tseg + (g.nseg_e - g.bseg0) : 0;
-	g.n_tb = interior ? (g.fs1 - g.fs0) * g.ntb : 0;
-	return g;
-}
-
-template <int S>
-void fq_launch_s(FqArgs& a, hipStream_t st, hipStream_t st2, hipEvent_t fork, hipEvent_t join)
-{
-	a.nseg = (a.H + S - 1) / S;
-	const FqGrid g = fq_grid(a, S);
-	const int nedge = g.n_lr + g.n_tb;
-	const bool interior = g.fs1 > g.fs0;
-	if (interior && nedge > 0 && st2) {
-		(void)hipEventRecord(fork, st);
-		(void)hipStreamWaitEvent(st2, fork, 0);
-	}
-	hipStream_t se = (interior && st2) ? st2 : st;
-	if (nedge > 0 && a.nofast != 2)
-		hipLaunchKernelGGL(k_fwdq_edge<kFqEdgeRows>, dim3((nedge + kWavesPerBlock - 1) / kWavesPerBlock), dim3(256), 0, se, a, g);
-	if (interior)
-		hipLaunchKernelGGL(k_fwdq_fast<S>, dim3(g.fs1 - g.fs0, (g.fg1 - g.fg0 + kWavesPerBlock - 1) / kWavesPerBlock),
-		                   dim3(256), 0, st, a, g);
-	if (interior && nedge > 0 && st2) {
-		(void)hipEventRecord(join, st2);
-		(void)hipStreamWaitEvent(st, join, 0);
+	if (ll.on) {
+		// CBand::TSUQ with Thres 0.5 on this wave's LL samples: all loads first
+		constexpr bool SH = sizeof(TO) == 2;
+		constexpr int NLL = (kGenRows / 2) * (kStripValid / 2);
+		constexpr int PER = (NLL + kLanes - 1) / kLanes;
+		const int ldx = a.W >> 1, ldy = a.H >> 1, c0 = strip * (kStripValid / 2), r0 = y0 >> 1;
+		int val[PER];
+		TO* q[PER];
+		bool in[PER];
+#pragma unroll
+		for (int k = 0; k < PER; k++) {
+			const int i = lane + k * kLanes;
+			const int r = r0 + i / (kStripValid / 2), c = c0 + i % (kStripValid / 2);
+			in[k] = i < NLL && r < ldy && c < ldx;
+			q[k] = f.d[BL] + (long)min(r, ldy - 1) * f.p[BL] + min(c, ldx - 1);
+			val[k] = *q[k];
+		}
+#pragma unroll
+		for (int k = 0; k < PER; k++) {
+			const int v = val[k];
+			if (in[k])
+				*q[k] = (uint32_t)(v + ll.T0) <= (uint32_t)(2 * ll.T0) ? (TO)0
+				        : (TO)tr<SH>((int)((uint32_t)v * (uint32_t)ll.iQ + 32768u) >> 16);
+		}
 	}
 }
 
@@ -1386,8 +1427,17 @@ __device__ __forceinline__ void inv_seg(const InvArgs<TB, TL, TO>& a, int x, int
 #pragma unroll
 		for (int i = 0; i < R; i++) {
 			const int y = y0 - 4 + i;
-			if (FAST || (y >= 0 && y < H)) load_pair(y, rlo[i], rhi[i]);
-			else { rlo[i] = R2{}; rhi[i] = R2{}; }
+			if (FAST) {
+				load_pair(y, rlo[i], rhi[i]);
+			} else {
+				// rows outside the image read as 0: the nearest row of the same
+				// parity (same bands), then a select -- no divergent branch
+				const int yc = y < 0 ? (y & 1) : y >= H ? H - 1 - ((H - 1 - y) & 1) : y;
+				R2 lo, hi;
+				load_pair(yc, lo, hi);
+				const bool in = y >= 0 && y < H;
+				rlo[i] = in ? lo : R2{}; rhi[i] = in ? hi : R2{};
+			}
 		}
 		int w0[4] = {0, 0, 0, 0}, w1[4] = {0, 0, 0, 0}, w2[4] = {0, 0, 0, 0}, w3[4] = {0, 0, 0, 0};
 		int w4[4] = {0, 0, 0, 0}, w5[4], w6[4] = {0, 0, 0, 0};
@@ -1494,17 +1544,22 @@ __device__ __forceinline__ void inv97p_seg(const InvArgs<int16_t, int16_t, int16
 	const int16_t* pL = a.ll + by0 * a.pl;
 	int yl = y0 - 4;
 	auto load_next = [&](uint4& dst) {
-		if (FAST || (yl >= 0 && yl < H)) {
-			dst.x = load_band2<int16_t, EDGE>(pD, bx, dxD);
-			dst.y = load_band2<int16_t, EDGE>(pH, bx, dxH);
+		if (FAST) {
+			dst.x = load_band2<int16_t, false>(pD, bx, dxD);
+			dst.y = load_band2<int16_t, false>(pH, bx, dxH);
+			dst.z = load_band2<int16_t, false>(pV, bx, dxD);
+			dst.w = load_band2<int16_t, false>(pL, bx, dxH);
 		} else {
-			dst.x = 0; dst.y = 0;
-		}
-		if (FAST || (yl + 1 >= 0 && yl + 1 < H)) {
-			dst.z = load_band2<int16_t, EDGE>(pV, bx, dxD);
-			dst.w = load_band2<int16_t, EDGE>(pL, bx, dxH);
-		} else {
-			dst.z = 0; dst.w = 0;
+			// band rows outside the bands read as 0: clamped row, then a select
+			const int by = yl >> 1;
+			const int be = min(max(by, 0), max(((H + 1) >> 1) - 1, 0)), bo = min(max(by, 0), max((H >> 1) - 1, 0));
+			const uint32_t xd = load_band2<int16_t, true>(a.d[BD] + (long)be * a.p[BD], bx, dxD);
+			const uint32_t xh = load_band2<int16_t, true>(a.d[BH] + (long)be * a.p[BH], bx, dxH);
+			const uint32_t xv = load_band2<int16_t, true>(a.d[BV] + (long)bo * a.p[BV], bx, dxD);
+			const uint32_t xl = load_band2<int16_t, true>(a.ll + (long)bo * a.pl, bx, dxH);
+			const bool ie = yl >= 0 && yl < H, io = yl + 1 >= 0 && yl + 1 < H;
+			dst.x = ie ? xd : 0u; dst.y = ie ? xh : 0u;
+			dst.z = io ? xv : 0u; dst.w = io ? xl : 0u;
 		}
 		pD += a.p[BD]; pH += a.p[BH]; pV += a.p[BV]; pL += a.pl; yl += 2;
 	};
@@ -1685,15 +1740,19 @@ void launch_fwd_level(const Level& L, const void* src, long sp, char* arena, int
 	else fwd_dispatch<HAAR>(L, src, sp, arena, vec, st);
 }
 
-bool fwdq_supported(const Level& L, int trans, const QuantParams& qp)
+int fwdq_mode(const Level& L, int trans, const QuantParams& qp, int vec16)
 {
 	static const bool off = [] { const char* e = getenv("RIC_NOFUSE"); return e && atoi(e) != 0; }();
-	return !off && trans == CDF97 && !L.in_is_int && !L.is_int && pk_ok(qp.thres[0]) && pk_ok(qp.thres[1]) &&
-	       pk_ok(qp.thres[2]);
+	// tuning knob: RIC_FQ_GEN_BELOW=h runs levels less than h rows high generically
+	static const int gen_below = [] { const char* e = getenv("RIC_FQ_GEN_BELOW"); return e ? atoi(e) : 0; }();
+	if (off || trans != CDF97) return FQ_NONE;
+	const bool packed = L.h >= gen_below && !L.in_is_int && !L.is_int && vec16 && !dbg_nofast() && L.w % 8 == 0 && L.h % 8 == 0 &&
+	                    pk_ok(qp.thres[0]) && pk_ok(qp.thres[1]) && pk_ok(qp.thres[2]);
+	return packed ? FQ_PACKED : FQ_GENERIC;
 }
 
 void launch_fwdq_level(const Pyramid& P, int l, const void* src, long sp, int vec8, int vec16, const QuantParams& qp,
-                       char* arena, hipStream_t st, hipStream_t st2, hipEvent_t fork, hipEvent_t join)
+                       char* arena, hipStream_t st)
 {
 	const Level& L = P.L[l];
 	FqArgs a;
@@ -1716,9 +1775,44 @@ void launch_fwdq_level(const Pyramid& P, int l, const void* src, long sp, int ve
 		a.Q[b] = qp.Q[b]; a.iQ[b] = qp.iQ[b];
 		for (int i = 0; i < 16; i++) a.thres[b][i] = qp.thres[b][i];
 	}
+	if (fq_pc()) { fq_launch_pc(a, st); return; }
 	const int S = fq_seg_rows(L.h);
-	if (S == 32) fq_launch_s<32>(a, st, st2, fork, join);
-	else fq_launch_s<16>(a, st, st2, fork, join);
+	if (S == 32) fq_launch_s<32>(a, st);
+	else if (S == 16) fq_launch_s<16>(a, st);
+	else fq_launch_s<8>(a, st);
+}
+
+void launch_fwdq_gen_level(const Pyramid& P, int l, const void* src, long sp, int vec8, const QuantParams& qp,
+                           int ll_on, int ll_iQ, int ll_T0, char* arena, hipStream_t st)
+{
+	const Level& L = P.L[l];
+	FqArgs a;
+	a.src = (const int16_t*)src; a.sp = sp; a.W = L.w; a.H = L.h;
+	a.vec8 = vec8; a.vec16 = 0; a.nofast = 1; a.high = l == 0;
+	for (int b = 0; b < 4; b++) { a.d[b] = (int16_t*)(arena + L.b[b].off); a.p[b] = L.b[b].pitch; }
+	for (int b = 0; b < 3; b++) {
+		const Band& B = L.b[b];
+		a.dx[b] = B.dx; a.dy[b] = B.dy; a.bw[b] = B.bw(); a.bh[b] = B.bh();
+		a.rd[b] = (uint32_t*)(arena + B.rd_off);
+		a.rec[b] = (uint64_t*)(arena + P.rec_off[l][b]);
+		if (l > 0) {
+			const Band& C = P.L[l - 1].b[b];
+			a.crd[b] = (const uint32_t*)(arena + C.rd_off); a.cbw[b] = C.bw();
+			a.cpin[b] = (uint8_t*)(arena + P.pin_off[l - 1][b]); a.cpw[b] = C.bw(); a.cph[b] = C.bh();
+		} else {
+			a.crd[b] = nullptr; a.cbw[b] = 0;
+			a.cpin[b] = nullptr; a.cpw[b] = 0; a.cph[b] = 0;
+		}
+		a.Q[b] = qp.Q[b]; a.iQ[b] = qp.iQ[b];
+		for (int i = 0; i < 16; i++) a.thres[b][i] = qp.thres[b][i];
+	}
+	GenLL ll = {ll_on, ll_iQ, ll_T0};
+	const int nseg = (L.h + kGenRows - 1) / kGenRows;
+	a.nseg = nseg;
+	dim3 grid((L.w + kStripValid - 1) / kStripValid, (nseg + kWavesPerBlock - 1) / kWavesPerBlock);
+	if (!L.in_is_int && !L.is_int) hipLaunchKernelGGL((k_fwdq_gen<int16_t, int16_t>), grid, dim3(256), 0, st, a, ll, nseg);
+	else if (!L.in_is_int) hipLaunchKernelGGL((k_fwdq_gen<int16_t, int32_t>), grid, dim3(256), 0, st, a, ll, nseg);
+	else hipLaunchKernelGGL((k_fwdq_gen<int32_t, int32_t>), grid, dim3(256), 0, st, a, ll, nseg);
 }
 
 void launch_inv_level(const Level& L, const Band& lls, char* arena, void* out, long po, int out_is_int,

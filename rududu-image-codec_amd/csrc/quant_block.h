@@ -137,24 +137,27 @@ __device__ __forceinline__ v2u splat2(uint32_t x) { return as_v2u((x & 0xFFFFu) 
 // Packed 16-bit primitives as single instructions.  Inline asm keeps the
 // instruction combiner from rewriting a saturating-sub + min mask idiom into
 // per-half compares and selects (three times the instructions).
-__device__ __forceinline__ v2u pk_sub_sat(v2u a, v2u b)
+__device__ __forceinline__ v2u pk_sub_sat(v2u a, v2u b) { return __builtin_elementwise_sub_sat(a, b); }
+__device__ __forceinline__ v2u pk_add_sat(v2u a, v2u b) { return __builtin_elementwise_add_sat(a, b); }
+// 0xFFFF in each half where a > b (unsigned).  One opaque block: written in C
+// the combiner turns the saturating-sub / min / negate idiom into per-half
+// compares and selects (twice the instructions).
+__device__ __forceinline__ v2u gt_mask(v2u a, v2u b)
 {
 	uint32_t r;
-	asm("v_pk_sub_u16 %0, %1, %2 clamp" : "=v"(r) : "v"(as_w(a)), "v"(as_w(b)));
-	return as_v2u(r);
-}
-__device__ __forceinline__ v2u pk_add_sat(v2u a, v2u b)
-{
-	uint32_t r;
-	asm("v_pk_add_u16 %0, %1, %2 clamp" : "=v"(r) : "v"(as_w(a)), "v"(as_w(b)));
+	asm("v_pk_sub_u16 %0, %1, %2 clamp\n\t"
+	    "v_pk_min_u16 %0, %0, 1 op_sel_hi:[1,0]\n\t"
+	    "v_pk_sub_u16 %0, 0, %0"
+	    : "=&v"(r) : "v"(as_w(a)), "v"(as_w(b)));
 	return as_v2u(r);
 }
 // 0xFFFF in each half where x != 0
 __device__ __forceinline__ v2u nzmask(v2u x)
 {
-	uint32_t m, r;
-	asm("v_pk_min_u16 %0, %1, 1 op_sel_hi:[1,0]" : "=v"(m) : "v"(as_w(x)));
-	asm("v_pk_sub_u16 %0, 0, %1" : "=v"(r) : "v"(m));
+	uint32_t r;
+	asm("v_pk_min_u16 %0, %1, 1 op_sel_hi:[1,0]\n\t"
+	    "v_pk_sub_u16 %0, 0, %0"
+	    : "=&v"(r) : "v"(as_w(x)));
 	return as_v2u(r);
 }
 __device__ __forceinline__ v2u rot16(v2u x) { return as_v2u(__builtin_amdgcn_alignbit(as_w(x), as_w(x), 16)); }
@@ -212,8 +215,8 @@ __device__ __forceinline__ int tsuq_full_pk(uint32_t (&w)[8], int Q, int iQ, int
 		const v2u ax = as_v2u(as_u32(__builtin_elementwise_max(x, (v2s){0, 0} - x)));   // |x| (0x8000 for -32768)
 		const v2u sg = as_v2u(w[j]) >> (v2u){15, 15};
 		const v2u u = ax + ax + sg;                                                // s2u_, wrapped to short
-		const v2u mnz = nzmask(pk_sub_sat(ax, T0v));              // outside the dead zone
-		const v2u mlt = nzmask(pk_sub_sat(th0v, u));              // below rd_thres[0]
+		const v2u mnz = gt_mask(ax, T0v);                                          // outside the dead zone
+		const v2u mlt = gt_mask(th0v, u);                                          // below rd_thres[0]
 		// quant_mag: ((u >> 1) * iQ + 32768) >> 16, then (q << 1) | sign
 		const uint32_t uw = as_w(u);
 		const uint32_t qlo = __umul24((uw & 0xFFFFu) >> 1, (uint32_t)iQ) + 32768u;
@@ -240,14 +243,14 @@ __device__ __forceinline__ int tsuq_full_pk(uint32_t (&w)[8], int Q, int iQ, int
 	v2u t = {0xFFFF, 0xFFFF};
 #pragma unroll
 	for (int p = 0; p < 8; p++) {
-		const v2u pen = nzmask(pk_sub_sat(as_v2u(tc[p]), R[p] >> (v2u){4, 4}));
+		const v2u pen = gt_mask(as_v2u(tc[p]), R[p] >> (v2u){4, 4});
 		t = __builtin_elementwise_min(t, pk_add_sat(R[p], pen));
 	}
 	t = __builtin_elementwise_min(t, rot16(t));                               // both halves = thr
 	v2u accS = z;
 #pragma unroll
 	for (int j = 0; j < 8; j++) {
-		const v2u keep = ~nzmask(pk_sub_sat(t, key[j]));     // key >= thr (never for key 0)
+		const v2u keep = ~gt_mask(t, key[j]);                 // key >= thr (never for key 0)
 		const uint32_t nv = as_w(keep) & ((w[j] & 0x00010001u) | 0x00020002u);  // survivor: magnitude 1
 		w[j] = bfi(as_w(nzmask(key[j])), nv, w[j]);
 		accS = accS - keep;

@@ -13,12 +13,19 @@ void launch_fwd_level(const Level& L, const void* src, long sp, char* arena, int
 // short->short levels.  Writes level l's quantised D/H/V bands, pRD, block-local
 // records, its unquantised LL, and (l > 0) the parent info of level l-1.
 struct QuantParams;
-// 9/7 short->short levels whose rd thresholds suit the packed quantiser
-bool fwdq_supported(const Level& L, int trans, const QuantParams& qp);
-// The border frame runs on st2 (forked from st by `fork`, joined back by
-// `join`), concurrently with the interior on st; st2 == nullptr: all on st.
+// How a level's forward transform + quantiser run: FQ_PACKED = k_fwdq_fast
+// (9/7 short levels, sizes multiples of 8, 16-byte aligned rows, rd thresholds
+// in the packed range), FQ_GENERIC = k_fwdq_gen (other 9/7 levels), FQ_NONE =
+// separate forward / quantiser / record kernels (5/3, Haar).
+enum { FQ_NONE = 0, FQ_PACKED = 1, FQ_GENERIC = 2 };
+int fwdq_mode(const Level& L, int trans, const QuantParams& qp, int vec16);
 void launch_fwdq_level(const Pyramid& P, int l, const void* src, long sp, int vec8, int vec16, const QuantParams& qp,
-                       char* arena, hipStream_t st, hipStream_t st2, hipEvent_t fork, hipEvent_t join);
+                       char* arena, hipStream_t st);
+// Generic fused forward level + quantiser + records (dwt.hip k_fwdq_gen) for
+// any 9/7 level (int bands, odd sizes); ll_on: also CBand::TSUQ on the level's
+// LL (the coarsest level), with its iQ and dead zone T0.
+void launch_fwdq_gen_level(const Pyramid& P, int l, const void* src, long sp, int vec8, const QuantParams& qp,
+                           int ll_on, int ll_iQ, int ll_T0, char* arena, hipStream_t st);
 // Inverse level: D/H/V bands + lls (the level's LL) -> out (pitch po elements),
 // typed int32 if out_is_int else int16.
 void launch_inv_level(const Level& L, const Band& lls, char* arena, void* out, long po,

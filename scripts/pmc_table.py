@@ -1,16 +1,19 @@
 #!/usr/bin/env python3
-"""pmc_table.py TAG -- per-kernel (name, grid) median of every counter in gpurun_out/TAG_p*/"""
-import csv, glob, os, statistics, sys
-REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-tag = sys.argv[1]
-pat = sys.argv[2] if len(sys.argv) > 2 else ""
-tab = {}
-for f in sorted(glob.glob(os.path.join(REPO, "gpurun_out", tag + "_p*", "run_counter_collection.csv"))):
-    for r in csv.DictReader(open(f)):
-        n = r["Kernel_Name"].replace("void ric::(anonymous namespace)::", "").split("(")[0]
-        if pat not in n:
-            continue
-        key = (n, int(r.get("Grid_Size", 0)))
-        tab.setdefault(key, {}).setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
-for (n, g), cs in sorted(tab.items(), key=lambda kv: -kv[0][1]):
-    print("%-40s grid=%-8d " % (n[:40], g) + " ".join("%s=%.4g" % (c, statistics.median(v)) for c, v in sorted(cs.items())))
+"""pmc_table.py DIR... -- mean of each PMC counter per kernel name over the
+counter_collection.csv files of rocprofv3 --pmc passes (scripts/pmc_sweep.sh)."""
+import collections
+import csv
+import glob
+import os
+import sys
+
+acc = collections.defaultdict(lambda: collections.defaultdict(list))
+for d in sys.argv[1:]:
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            name = r["Kernel_Name"].replace("void ric::(anonymous namespace)::", "")[:48]
+            acc[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
+for name, ctrs in sorted(acc.items()):
+    print(name)
+    for c, v in sorted(ctrs.items()):
+        print("   %-28s %14.1f  (n=%d)" % (c, sum(v) / len(v), len(v)))
