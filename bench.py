@@ -32,6 +32,44 @@ sys.path.insert(0, os.path.join(REPO, "rududu-image-codec_amd"))
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak (spec)
 
 
+def wavelet_bytes(W, H, levels=5, level_chg=1):
+    """SURVEY.md §8(d) algorithmic byte model per level, at the reference's
+    band types (s16 above level_chg, i32 at or below; ric: level_chg 1, so only
+    the coarsest level is int):
+      dwt[l]   read the level's input plane + write its 4 subbands;
+      quant[l] read + write every coefficient of D, H, V + 8 B (pRD) per 4x4 block;
+      deq[l]   read + write every coefficient of D, H, V (TSUQi);
+      ll       the coarsest LL: TSUQ read + write (TSUQi the same, counted in deq)."""
+    out = {"dwt": [], "quant": [], "deq": []}
+    w, h = W, H
+    in_sz = 2
+    for l in range(levels):
+        lv = levels - l              # the reference's level counter (wavelet2d.cpp:69-72)
+        sz = 4 if lv <= level_chg else 2
+        dD = ((w + 1) // 2) * ((h + 1) // 2)
+        dV = ((w + 1) // 2) * (h // 2)
+        dH = (w // 2) * ((h + 1) // 2)
+        dL = (w // 2) * (h // 2)
+        blk = sum(((bx + 3) // 4) * ((by + 3) // 4) for bx, by in
+                  (((w + 1) // 2, (h + 1) // 2), ((w + 1) // 2, h // 2), (w // 2, (h + 1) // 2)))
+        coef = dD + dV + dH
+        out["dwt"].append(w * h * in_sz + (coef + dL) * sz)
+        out["quant"].append(coef * 2 * sz + 8 * blk)
+        out["deq"].append(coef * 2 * sz)
+        w, h, in_sz = w // 2, h // 2, sz
+        last_sz = sz
+    out["ll"] = w * h * 2 * last_sz
+    out["deq"][-1] += out["ll"]
+    return out
+
+
+def _frac(ms, nbytes):
+    if not ms:
+        return {"ms": None, "bytes": nbytes, "frac": None}
+    gbs = nbytes / (ms * 1e-3) / 1e9
+    return {"ms": round(ms, 4), "bytes": nbytes, "GBps": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -44,6 +82,7 @@ def parse():
     ap.add_argument("--q", type=int, default=9)
     ap.add_argument("--trans", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-gather", action="store_true", help="N>1: skip the per-step stream gather to rank 0")
     ap.add_argument("--cpu-frames", type=int, default=16)
     return ap.parse_args()
 
@@ -87,12 +126,23 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("gloo", init_method="env://")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    # one process per GPU; barrier, max-over-ranks timing and the final stream
+    # gather go over RCCL ("nccl" is RCCL on ROCm; RIC_BENCH_BACKEND=gloo for a
+    # CPU-side rehearsal)
+    backend = os.environ.get("RIC_BENCH_BACKEND", "nccl")
+    cdev = dev if backend == "nccl" else torch.device("cpu")
+    if world > 1:
+        dist.init_process_group(backend, init_method="env://")
+
+    def barrier():
+        if world > 1:
+            t = torch.ones(1, device=cdev)
+            dist.all_reduce(t)
 
     import ric_amd
+    import shard
     W, H = a.width, a.height
     threads = a.threads or 16
     batch = a.batch or threads
@@ -116,9 +166,14 @@ def main():
             for i in range(k, batch, threads):
                 ric = c.compress(frames[i], q=a.q, trans=a.trans, on_device=True)
                 sizes[i] = len(ric)
+                streams[i] = ric
                 c.decompress(ric, pix_out=outs[i])
         except Exception as e:  # surfaced after join
             errors.append(e)
+
+    gather = world > 1 and not a.no_gather
+    streams = [b""] * batch
+    gathered = [0]
 
     def step():
         ths = [threading.Thread(target=run_frames, args=(k,)) for k in range(threads)]
@@ -128,23 +183,28 @@ def main():
             t.join()
         if errors:
             raise errors[0]
+        if gather:
+            # the path's one exchange: every rank's .ric streams to rank 0
+            # (SURVEY.md §8(e)); rank 0 keeps them on the device
+            got = shard.gather_streams(streams, dist, device=cdev, to_host=False)
+            if rank == 0:
+                gathered[0] = int(sum(int(s[1:1 + int(s[0])].sum()) for s in got[1]))
 
     for _ in range(a.warmup):
         step()
     for c in codecs:
         c.prof_enable(True)
 
-    if world > 1:
-        dist.barrier()
+    barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    barrier()
     if world > 1:
-        dist.barrier()
-        tt = torch.tensor([dt], dtype=torch.float64)
+        tt = torch.tensor([dt], dtype=torch.float64, device=cdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt[0])
 
@@ -157,20 +217,31 @@ def main():
             s[1] += n
     stage_ms = {k: round(v[0] / v[1], 4) for k, v in prof.items() if v[1]}
 
-    # roofline of the dominant GPU kernel: the level-0 forward DWT
-    # (algorithmic bytes, SURVEY.md §8(d): read the s16 plane + write 4 s16 bands = 4 B/px)
-    fwd0_bytes = 4.0 * W * H
+    # roofline of the dominant GPU kernel: the level-0 launch of the fused
+    # forward 9/7 DWT + RD quantiser + zerotree records (dwt.hip k_fwdq_pc).
+    # Algorithmic bytes = SURVEY.md §8(d)'s per-unit figures for the work that
+    # one launch does: the level-0 DWT (4 B/px) plus the level-0 quantiser
+    # (read + write every s16 coefficient, 4 B/coef, + 8 B per 4x4 block).
+    bm = wavelet_bytes(W, H)
+    l0_bytes = bm["dwt"][0] + bm["quant"][0]
     t_fwd0 = stage_ms.get("fwd_l0")
-    achieved = fwd0_bytes / (t_fwd0 * 1e-3) / 1e9 if t_fwd0 else None
+    achieved = l0_bytes / (t_fwd0 * 1e-3) / 1e9 if t_fwd0 else None
     traffic = None
     pmc = os.path.join(REPO, "profiles", "pmc_fwd_l0.json")
     if os.path.exists(pmc):
         try:
-            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+            p = json.load(open(pmc))
+            if p.get("kernel", "").startswith("k_fwdq_pc"):
+                traffic = p.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
-    # the whole GPU wavelet-encode stage (DWT + RD quantiser): 9.851 B/px at C3
+    # the whole GPU wavelet encode (every forward level + quantiser + LL TSUQ):
+    # the §8(d) DWT + quant model, 326.8 MB at C3
+    enc_bytes = sum(bm["dwt"]) + sum(bm["quant"]) + bm["ll"]
     enc_gpu = (stage_ms.get("fwd", 0) + stage_ms.get("quant", 0)) or None
+    # the GPU decode stages: dequantiser (r + w) + inverse DWT (= forward bytes)
+    dec_bytes = sum(bm["dwt"]) + sum(bm["deq"])
+    dec_gpu = (stage_ms.get("dequant", 0) + stage_ms.get("inv", 0)) or None
 
     total_px = world * batch * W * H * a.steps
     value = total_px / 1e6 / dt
@@ -191,18 +262,19 @@ def main():
                                % (W, H, a.q),
                    "frames_per_gpu_per_step": batch, "host_coder_threads_per_gpu": threads,
                    "parallelism": "frames sharded over %d GPU(s)" % world},
-        "roofline": {"bound": "hbm", "kernel": "k_fwd (level 0 forward 9/7 DWT)",
+        "roofline": {"bound": "hbm",
+                     "kernel": "k_fwdq_pc level 0 (fused forward 9/7 DWT + RD quantiser + block records)",
                      "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                     "traffic": traffic, "algorithmic_bytes_per_launch": fwd0_bytes,
+                     "traffic": traffic, "algorithmic_bytes_per_launch": l0_bytes,
                      "avg_launch_ms": t_fwd0},
-        "gpu_wavelet_encode": {"ms": round(enc_gpu, 4) if enc_gpu else None,
-                               "bytes": 9.851 * W * H,
-                               "frac": round(9.851 * W * H / (enc_gpu * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
-                               if enc_gpu else None},
+        "gpu_wavelet_encode": _frac(enc_gpu, enc_bytes),
+        "gpu_wavelet_decode": _frac(dec_gpu, dec_bytes),
         "stage_ms": stage_ms,
         "bytes_per_frame": int(np.mean(sizes)),
     }
+    if gather:
+        out["gather"] = {"backend": backend, "bytes_to_rank0_per_step": gathered[0]}
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(W, H, a.q, a.trans, a.cpu_frames, min(16, a.cpu_frames))

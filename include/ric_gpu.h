@@ -144,6 +144,12 @@ int ric_quants(int idx);
 int ric_prof_enable(ric_wavelet* w, int on);
 int ric_prof_read(ric_wavelet* w, double* ms, long* counts, int n);
 ric_wavelet* ric_codec_wavelet(ric_codec* c);
+/* Diagnostics: with RIC_FQ_PC bit 128 set, every level-0 launch of the fused
+ * level kernel records 168 u64 per workgroup: start realtime, start shader
+ * clock, end realtime of waves 0-3, producer HW_ID << 32 | end clock,
+ * XCC_ID << 32 | workgroup index, then per role (producer, D, H, V) 20
+ * (barrier arrival, departure) realtime pairs; copies up to n u64. */
+int ric_diag_wgtrace(int device, uint64_t* out, int n);
 /* SURVEY.md §8(d) synthetic image: channels planes of w*h bytes */
 void ric_synth_image(int w, int h, int channels, int frame, uint8_t* out);
 

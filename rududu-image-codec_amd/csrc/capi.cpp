@@ -923,6 +923,13 @@ int ric_prof_read(ric_wavelet* w, double* ms, long* counts, int n)
 
 ric_wavelet* ric_codec_wavelet(ric_codec* c) { return c ? c->wav : nullptr; }
 
+int ric_diag_wgtrace(int device, uint64_t* out, int n)
+{
+	if (!out || n < 0) return RIC_E_ARG;
+	const int r = diag_wgtrace(device, out, n);
+	return r < 0 ? RIC_E_HIP : r;
+}
+
 // SURVEY.md §8(d) synthetic generator (integer-only, bit-reproducible)
 void ric_synth_image(int w, int h, int channels, int frame, uint8_t* out)
 {

@@ -17,6 +17,7 @@
 // start/tail cases (symmetric extension).
 #include <hip/hip_runtime.h>
 #include <cstdlib>
+#include <mutex>
 #include "ric_types.h"
 #include "ric_kernels.h"
 #include "quant_block.h"
@@ -761,6 +762,8 @@ struct FqArgs {
 	uint8_t* cpin[3]; int cpw[3], cph[3];  // the finer level's parent info, or null
 	int Q[3], iQ[3];
 	int thres[3][16];
+	uint32_t* cu_ctr;                  // k_fwdq_pc producer placement, policy 2 (2048 u32)
+	uint64_t* wgt;                     // diagnostics: per-workgroup timestamps (dbg 128), or null
 };
 
 struct PRow8 { v2s q[4]; };            // (c0,c2) (c4,c6) | (c1,c3) (c5,c7)
@@ -922,6 +925,25 @@ __device__ __forceinline__ void row_fwd97p8x2_edge(PRow8& r, PRow8& s, const FqB
 	u = s.q[1] + b1; s.q[3] += sel(m.oR3, s.q[1] - (s.q[1] >> 4), (u >> 1) - (u >> 5));
 }
 
+// The per-iteration hand-off barrier of k_fwdq_pc.  Only LDS is shared
+// between the producer and the consumers, so the barrier waits for the
+// wave's LDS operations alone (lgkmcnt) -- __syncthreads() would also drain
+// every outstanding global load and store (vmcnt(0) of its workgroup-scope
+// fence), i.e. wait out the producer's row prefetch and everyone's band /
+// record stores once per iteration.  gfx950's s_barrier does not wait for
+// memory by itself; the "memory" clobber keeps the compiler from moving LDS
+// accesses across it.  dbg 1024: the full __syncthreads() (comparison).
+constexpr int kWgIt = 20;                 // diagnostics: traced barrier iterations per wave
+constexpr int kWgRec = 8 + 4 * 2 * kWgIt; // u64 per workgroup record
+// tr (diagnostics, dbg 128): arrival and departure realtime stamps
+__device__ __forceinline__ void pc_barrier(int dbg, uint64_t* tr = nullptr)
+{
+	if (tr && threadIdx.x % 64 == 0) tr[0] = __builtin_amdgcn_s_memrealtime();
+	if (dbg & 1024) __syncthreads();
+	else asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+	if (tr && threadIdx.x % 64 == 0) tr[1] = __builtin_amdgcn_s_memrealtime();
+}
+
 // One wave's segment: the forward 9/7 of rows [y0, y0 + S) of a 496-column
 // strip and the quantiser, records and parent info of the block rows they
 // make, all in registers.  EDGE: the wave touches an image border (m).
@@ -931,7 +953,7 @@ __device__ __forceinline__ void row_fwd97p8x2_edge(PRow8& r, PRow8& s, const FqB
 template <bool EDGE, bool PC = false>
 __device__ __forceinline__ void fq_seg(const FqArgs& a, const int (*thr)[16], const uint32_t (*tpk)[17 * 8],
                                        const FqTables& F, int x, int lane, int y0, int kx, const FqBorder& m, int S,
-                                       uint2 (*pcbuf)[3][4][kLanes] = nullptr, int dbg = 0)
+                                       uint2 (*pcbuf)[3][4][kLanes] = nullptr, int dbg = 0, uint64_t* tr = nullptr)
 {
 	const bool out_lane = lane >= 1 && lane <= kLanes - 2 && (!EDGE || x < a.W);
 	int16_t* pL = a.d[BL] + (long)(y0 >> 1) * a.p[BL] + (x >> 1);
@@ -947,28 +969,24 @@ __device__ __forceinline__ void fq_seg(const FqArgs& a, const int (*thr)[16], co
 	// PC form has the registers for two
 	constexpr int DEPTH = PC ? 2 : 1;
 	uint4 ring[DEPTH][2 * PF];
-	const int16_t* rp = a.src + (long)(y0 - 4) * a.sp + x;
 	int yl = y0 - 4;
-	// border waves: clamped row / column, then a select (no divergent branch,
-	// which would drain every load at the join)
+	// Every row load is unconditional, from a wave-uniform clamped row (the
+	// refills past the segment re-read its last row, an L2 hit): a load under
+	// a branch, or a select on its value, makes the compiler wait for it at
+	// once, and the prefetch ring would degrade to one memory round trip per
+	// row.  Border waves clamp the column too and zero the lanes outside the
+	// image when the row is consumed.
+	const int ylast = min(y0 + S + 3, a.H - 1);
 	const int xcl = EDGE ? min(max(x, 0), a.W - 8) : x;
 	auto load_next = [&](uint4& dst) {
-		if (dbg & 8) {                            // timing experiment: no input loads
-			dst = make_uint4(yl, x, yl ^ x, 7);
-		} else if (!EDGE) {
-			dst = *reinterpret_cast<const uint4*>(rp);
-		} else {
-			uint4 u = *reinterpret_cast<const uint4*>(a.src + (long)min(max(yl, 0), a.H - 1) * a.sp + xcl);
-			asm("" : "+v"(u.x), "+v"(u.y), "+v"(u.z), "+v"(u.w));
-			dst = (m.ld && yl >= 0 && yl < a.H) ? u : make_uint4(0, 0, 0, 0);
-		}
-		rp += a.sp; yl++;
+		const int yc = min(max(yl, 0), ylast);
+		dst = *reinterpret_cast<const uint4*>(a.src + (long)yc * a.sp + xcl);
+		yl++;
 	};
 #pragma unroll
 	for (int d = 0; d < DEPTH; d++) {
 #pragma unroll
-		for (int j = 0; j < 2 * PF; j++)
-			if (d == 0 || d < nit) load_next(ring[d][j]);
+		for (int j = 0; j < 2 * PF; j++) load_next(ring[d][j]);
 	}
 	const v2s z = {0, 0};
 	PRow8 w0, w1, w2, w3, w4, w5;
@@ -1002,15 +1020,17 @@ __device__ __forceinline__ void fq_seg(const FqArgs& a, const int (*thr)[16], co
 	};
 	auto iteration = [&](int it, uint4 (&rg)[2 * PF]) {
 		const bool last = it + 1 == nit;
-		const bool refill = it + DEPTH < nit;
 		cur = it & 1;
 #pragma unroll
 		for (int k = 0; k < PF; k++) {
 			if (EDGE && last && k >= kend) break;
 			const int e = y0 - 4 + 2 * (it * PF + k);   // the pair's even row
-			w4 = prow8_from(rg[2 * k]);
-			w5 = prow8_from(rg[2 * k + 1]);
-			if (refill) { load_next(rg[2 * k]); load_next(rg[2 * k + 1]); }
+			uint4 u0 = rg[2 * k], u1 = rg[2 * k + 1];
+			if (EDGE && !m.ld) { u0 = make_uint4(0, 0, 0, 0); u1 = u0; }
+			w4 = prow8_from(u0);
+			w5 = prow8_from(u1);
+			load_next(rg[2 * k]);
+			load_next(rg[2 * k + 1]);
 			if (EDGE && e < 0) continue;                 // above the image (top segment)
 			if (EDGE) row_fwd97p8x2_edge(w4, w5, m);
 			else row_fwd97p8x2(w4, w5);
@@ -1054,18 +1074,22 @@ __device__ __forceinline__ void fq_seg(const FqArgs& a, const int (*thr)[16], co
 			w0 = w2; w1 = w3;
 			emit(3);
 		}
-		if constexpr (PC) __syncthreads();           // the consumers take the block row
+		if constexpr (PC) pc_barrier(dbg, tr ? tr + 2 * min(it, kWgIt - 1) : nullptr);   // the consumers take the block row
 		else if (it >= 1) quant_row((y0 >> 3) + it - 1);   // a block row is complete
 	};
 	if constexpr (DEPTH == 1) {
 #pragma unroll 1
 		for (int it = 0; it < nit; it++) iteration(it, ring[0]);
 	} else {
+		// pairs of iterations, then the odd one out: a conditional second
+		// iteration would put its refills under a branch (see load_next)
+		int it = 0;
 #pragma unroll 1
-		for (int it = 0; it < nit; it += 2) {
+		for (; it + 1 < nit; it += 2) {
 			iteration(it, ring[0]);
-			if (it + 1 < nit) iteration(it + 1, ring[1]);
+			iteration(it + 1, ring[1]);
 		}
+		if (it < nit) iteration(it, ring[0]);
 	}
 }
 
@@ -1126,45 +1150,113 @@ __global__ void __launch_bounds__(256, 3) k_fwdq_fast(FqArgs a)
 // of resident workgroups.  The producer role rotates over the four waves with
 // the workgroup index, so the lifting chains of the workgroups on a CU spread
 // over its four SIMDs.
+// Producer placement.  The lifting chain is the segment's critical path and
+// runs at the issue rate of one wave alone only if no other producer shares
+// its SIMD; the workgroups resident on a CU must therefore put their
+// producers on different SIMDs.  Block indices say nothing about which
+// workgroups share a CU, so the placement reads the hardware:
+//   policy 1 -- HW_REG_HW_ID of every wave (SIMD_ID 5:4, WAVE_ID 3:0 = the
+//               wave slot on its SIMD, allocated in arrival order): the
+//               producer is the wave on SIMD (slot of wave 0) & 3;
+//   policy 2 -- a per-CU arrival counter (one u32 atomic per workgroup,
+//               indexed by XCC/SE/SH/CU id): the k-th workgroup on a CU puts
+//               its producer on SIMD k & 3;
+//   policy 0 -- the block-index rotation (no hardware information).
+// All waves read the same LDS words after a barrier, so they agree on the
+// roles whatever the placement turns out to be.
+constexpr uint32_t kHwRegHwId = (31u << 11) | 4u;    // hwreg(HW_REG_HW_ID, 0, 32)
+constexpr uint32_t kHwRegXcc = (3u << 11) | 20u;     // hwreg(HW_REG_XCC_ID, 0, 4)
+constexpr int kWgTraceMax = 8192;
+
+__device__ __forceinline__ int fq_producer_wave(int policy, uint32_t* cu_ctr, uint32_t* s_hw, int w)
+{
+	const uint32_t hw = __builtin_amdgcn_s_getreg(kHwRegHwId);
+	if (threadIdx.x % 64 == 0) s_hw[w] = hw;
+	if (policy == 2 && threadIdx.x == 0) {
+		const uint32_t xcc = __builtin_amdgcn_s_getreg(kHwRegXcc) & 7u;
+		const uint32_t cu = (hw >> 8) & 15u, sh = (hw >> 12) & 1u, se = (hw >> 13) & 7u;
+		s_hw[4] = atomicAdd(cu_ctr + ((((xcc << 3) | se) << 1 | sh) << 4 | cu), 1u);
+	}
+	__syncthreads();
+	uint32_t target;
+	if (policy == 2) target = s_hw[4] & 3u;
+	else target = s_hw[0] & 3u;                        // wave slot of wave 0
+	int p = (int)target;                               // fallback: wave index
+#pragma unroll
+	for (int k = 3; k >= 0; k--)
+		if (((s_hw[k] >> 4) & 3u) == target) p = k;
+	return p;
+}
+
 __global__ void __launch_bounds__(256, 4) k_fwdq_pc(FqArgs a, int S, int dbg)
 {
 	__shared__ int s_thres[3][16];
 	__shared__ FqTables s_F __attribute__((aligned(16)));
 	__shared__ uint32_t s_tpk[3][17 * 8];
 	__shared__ uint2 s_buf[2][3][4][kLanes];
+	__shared__ uint32_t s_hw[5];
+	// dbg 128 (diagnostics, level 0 only): per-workgroup record of 8 u64 --
+	// start realtime (100 MHz), start shader clock, the end realtime of waves
+	// 0-3, producer hw id << 32 | end shader clock of wave 0, workgroup index
+	const int wgi = blockIdx.y * gridDim.x + blockIdx.x;
+	uint64_t* wgt = ((dbg & 128) && a.wgt && wgi < kWgTraceMax) ? a.wgt + kWgRec * wgi : nullptr;
+	if (wgt && threadIdx.x == 0) {
+		wgt[0] = __builtin_amdgcn_s_memrealtime();
+		wgt[1] = __builtin_amdgcn_s_memtime();
+	}
 	fq_stage_tables(a, s_thres, s_F, s_tpk);
-	__syncthreads();
+	const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+	const int policy = (dbg >> 8) & 3;
+	int wave;                                                   // role: 0 = producer, 1..3 = D, H, V
+	if (policy == 0) {
+		__syncthreads();
+		wave = (w + blockIdx.x + blockIdx.y) & 3;
+	} else {
+		wave = (w - fq_producer_wave(policy, a.cu_ctr, s_hw, w)) & 3;   // (its barrier covers the tables)
+	}
+	wave = __builtin_amdgcn_readfirstlane(wave);
 	const int lane = threadIdx.x & 63;
-	const int strip = (dbg & 4) ? 1 : blockIdx.x, seg = (dbg & 4) ? 2 : blockIdx.y;
-	const int wave = (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) + blockIdx.x + blockIdx.y) & 3;   // role
+	// dbg 4: one workgroup (strip 1, or strip 0 with dbg 64), timing only
+	const int strip = (dbg & 4) ? ((dbg & 64) ? 0 : 1) : blockIdx.x, seg = (dbg & 4) ? 2 : blockIdx.y;
 	const int X0 = strip * kFqStrip - 8, x = X0 + lane * 8, y0 = seg * S;
 	const int kx = strip * (kFqStrip / 8) + lane - 1;
 	FqBorder m;
 	m.top = y0 == 0;
 	m.bottom = y0 + S >= a.H;
 	const bool edge = X0 < 0 || X0 + kLanes * 8 >= a.W || m.top || m.bottom;
+	if ((dbg & 32) && edge) return;   // timing experiment: interior workgroups only (results invalid)
 	const int nit = m.bottom ? (a.H - y0) / 8 + 1 : S / 8 + 1;
 	if (wave == 0) {
+		// the lifting chain is the segment's critical path: it issues ahead
+		// of the consumer waves of other workgroups on its SIMD (dbg 2048: off)
+		if (!(dbg & 2048)) __builtin_amdgcn_s_setprio(2);
 		if (edge) {
 			m.eL0 = x == 0 ? 0x0000FFFFu : 0u;
 			m.oR3 = x + 7 == a.W - 1 ? 0xFFFF0000u : 0u;
 			m.ld = x >= 0 && x < a.W;
-			fq_seg<true, true>(a, s_thres, s_tpk, s_F, x, lane, y0, kx, m, S, s_buf, dbg);
+			fq_seg<true, true>(a, s_thres, s_tpk, s_F, x, lane, y0, kx, m, S, s_buf, dbg, wgt ? wgt + 8 : nullptr);
 		} else {
-			fq_seg<false, true>(a, s_thres, s_tpk, s_F, x, lane, y0, kx, m, S, s_buf, dbg);
+			fq_seg<false, true>(a, s_thres, s_tpk, s_F, x, lane, y0, kx, m, S, s_buf, dbg, wgt ? wgt + 8 : nullptr);
 		}
 	} else {
 		const int b = wave - 1;
 		const bool out_lane = lane >= 1 && lane <= kLanes - 2 && x < a.W;
 #pragma unroll 1
 		for (int it = 0; it < nit; it++) {
-			__syncthreads();                     // matches the producer's iteration `it`
+			pc_barrier(dbg, wgt ? wgt + 8 + wave * 2 * kWgIt + 2 * min(it, kWgIt - 1) : nullptr);   // matches the producer's iteration `it`
 			if (it == 0 || (dbg & 3) == 2) continue;     // dbg 2: timing of the lifting alone
 			uint2 buf[4];
 #pragma unroll
 			for (int r = 0; r < 4; r++) buf[r] = s_buf[it & 1][b][r][lane];
 			fq_block_regs(a, s_thres[b], s_tpk[b], s_F, b, buf, kx, (y0 >> 3) + it - 1, out_lane);
 		}
+	}
+	if (wgt && lane == 0) {
+		const int w0 = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+		wgt[2 + w0] = __builtin_amdgcn_s_memrealtime();
+		if (wave == 0) wgt[6] = ((uint64_t)__builtin_amdgcn_s_getreg(kHwRegHwId) << 32) |
+		                        (uint32_t)__builtin_amdgcn_s_memtime();
+		if (w0 == 0) wgt[7] = (uint64_t)wgi | ((uint64_t)__builtin_amdgcn_s_getreg(kHwRegXcc) << 32);
 	}
 }
 
@@ -1179,6 +1271,33 @@ int fq_pc()
 {
 	static const int v = [] { const char* e = getenv("RIC_FQ_PC"); return e ? atoi(e) : 1; }();
 	return v;
+}
+
+// producer placement policy of k_fwdq_pc (see fq_producer_wave)
+int fq_role_policy()
+{
+	static const int v = [] { const char* e = getenv("RIC_FQ_ROLE"); return e ? atoi(e) & 3 : 1; }();
+	return v;
+}
+
+// per-device CU arrival counters (policy 2): monotonic, never reset (k & 3
+// only needs the increments)
+uint32_t* fq_cu_counters()
+{
+	static std::mutex mu;
+	static uint32_t* ctr[64] = {};
+	int dev = 0;
+	if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+	std::lock_guard<std::mutex> g(mu);
+	uint32_t*& c = ctr[dev & 63];
+	if (!c) {
+		if (hipMalloc(&c, 2048 * sizeof(uint32_t)) != hipSuccess) { c = nullptr; return nullptr; }
+		if (hipMemset(c, 0, 2048 * sizeof(uint32_t)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+			(void)hipFree(c);
+			c = nullptr;
+		}
+	}
+	return c;
 }
 
 template <int S>
@@ -1203,6 +1322,20 @@ int pc_seg_rows(int W, int H)
 	return s < 8 ? 8 : s;
 }
 
+// diagnostics: per-device workgroup trace buffer of k_fwdq_pc (dbg 128)
+uint64_t* g_wgtrace[64] = {};
+std::mutex g_wgtrace_mu;
+uint64_t* fq_wgtrace()
+{
+	int dev = 0;
+	if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+	std::lock_guard<std::mutex> g(g_wgtrace_mu);
+	uint64_t*& b = g_wgtrace[dev & 63];
+	if (!b && hipMalloc(&b, (size_t)kWgTraceMax * kWgRec * sizeof(uint64_t)) != hipSuccess) b = nullptr;
+	if (b) (void)hipMemset(b, 0, (size_t)kWgTraceMax * kWgRec * sizeof(uint64_t));
+	return b;
+}
+
 void fq_launch_pc(FqArgs& a, hipStream_t st)
 {
 	const int S = pc_seg_rows(a.W, a.H);
@@ -1210,8 +1343,14 @@ void fq_launch_pc(FqArgs& a, hipStream_t st)
 	const int nstrip = (a.W + kFqStrip - 1) / kFqStrip;
 	static const int onewg = [] { const char* e = getenv("RIC_FQ_ONEWG"); return e ? atoi(e) : 0; }();
 	// RIC_FQ_ONEWG=1: one interior workgroup only (latency of one segment; results invalid)
-	if (onewg) hipLaunchKernelGGL(k_fwdq_pc, dim3(1, 1), dim3(256), 0, st, a, S, fq_pc() | 4);
-	else hipLaunchKernelGGL(k_fwdq_pc, dim3(nstrip, a.nseg), dim3(256), 0, st, a, S, fq_pc());
+	int policy = fq_role_policy();
+	a.cu_ctr = nullptr;
+	if (policy == 2 && !(a.cu_ctr = fq_cu_counters())) policy = 1;
+	int dbg = fq_pc() | (policy << 8);
+	a.wgt = nullptr;
+	if ((dbg & 128) && a.high && !(a.wgt = fq_wgtrace())) dbg &= ~128;
+	if (onewg) hipLaunchKernelGGL(k_fwdq_pc, dim3(1, 1), dim3(256), 0, st, a, S, dbg | 4);
+	else hipLaunchKernelGGL(k_fwdq_pc, dim3(nstrip, a.nseg), dim3(256), 0, st, a, S, dbg);
 }
 
 // ------------------------------ generic fused forward level + quantiser
@@ -1756,6 +1895,8 @@ void launch_fwdq_level(const Pyramid& P, int l, const void* src, long sp, int ve
 {
 	const Level& L = P.L[l];
 	FqArgs a;
+	a.cu_ctr = nullptr;
+	a.wgt = nullptr;
 	a.src = (const int16_t*)src; a.sp = sp; a.W = L.w; a.H = L.h;
 	a.vec8 = vec8; a.vec16 = vec16; a.nofast = dbg_nofast(); a.high = l == 0;
 	for (int b = 0; b < 4; b++) { a.d[b] = (int16_t*)(arena + L.b[b].off); a.p[b] = L.b[b].pitch; }
@@ -1787,6 +1928,8 @@ void launch_fwdq_gen_level(const Pyramid& P, int l, const void* src, long sp, in
 {
 	const Level& L = P.L[l];
 	FqArgs a;
+	a.cu_ctr = nullptr;
+	a.wgt = nullptr;
 	a.src = (const int16_t*)src; a.sp = sp; a.W = L.w; a.H = L.h;
 	a.vec8 = vec8; a.vec16 = 0; a.nofast = 1; a.high = l == 0;
 	for (int b = 0; b < 4; b++) { a.d[b] = (int16_t*)(arena + L.b[b].off); a.p[b] = L.b[b].pitch; }
@@ -1823,4 +1966,23 @@ void launch_inv_level(const Level& L, const Band& lls, char* arena, void* out, l
 	else inv_dispatch<HAAR>(L, lls, arena, out, po, out_is_int, st);
 }
 
+}  // namespace ric
+
+namespace ric {
+// diagnostics (include/ric_gpu.h ric_diag_wgtrace): copy the level-0
+// workgroup trace of the last k_fwdq_pc launch traced on `device`
+int diag_wgtrace(int device, uint64_t* host, int n)
+{
+	if (hipSetDevice(device) != hipSuccess) return -1;
+	uint64_t* b;
+	{
+		std::lock_guard<std::mutex> g(g_wgtrace_mu);
+		b = g_wgtrace[device & 63];
+	}
+	if (!b) return 0;
+	if (n > kWgTraceMax * kWgRec) n = kWgTraceMax * kWgRec;
+	if (hipDeviceSynchronize() != hipSuccess || hipMemcpy(host, b, (size_t)n * 8, hipMemcpyDeviceToHost) != hipSuccess)
+		return -1;
+	return n;
+}
 }  // namespace ric

@@ -50,5 +50,7 @@ void launch_blocks_level(const Pyramid& P, int l, bool do_rec, bool do_pin, char
 void launch_tsuq_band(const Band& B, int iQ, int T0, char* arena, unsigned int* count, hipStream_t st);
 // CBand::TSUQi on one band (src/lib/band.h:94-107).
 void launch_dequant_band(const Band& B, int q, char* arena, hipStream_t st);
+// diagnostics: the level-0 workgroup trace of the fused level kernel (dwt.hip)
+int diag_wgtrace(int device, uint64_t* host, int n);
 
 }  // namespace ric

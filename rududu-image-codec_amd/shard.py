@@ -62,10 +62,11 @@ def unpack_tiles(blob):
     return W, H, nx, ny, streams
 
 
-def gather_streams(local, dist, device=None):
+def gather_streams(local, dist, device=None, to_host=True):
     """All ranks pass their list of byte streams; rank 0 gets every rank's
     list (in rank order), other ranks get None.  Two collectives: sizes, then
-    the padded payloads."""
+    the padded payloads.  to_host=False: rank 0 gets (payload tensors, size
+    tensors) per rank as they arrived on `device` (size tensor = [n, len...])."""
     import torch
     world = dist.get_world_size()
     rank = dist.get_rank()
@@ -89,6 +90,8 @@ def gather_streams(local, dist, device=None):
     dist.all_gather(all_buf, buf)
     if rank != 0:
         return None
+    if not to_host:
+        return all_buf, all_sz
     out = []
     for r in range(world):
         n = int(all_sz[r][0])

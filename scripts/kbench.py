@@ -22,6 +22,49 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "rududu-image-codec_amd"))
 
 
+def wgtrace_summary(ric_amd, path):
+    """Per-workgroup timeline of the last traced level-0 launch: dispatch ramp,
+    durations, producer SIMD placement; raw records go to `path`."""
+    REC = 168
+    n = 8192 * REC
+    buf = np.zeros(n, np.uint64)
+    got = ric_amd.lib().ric_diag_wgtrace(0, buf.ctypes.data, n)
+    r = buf[:max(got, 0)].reshape(-1, REC)
+    r = r[r[:, 0] != 0]
+    if not len(r):
+        return None
+    t0 = r[:, 0].min()
+    start = (r[:, 0] - t0) * 10.0 / 1e3            # us (100 MHz realtime)
+    end = (r[:, 2:6].max(axis=1) - t0) * 10.0 / 1e3
+    prod_end = np.zeros(len(r))
+    hw = (r[:, 6] >> np.uint64(32)).astype(np.int64)
+    clk = (r[:, 6] & np.uint64(0xFFFFFFFF)).astype(np.int64) - (r[:, 1] & np.uint64(0xFFFFFFFF)).astype(np.int64)
+    clk %= 1 << 32
+    dur = end - start
+    simd = (hw >> 4) & 3
+    cu = (hw >> 8) & 15
+    sh = (hw >> 12) & 1
+    se = (hw >> 13) & 7
+    xcc = (r[:, 7] >> np.uint64(32)).astype(np.int64) & 7
+    key = ((xcc * 8 + se) * 2 + sh) * 16 + cu
+    per_cu = {}
+    for k, s_ in zip(key, simd):
+        per_cu.setdefault(int(k), []).append(int(s_))
+    same = sum(1 for v in per_cu.values() if len(v) != len(set(v)))
+    ghz = np.median(clk / np.maximum(dur, 1e-3) / 1e3)
+    np.save(path + ".npy", r)
+    summ = {"wgs": int(len(r)), "span_us": round(float(end.max()), 2),
+            "start_us_pct": [round(float(np.percentile(start, p)), 2) for p in (0, 10, 50, 90, 100)],
+            "dur_us_pct": [round(float(np.percentile(dur, p)), 2) for p in (0, 10, 50, 90, 100)],
+            "end_us_pct": [round(float(np.percentile(end, p)), 2) for p in (0, 10, 50, 90, 100)],
+            "cus": len(per_cu), "wgs_per_cu_max": max(len(v) for v in per_cu.values()),
+            "cus_with_shared_producer_simd": same, "shader_ghz_median": round(float(ghz), 3)}
+    import json as _j
+    with open(path, "w") as f:
+        _j.dump(summ, f, indent=1)
+    return summ
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
@@ -29,6 +72,7 @@ def main():
     ap.add_argument("--width", type=int, default=7680)
     ap.add_argument("--height", type=int, default=4320)
     ap.add_argument("--codec", action="store_true")
+    ap.add_argument("--wgtrace", default="", help="write the level-0 workgroup trace summary (needs RIC_FQ_PC bit 128) to this json")
     a = ap.parse_args()
     import torch
     torch.cuda.init()
@@ -54,6 +98,8 @@ def main():
     enc = out["wavelet_ms"].get("fwd", 0) + out["wavelet_ms"].get("quant", 0)
     if enc:
         out["wavelet_encode_GBps"] = round(9.851 * W * H / (enc * 1e-3) / 1e9, 1)
+    if a.wgtrace:
+        out["wgtrace"] = wgtrace_summary(ric_amd, a.wgtrace)
     if a.codec:
         c = ric_amd.Codec(W, H, 1)
         dpix = torch.from_numpy(pix).cuda()

@@ -57,7 +57,12 @@ def _worker(rank, world, port, q):
     frames = S.frames_of_rank(7, world, rank)
     local = [(b"frame%d:" % f) * (f + 1) for f in frames]
     res = S.gather_streams(local, dist)
-    q.put((rank, res))
+    dev = S.gather_streams(local, dist, to_host=False)   # bench.py's form
+    if dev is not None:
+        bufs, szs = dev
+        dev = [[bytes(b[int(s[1:1 + i].sum()):int(s[1:2 + i].sum())].numpy()) for i in range(int(s[0]))]
+               for b, s in zip(bufs, szs)]
+    q.put((rank, (res, dev)))
     dist.destroy_process_group()
 
 
@@ -72,8 +77,9 @@ def test_gather_streams_gloo_world2():
     out = dict(q.get(timeout=120) for _ in range(2))
     for p in ps:
         p.join(timeout=60)
-    assert out[1] is None
-    got = out[0]
+    assert out[1] == (None, None)
+    got, got_dev = out[0]
+    assert got_dev == got
     assert [len(x) for x in got] == [4, 3]
     flat = {}
     for r, lst in enumerate(got):
