@@ -210,6 +210,40 @@ int inverse(ric_wavelet* w, int16_t* dimg, long stride, int trans)
 	return RIC_OK;
 }
 
+// CWavelet2D::TSUQi fused into TransformI (the codec's decode path): the
+// bands stay quantised in HBM and every inverse level multiplies the band
+// values it loads by their TSUQi factor (src/lib/band.h:94-107,
+// src/lib/wavelet2d.cpp:248-268); the coarsest level also its LL.
+int tsuqi_factor(const Band& B, int quant)
+{
+	const bool sh = !B.is_int;
+	int q = tr_any(sh, quant);
+	q = tr_any(sh, (int)((float)q / B.weight));
+	return q == 0 ? 1 : q;
+}
+
+int inverse_deq(ric_wavelet* w, int16_t* dimg, long stride, int trans, int quant)
+{
+	Pyramid& P = w->P;
+	int rc = to_device(w);
+	if (rc) return rc;
+	w->prof.begin(S_INV, w->st);
+	for (int l = P.nlev - 1; l >= 0; l--) {
+		const Level& L = P.L[l];
+		void* out;
+		long po;
+		int out_int;
+		if (l == 0) { out = dimg; po = stride; out_int = 0; }
+		else { const Band& LL = P.L[l - 1].b[BL]; out = w->d_arena + LL.off; po = LL.pitch; out_int = LL.is_int; }
+		const int q[4] = {tsuqi_factor(L.b[BD], quant), tsuqi_factor(L.b[BH], quant), tsuqi_factor(L.b[BV], quant),
+		                  l + 1 == P.nlev ? tsuqi_factor(L.b[BL], quant) : 1};
+		launch_inv_level(L, L.b[BL], w->d_arena, out, po, out_int, trans, w->st, q);
+	}
+	w->prof.end(S_INV, w->st);
+	HIPCHK(hipGetLastError());
+	return RIC_OK;
+}
+
 // buildTree parameters of level l (src/lib/bandcodec.cpp:243-247, float32 as
 // the reference); qin carries CodeBand's per-level C-typed Quant.
 QuantParams level_qp(const Pyramid& P, int l, int& qin, int lambda)
@@ -325,12 +359,15 @@ int flush_pending(ric_wavelet* w)
 	return forward(w, w->d_img, (long)w->img_pitch, w->pend_trans);
 }
 
-// The host half: bands + records to the pinned mirror, then the serial coder.
-int code_band_host(ric_wavelet* w, Mux& m)
+// The host half: bands + records to the pinned mirror (unless the caller
+// copied them already), then the serial coder.
+int code_band_host(ric_wavelet* w, Mux& m, bool copy = true)
 {
 	Pyramid& P = w->P;
-	int rc = to_host(w, true);
-	if (rc) return rc;
+	if (copy) {
+		int rc = to_host(w, true);
+		if (rc) return rc;
+	}
 	// serial part: LL DPCM, then coarse -> fine, V, H, D (wavelet2d.cpp:119-159)
 	const double t0 = now_ms();
 	pred_encode(m, view(w, P.coarsest_ll()));
@@ -796,9 +833,12 @@ int ric_codec_encode(ric_codec* c, const uint8_t* pix, int on_device, int q, int
 			int rc = encode_gpu(w, c->d_planes + p * plane, c->pitch, trans,
 			                    q ? ric_quants(q + 20 + boost) : 0, q ? ric_quants(q + 13 + boost) : 0);
 			if (rc) return rc;
-			HIPCHK(hipStreamSynchronize(w->st));
+			// the copy runs inside the section too: its blit kernels would
+			// otherwise share the CUs with another codec's level kernels
+			rc = to_host(w, true);
+			if (rc) return rc;
 		}
-		int rc = code_band_host(w, m);
+		int rc = code_band_host(w, m, false);
 		if (rc) return rc;
 	}
 	uint8_t* e = m.end_coding();
@@ -838,11 +878,11 @@ int ric_codec_decode(ric_codec* c, const uint8_t* ric, size_t len, int dither,
 		const int boost = p ? 8 : 0;
 		rc = decode_band(w, m);
 		if (rc && rc != RIC_E_STREAM) return rc;
+		GpuSection gs(c->device);
 		rc = to_device(w);
 		if (rc) return rc;
-		GpuSection gs(c->device);
-		if (q) { rc = tsuqi(w, ric_quants(q + 20 + boost)); if (rc) return rc; }
-		rc = inverse(w, c->d_planes + p * plane, c->pitch, trans);
+		rc = q ? inverse_deq(w, c->d_planes + p * plane, c->pitch, trans, ric_quants(q + 20 + boost))
+		       : inverse(w, c->d_planes + p * plane, c->pitch, trans);
 		if (rc) return rc;
 		HIPCHK(hipStreamSynchronize(w->st));
 	}

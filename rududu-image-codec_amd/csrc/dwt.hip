@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdlib>
 #include <mutex>
+#include <type_traits>
 #include "ric_types.h"
 #include "ric_kernels.h"
 #include "quant_block.h"
@@ -72,6 +73,17 @@ __device__ __forceinline__ void load2(const T* __restrict__ row, int bx, int dx,
 	const int v0 = pinned((int)row[min(max(bx, 0), hi)]), v1 = pinned((int)row[min(max(bx + 1, 0), hi)]);
 	a = (bx >= 0 && bx < dx) ? v0 : 0;
 	b = (bx + 1 >= 0 && bx + 1 < dx) ? v1 : 0;
+}
+
+// a register copy the compiler cannot fold away
+__device__ __forceinline__ uint4 opaque_copy(const uint4& v)
+{
+	uint4 r;
+	asm volatile("v_mov_b32 %0, %1" : "=v"(r.x) : "v"(v.x));
+	asm volatile("v_mov_b32 %0, %1" : "=v"(r.y) : "v"(v.y));
+	asm volatile("v_mov_b32 %0, %1" : "=v"(r.z) : "v"(v.z));
+	asm volatile("v_mov_b32 %0, %1" : "=v"(r.w) : "v"(v.w));
+	return r;
 }
 
 // Neighbour exchange across lanes with DPP wave shifts (GFX9 wave_shr:1 /
@@ -762,7 +774,6 @@ struct FqArgs {
 	uint8_t* cpin[3]; int cpw[3], cph[3];  // the finer level's parent info, or null
 	int Q[3], iQ[3];
 	int thres[3][16];
-	uint32_t* cu_ctr;                  // k_fwdq_pc producer placement, policy 2 (2048 u32)
 	uint64_t* wgt;                     // diagnostics: per-workgroup timestamps (dbg 128), or null
 };
 
@@ -950,10 +961,17 @@ __device__ __forceinline__ void pc_barrier(int dbg, uint64_t* tr = nullptr)
 // PC (producer-consumer mode, k_fwdq_pc): this wave only lifts; each
 // completed block row goes to the LDS double buffer `pcbuf` and every loop
 // iteration ends in a workgroup barrier that the consumer waves match.
-template <bool EDGE, bool PC = false>
+struct NoStage {
+	__device__ void operator()() const {}
+};
+
+// stage(): called once the prologue row loads are in flight (k_fwdq_pc
+// stages the format tables there, so their latency overlaps the loads')
+template <bool EDGE, bool PC = false, typename Stage = NoStage>
 __device__ __forceinline__ void fq_seg(const FqArgs& a, const int (*thr)[16], const uint32_t (*tpk)[17 * 8],
                                        const FqTables& F, int x, int lane, int y0, int kx, const FqBorder& m, int S,
-                                       uint2 (*pcbuf)[3][4][kLanes] = nullptr, int dbg = 0, uint64_t* tr = nullptr)
+                                       uint2 (*pcbuf)[3][4][kLanes] = nullptr, int dbg = 0, uint64_t* tr = nullptr,
+                                       const Stage& stage = Stage())
 {
 	const bool out_lane = lane >= 1 && lane <= kLanes - 2 && (!EDGE || x < a.W);
 	int16_t* pL = a.d[BL] + (long)(y0 >> 1) * a.p[BL] + (x >> 1);
@@ -988,6 +1006,7 @@ __device__ __forceinline__ void fq_seg(const FqArgs& a, const int (*thr)[16], co
 #pragma unroll
 		for (int j = 0; j < 2 * PF; j++) load_next(ring[d][j]);
 	}
+	stage();
 	const v2s z = {0, 0};
 	PRow8 w0, w1, w2, w3, w4, w5;
 #pragma unroll
@@ -1150,71 +1169,32 @@ __global__ void __launch_bounds__(256, 3) k_fwdq_fast(FqArgs a)
 // of resident workgroups.  The producer role rotates over the four waves with
 // the workgroup index, so the lifting chains of the workgroups on a CU spread
 // over its four SIMDs.
-// Producer placement.  The lifting chain is the segment's critical path and
-// runs at the issue rate of one wave alone only if no other producer shares
-// its SIMD; the workgroups resident on a CU must therefore put their
-// producers on different SIMDs.  Block indices say nothing about which
-// workgroups share a CU, so the placement reads the hardware:
-//   policy 1 -- HW_REG_HW_ID of every wave (SIMD_ID 5:4, WAVE_ID 3:0 = the
-//               wave slot on its SIMD, allocated in arrival order): the
-//               producer is the wave on SIMD (slot of wave 0) & 3;
-//   policy 2 -- a per-CU arrival counter (one u32 atomic per workgroup,
-//               indexed by XCC/SE/SH/CU id): the k-th workgroup on a CU puts
-//               its producer on SIMD k & 3;
-//   policy 0 -- the block-index rotation (no hardware information).
-// All waves read the same LDS words after a barrier, so they agree on the
-// roles whatever the placement turns out to be.
 constexpr uint32_t kHwRegHwId = (31u << 11) | 4u;    // hwreg(HW_REG_HW_ID, 0, 32)
 constexpr uint32_t kHwRegXcc = (3u << 11) | 20u;     // hwreg(HW_REG_XCC_ID, 0, 4)
 constexpr int kWgTraceMax = 8192;
 
-__device__ __forceinline__ int fq_producer_wave(int policy, uint32_t* cu_ctr, uint32_t* s_hw, int w)
-{
-	const uint32_t hw = __builtin_amdgcn_s_getreg(kHwRegHwId);
-	if (threadIdx.x % 64 == 0) s_hw[w] = hw;
-	if (policy == 2 && threadIdx.x == 0) {
-		const uint32_t xcc = __builtin_amdgcn_s_getreg(kHwRegXcc) & 7u;
-		const uint32_t cu = (hw >> 8) & 15u, sh = (hw >> 12) & 1u, se = (hw >> 13) & 7u;
-		s_hw[4] = atomicAdd(cu_ctr + ((((xcc << 3) | se) << 1 | sh) << 4 | cu), 1u);
-	}
-	__syncthreads();
-	uint32_t target;
-	if (policy == 2) target = s_hw[4] & 3u;
-	else target = s_hw[0] & 3u;                        // wave slot of wave 0
-	int p = (int)target;                               // fallback: wave index
-#pragma unroll
-	for (int k = 3; k >= 0; k--)
-		if (((s_hw[k] >> 4) & 3u) == target) p = k;
-	return p;
-}
-
+// Roles are static (wave (index + block x + block y) & 3 lifts): placing the
+// producers on distinct SIMDs by HW_ID made no measurable difference, and a
+// role known before the first barrier lets the producer issue its prologue
+// row loads before the workgroup stages the format tables.
 __global__ void __launch_bounds__(256, 4) k_fwdq_pc(FqArgs a, int S, int dbg)
 {
 	__shared__ int s_thres[3][16];
 	__shared__ FqTables s_F __attribute__((aligned(16)));
 	__shared__ uint32_t s_tpk[3][17 * 8];
 	__shared__ uint2 s_buf[2][3][4][kLanes];
-	__shared__ uint32_t s_hw[5];
-	// dbg 128 (diagnostics, level 0 only): per-workgroup record of 8 u64 --
+	// dbg 128 (diagnostics, level 0 only): per-workgroup record of kWgRec u64 --
 	// start realtime (100 MHz), start shader clock, the end realtime of waves
-	// 0-3, producer hw id << 32 | end shader clock of wave 0, workgroup index
+	// 0-3, producer hw id << 32 | end shader clock of wave 0, workgroup index,
+	// then the barrier stamps of each role
 	const int wgi = blockIdx.y * gridDim.x + blockIdx.x;
 	uint64_t* wgt = ((dbg & 128) && a.wgt && wgi < kWgTraceMax) ? a.wgt + kWgRec * wgi : nullptr;
 	if (wgt && threadIdx.x == 0) {
 		wgt[0] = __builtin_amdgcn_s_memrealtime();
 		wgt[1] = __builtin_amdgcn_s_memtime();
 	}
-	fq_stage_tables(a, s_thres, s_F, s_tpk);
 	const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-	const int policy = (dbg >> 8) & 3;
-	int wave;                                                   // role: 0 = producer, 1..3 = D, H, V
-	if (policy == 0) {
-		__syncthreads();
-		wave = (w + blockIdx.x + blockIdx.y) & 3;
-	} else {
-		wave = (w - fq_producer_wave(policy, a.cu_ctr, s_hw, w)) & 3;   // (its barrier covers the tables)
-	}
-	wave = __builtin_amdgcn_readfirstlane(wave);
+	const int wave = __builtin_amdgcn_readfirstlane((w + blockIdx.x + blockIdx.y) & 3);   // 0 = producer, 1..3 = D, H, V
 	const int lane = threadIdx.x & 63;
 	// dbg 4: one workgroup (strip 1, or strip 0 with dbg 64), timing only
 	const int strip = (dbg & 4) ? ((dbg & 64) ? 0 : 1) : blockIdx.x, seg = (dbg & 4) ? 2 : blockIdx.y;
@@ -1226,6 +1206,10 @@ __global__ void __launch_bounds__(256, 4) k_fwdq_pc(FqArgs a, int S, int dbg)
 	const bool edge = X0 < 0 || X0 + kLanes * 8 >= a.W || m.top || m.bottom;
 	if ((dbg & 32) && edge) return;   // timing experiment: interior workgroups only (results invalid)
 	const int nit = m.bottom ? (a.H - y0) / 8 + 1 : S / 8 + 1;
+	auto stage = [&]() {
+		fq_stage_tables(a, s_thres, s_F, s_tpk);
+		__syncthreads();
+	};
 	if (wave == 0) {
 		// the lifting chain is the segment's critical path: it issues ahead
 		// of the consumer waves of other workgroups on its SIMD (dbg 2048: off)
@@ -1234,11 +1218,12 @@ __global__ void __launch_bounds__(256, 4) k_fwdq_pc(FqArgs a, int S, int dbg)
 			m.eL0 = x == 0 ? 0x0000FFFFu : 0u;
 			m.oR3 = x + 7 == a.W - 1 ? 0xFFFF0000u : 0u;
 			m.ld = x >= 0 && x < a.W;
-			fq_seg<true, true>(a, s_thres, s_tpk, s_F, x, lane, y0, kx, m, S, s_buf, dbg, wgt ? wgt + 8 : nullptr);
+			fq_seg<true, true>(a, s_thres, s_tpk, s_F, x, lane, y0, kx, m, S, s_buf, dbg, wgt ? wgt + 8 : nullptr, stage);
 		} else {
-			fq_seg<false, true>(a, s_thres, s_tpk, s_F, x, lane, y0, kx, m, S, s_buf, dbg, wgt ? wgt + 8 : nullptr);
+			fq_seg<false, true>(a, s_thres, s_tpk, s_F, x, lane, y0, kx, m, S, s_buf, dbg, wgt ? wgt + 8 : nullptr, stage);
 		}
 	} else {
+		stage();
 		const int b = wave - 1;
 		const bool out_lane = lane >= 1 && lane <= kLanes - 2 && x < a.W;
 #pragma unroll 1
@@ -1252,11 +1237,10 @@ __global__ void __launch_bounds__(256, 4) k_fwdq_pc(FqArgs a, int S, int dbg)
 		}
 	}
 	if (wgt && lane == 0) {
-		const int w0 = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-		wgt[2 + w0] = __builtin_amdgcn_s_memrealtime();
+		wgt[2 + w] = __builtin_amdgcn_s_memrealtime();
 		if (wave == 0) wgt[6] = ((uint64_t)__builtin_amdgcn_s_getreg(kHwRegHwId) << 32) |
 		                        (uint32_t)__builtin_amdgcn_s_memtime();
-		if (w0 == 0) wgt[7] = (uint64_t)wgi | ((uint64_t)__builtin_amdgcn_s_getreg(kHwRegXcc) << 32);
+		if (w == 0) wgt[7] = (uint64_t)wgi | ((uint64_t)__builtin_amdgcn_s_getreg(kHwRegXcc) << 32);
 	}
 }
 
@@ -1271,33 +1255,6 @@ int fq_pc()
 {
 	static const int v = [] { const char* e = getenv("RIC_FQ_PC"); return e ? atoi(e) : 1; }();
 	return v;
-}
-
-// producer placement policy of k_fwdq_pc (see fq_producer_wave)
-int fq_role_policy()
-{
-	static const int v = [] { const char* e = getenv("RIC_FQ_ROLE"); return e ? atoi(e) & 3 : 1; }();
-	return v;
-}
-
-// per-device CU arrival counters (policy 2): monotonic, never reset (k & 3
-// only needs the increments)
-uint32_t* fq_cu_counters()
-{
-	static std::mutex mu;
-	static uint32_t* ctr[64] = {};
-	int dev = 0;
-	if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-	std::lock_guard<std::mutex> g(mu);
-	uint32_t*& c = ctr[dev & 63];
-	if (!c) {
-		if (hipMalloc(&c, 2048 * sizeof(uint32_t)) != hipSuccess) { c = nullptr; return nullptr; }
-		if (hipMemset(c, 0, 2048 * sizeof(uint32_t)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
-			(void)hipFree(c);
-			c = nullptr;
-		}
-	}
-	return c;
 }
 
 template <int S>
@@ -1343,10 +1300,7 @@ void fq_launch_pc(FqArgs& a, hipStream_t st)
 	const int nstrip = (a.W + kFqStrip - 1) / kFqStrip;
 	static const int onewg = [] { const char* e = getenv("RIC_FQ_ONEWG"); return e ? atoi(e) : 0; }();
 	// RIC_FQ_ONEWG=1: one interior workgroup only (latency of one segment; results invalid)
-	int policy = fq_role_policy();
-	a.cu_ctr = nullptr;
-	if (policy == 2 && !(a.cu_ctr = fq_cu_counters())) policy = 1;
-	int dbg = fq_pc() | (policy << 8);
+	int dbg = fq_pc();
 	a.wgt = nullptr;
 	if ((dbg & 128) && a.high && !(a.wgt = fq_wgtrace())) dbg &= ~128;
 	if (onewg) hipLaunchKernelGGL(k_fwdq_pc, dim3(1, 1), dim3(256), 0, st, a, S, dbg | 4);
@@ -1484,7 +1438,17 @@ struct InvArgs {
 	TO* out; long po;           // reconstructed plane (finer level type / image)
 	int W, H, nseg, ovec, nofast;
 	int quirk_dalign, quirk_halign;   // reference DimXAlign of D and H (5/3 only)
+	int q[4];                   // fused TSUQi multipliers of D, H, V, LL (1 = none)
 };
+
+// CBand::TSUQi (src/lib/band.h:94-107) on a loaded band value: v *= (C)q
+template <bool SH>
+__device__ __forceinline__ int deq(int v, int q) { return tr<SH>((int)((uint32_t)v * (uint32_t)q)); }
+// the same on two packed shorts (the low 16 bits of the product)
+__device__ __forceinline__ uint32_t deq2(uint32_t w, int q)
+{
+	return as_w(as_v2u(w) * splat2((uint32_t)q));
+}
 
 template <int TRANS, typename TB, typename TL, typename TO, int S, bool FAST>
 __device__ __forceinline__ void inv_seg(const InvArgs<TB, TL, TO>& a, int x, int lane, int y0)
@@ -1525,10 +1489,13 @@ __device__ __forceinline__ void inv_seg(const InvArgs<TB, TL, TO>& a, int x, int
 			hi = load_band2<TL, EDGE>(a.ll + (long)by * a.pl, bx, dxH);
 		}
 	};
-	auto unpack_row = [&](const R2& lo, const R2& hi, int (&r)[4]) {
+	// odd: the row's bands are V + LL, else D + H (fused TSUQi multipliers)
+	auto unpack_row = [&](const R2& lo, const R2& hi, int (&r)[4], bool odd) {
 		unpack2<TB>(lo, r[0], r[2]);
 		unpack2<TB>(hi, r[1], r[3]);
-		FOR4 r[j] = tr<SH>(r[j]);
+		const int ql = odd ? a.q[BV] : a.q[BD], qh = odd ? a.q[BL] : a.q[BH];
+		r[0] = deq<SH>(r[0], ql); r[2] = deq<SH>(r[2], ql);
+		r[1] = deq<SH>(r[1], qh); r[3] = deq<SH>(r[3], qh);
 	};
 	auto emit = [&](int y, const int (&rw)[4]) {
 		if (!FAST && (y < y0 || y >= y0 + S || y >= H)) return;
@@ -1556,7 +1523,7 @@ __device__ __forceinline__ void inv_seg(const InvArgs<TB, TL, TO>& a, int x, int
 			R2 l0, h0, l1, h1;
 			int r0[4], r1[4];
 			load_pair(e, l0, h0); load_pair(e + 1, l1, h1);
-			unpack_row(l0, h0, r0); unpack_row(l1, h1, r1);
+			unpack_row(l0, h0, r0, false); unpack_row(l1, h1, r1, true);
 			FOR4 { r1[j] = tr<SH>(r1[j] - (r0[j] >> 1)); r0[j] = tr<SH>(r0[j] + r1[j]); }
 			emit(e, r0); emit(e + 1, r1);
 		}
@@ -1585,8 +1552,8 @@ __device__ __forceinline__ void inv_seg(const InvArgs<TB, TL, TO>& a, int x, int
 		for (int i = 0; i < R; i += 2) {
 			const int e = y0 - 4 + i;
 			if (!FAST && (e < 0 || e >= H)) continue;
-			unpack_row(rlo[i], rhi[i], w5);
-			if (FAST || e + 1 < H) unpack_row(rlo[i + 1], rhi[i + 1], w6);
+			unpack_row(rlo[i], rhi[i], w5, false);
+			if (FAST || e + 1 < H) unpack_row(rlo[i + 1], rhi[i + 1], w6, true);
 			if constexpr (TRANS == CDF97) {
 				// U2^-1 at e-1, P2^-1 at e-2, U1^-1 at e-3, P1^-1 at e-4
 				// (src/lib/wavelet2d.cpp:512-561)
@@ -1675,48 +1642,81 @@ __device__ __forceinline__ void inv97p_seg(const InvArgs<int16_t, int16_t, int16
 	// odd ones) stream through a ring of PF row pairs, as in fwd97p_seg
 	constexpr int NP = (S + 8) / 2, PF = 4;
 	static_assert(NP % PF == 0, "segment rows");
-	uint4 ring[PF];                               // (D, H, V, LL) words of one pair
-	const long by0 = (y0 - 4) >> 1;
-	const int16_t* pD = a.d[BD] + by0 * a.p[BD];
-	const int16_t* pH = a.d[BH] + by0 * a.p[BH];
-	const int16_t* pV = a.d[BV] + by0 * a.p[BV];
-	const int16_t* pL = a.ll + by0 * a.pl;
+	// Ring slots: FAST, the (D, H, V, LL) words of one pair; border waves,
+	// the raw elements at clamped band columns, masked when consumed.  Every
+	// refill is unconditional, from a wave-uniform clamped band row (the
+	// refills past the segment re-read valid rows): a load under a branch,
+	// or a select right after it, is waited for at once -- one memory round
+	// trip per row pair.  Rows outside the image are never consumed.
+	struct ERaw { int d0, d1, h0, h1, v0, v1, l0, l1; };
+	using Slot = typename std::conditional<FAST, uint4, ERaw>::type;
+	// FAST: two rings, alternate iterations (prefetch depth two iterations);
+	// a pass of the loop runs two iterations, so the ring registers are the
+	// same at the back-edge and no copy waits for a load in flight
+	constexpr int DEPTH = FAST ? 2 : 1;
+	Slot ring[DEPTH][PF];
 	int yl = y0 - 4;
-	auto load_next = [&](uint4& dst) {
-		if (FAST) {
-			dst.x = load_band2<int16_t, false>(pD, bx, dxD);
-			dst.y = load_band2<int16_t, false>(pH, bx, dxH);
-			dst.z = load_band2<int16_t, false>(pV, bx, dxD);
-			dst.w = load_band2<int16_t, false>(pL, bx, dxH);
+	const int byl = FAST ? min((y0 + S + 3) >> 1, (H >> 1) - 1) : 0;
+	const int hiD = max(dxD - 1, 0), hiH = max(dxH - 1, 0);
+	const int beMax = max(((H + 1) >> 1) - 1, 0), boMax = max((H >> 1) - 1, 0);
+	auto load_next = [&](Slot& dst) {
+		if constexpr (FAST) {
+			const long by = min(yl >> 1, byl);
+			dst.x = load_band2<int16_t, false>(a.d[BD] + by * a.p[BD], bx, dxD);
+			dst.y = load_band2<int16_t, false>(a.d[BH] + by * a.p[BH], bx, dxH);
+			dst.z = load_band2<int16_t, false>(a.d[BV] + by * a.p[BV], bx, dxD);
+			dst.w = load_band2<int16_t, false>(a.ll + by * a.pl, bx, dxH);
 		} else {
-			// band rows outside the bands read as 0: clamped row, then a select
 			const int by = yl >> 1;
-			const int be = min(max(by, 0), max(((H + 1) >> 1) - 1, 0)), bo = min(max(by, 0), max((H >> 1) - 1, 0));
-			const uint32_t xd = load_band2<int16_t, true>(a.d[BD] + (long)be * a.p[BD], bx, dxD);
-			const uint32_t xh = load_band2<int16_t, true>(a.d[BH] + (long)be * a.p[BH], bx, dxH);
-			const uint32_t xv = load_band2<int16_t, true>(a.d[BV] + (long)bo * a.p[BV], bx, dxD);
-			const uint32_t xl = load_band2<int16_t, true>(a.ll + (long)bo * a.pl, bx, dxH);
-			const bool ie = yl >= 0 && yl < H, io = yl + 1 >= 0 && yl + 1 < H;
-			dst.x = ie ? xd : 0u; dst.y = ie ? xh : 0u;
-			dst.z = io ? xv : 0u; dst.w = io ? xl : 0u;
+			const long be = min(max(by, 0), beMax), bo = min(max(by, 0), boMax);
+			const int16_t* rD = a.d[BD] + be * a.p[BD];
+			const int16_t* rH = a.d[BH] + be * a.p[BH];
+			const int16_t* rV = a.d[BV] + bo * a.p[BV];
+			const int16_t* rL = a.ll + bo * a.pl;
+			const int cD0 = min(max(bx, 0), hiD), cD1 = min(max(bx + 1, 0), hiD);
+			const int cH0 = min(max(bx, 0), hiH), cH1 = min(max(bx + 1, 0), hiH);
+			dst.d0 = rD[cD0]; dst.d1 = rD[cD1];
+			dst.h0 = rH[cH0]; dst.h1 = rH[cH1];
+			dst.v0 = rV[cD0]; dst.v1 = rV[cD1];
+			dst.l0 = rL[cH0]; dst.l1 = rL[cH1];
 		}
-		pD += a.p[BD]; pH += a.p[BH]; pV += a.p[BV]; pL += a.pl; yl += 2;
+		yl += 2;
+	};
+	// border waves: band columns outside the bands read as 0
+	const bool inD0 = bx >= 0 && bx < dxD, inD1 = bx + 1 >= 0 && bx + 1 < dxD;
+	const bool inH0 = bx >= 0 && bx < dxH, inH1 = bx + 1 >= 0 && bx + 1 < dxH;
+	auto words = [&](const Slot& r) -> uint4 {
+		if constexpr (FAST) {
+			return make_uint4(deq2(r.x, a.q[BD]), deq2(r.y, a.q[BH]), deq2(r.z, a.q[BV]), deq2(r.w, a.q[BL]));
+		} else {
+			auto pk = [](bool i0, int a0, bool i1, int a1) {
+				return (uint32_t)(uint16_t)(i0 ? a0 : 0) | ((uint32_t)(uint16_t)(i1 ? a1 : 0) << 16);
+			};
+			return make_uint4(deq2(pk(inD0, r.d0, inD1, r.d1), a.q[BD]), deq2(pk(inH0, r.h0, inH1, r.h1), a.q[BH]),
+			                  deq2(pk(inD0, r.v0, inD1, r.v1), a.q[BV]), deq2(pk(inH0, r.l0, inH1, r.l1), a.q[BL]));
+		}
 	};
 #pragma unroll
-	for (int j = 0; j < PF; j++) load_next(ring[j]);
+	for (int d = 0; d < DEPTH; d++) {
+#pragma unroll
+		for (int j = 0; j < PF; j++) load_next(ring[d][j]);
+	}
 	const v2s z = {0, 0};
 	PRow w0 = {z, z}, w1 = {z, z}, w2 = {z, z}, w3 = {z, z}, w4 = {z, z}, w5 = {z, z}, w6 = {z, z};
-#pragma unroll 1
-	for (int it = 0; it < NP / PF; it++) {
-#pragma unroll
-	for (int k = 0; k < PF; k++) {
+	auto pair = [&](int it, int k, Slot& rs) {
 		const int i = 2 * (it * PF + k);
 		const int e = y0 - 4 + i;
-		const uint4 rr = ring[k];
-		if (!FAST && (e < 0 || e >= H)) { if (it + 1 < NP / PF) load_next(ring[k]); continue; }
+		// take the slot into fresh registers first (FAST: an opaque copy), so
+		// the refill can land in the slot's own registers and the loop-carried
+		// ring needs no copy at the back-edge (a copy waits for its load)
+		Slot slot;
+		if constexpr (FAST) slot = opaque_copy(rs);
+		else slot = rs;
+		load_next(rs);
+		if (!FAST && (e < 0 || e >= H)) return;
+		const uint4 rr = words(slot);
 		w5.e = as_v2(rr.x); w5.o = as_v2(rr.y);
 		if (FAST || e + 1 < H) { w6.e = as_v2(rr.z); w6.o = as_v2(rr.w); }
-		if (it + 1 < NP / PF) load_next(ring[k]);
 		// U2^-1 at e-1, P2^-1 at e-2, U1^-1 at e-3, P1^-1 at e-4 (src/lib/wavelet2d.cpp:512-561)
 		if (FAST || e >= 2) {
 			v2s te = w3.e + w5.e, to = w3.o + w5.o;
@@ -1737,7 +1737,23 @@ __device__ __forceinline__ void inv97p_seg(const InvArgs<int16_t, int16_t, int16
 		if (FAST) { if (i >= 8) emit_pair(w1, w2); }
 		else { emit(e - 4, w1); emit(e - 3, w2); }
 		w0 = w2; w1 = w3; w2 = w4; w3 = w5; w4 = w6;
-	}
+	};
+	auto iteration = [&](int it, Slot (&rg)[PF]) {
+#pragma unroll
+		for (int k = 0; k < PF; k++) pair(it, k, rg[k]);
+	};
+	constexpr int NIT = NP / PF;
+	if constexpr (DEPTH == 2) {
+		int it = 0;
+#pragma unroll 1
+		for (; it + 1 < NIT; it += 2) {
+			iteration(it, ring[0]);
+			iteration(it + 1, ring[1]);
+		}
+		if (it < NIT) iteration(it, ring[0]);
+	} else {
+#pragma unroll 1
+		for (int it = 0; it < NIT; it++) iteration(it, ring[0]);
 	}
 	if (!FAST && y0 + S + 4 >= H) {
 		if (!(H & 1)) {                              // src/lib/wavelet2d.cpp:572-587
@@ -1827,9 +1843,10 @@ void fwd_launch(const Level& L, const void* src, long sp, char* arena, int vec, 
 }
 
 template <int TRANS, typename TB, typename TO, int S>
-void inv_launch_s(const Level& L, const Band& lls, char* arena, void* out, long po, hipStream_t st)
+void inv_launch_s(const Level& L, const Band& lls, char* arena, void* out, long po, const int* q, hipStream_t st)
 {
 	InvArgs<TB, TB, TO> a;
+	for (int b = 0; b < 4; b++) a.q[b] = q ? q[b] : 1;
 	a.ovec = (po % 4 == 0) && ((uintptr_t)out % 16 == 0);
 	a.nofast = dbg_nofast();
 	for (int b = 0; b < 3; b++) { a.d[b] = (const TB*)(arena + L.b[b].off); a.p[b] = L.b[b].pitch; }
@@ -1843,15 +1860,15 @@ void inv_launch_s(const Level& L, const Band& lls, char* arena, void* out, long 
 }
 
 template <int TRANS, typename TB, typename TO>
-void inv_launch(const Level& L, const Band& lls, char* arena, void* out, long po, hipStream_t st)
+void inv_launch(const Level& L, const Band& lls, char* arena, void* out, long po, const int* q, hipStream_t st)
 {
 	const int S = seg_rows<TB>(L.h);
 	if constexpr (sizeof(TB) == 2) {
-		if (S == 64) { inv_launch_s<TRANS, TB, TO, 64>(L, lls, arena, out, po, st); return; }
-		if (S == 32) { inv_launch_s<TRANS, TB, TO, 32>(L, lls, arena, out, po, st); return; }
+		if (S == 64) { inv_launch_s<TRANS, TB, TO, 64>(L, lls, arena, out, po, q, st); return; }
+		if (S == 32) { inv_launch_s<TRANS, TB, TO, 32>(L, lls, arena, out, po, q, st); return; }
 	}
-	if (S == 16) inv_launch_s<TRANS, TB, TO, 16>(L, lls, arena, out, po, st);
-	else inv_launch_s<TRANS, TB, TO, 8>(L, lls, arena, out, po, st);
+	if (S == 16) inv_launch_s<TRANS, TB, TO, 16>(L, lls, arena, out, po, q, st);
+	else inv_launch_s<TRANS, TB, TO, 8>(L, lls, arena, out, po, q, st);
 }
 
 template <int TRANS>
@@ -1863,11 +1880,11 @@ void fwd_dispatch(const Level& L, const void* src, long sp, char* arena, int vec
 }
 
 template <int TRANS>
-void inv_dispatch(const Level& L, const Band& lls, char* arena, void* out, long po, int out_is_int, hipStream_t st)
+void inv_dispatch(const Level& L, const Band& lls, char* arena, void* out, long po, int out_is_int, const int* q, hipStream_t st)
 {
-	if (!L.is_int) inv_launch<TRANS, int16_t, int16_t>(L, lls, arena, out, po, st);
-	else if (out_is_int) inv_launch<TRANS, int32_t, int32_t>(L, lls, arena, out, po, st);
-	else inv_launch<TRANS, int32_t, int16_t>(L, lls, arena, out, po, st);
+	if (!L.is_int) inv_launch<TRANS, int16_t, int16_t>(L, lls, arena, out, po, q, st);
+	else if (out_is_int) inv_launch<TRANS, int32_t, int32_t>(L, lls, arena, out, po, q, st);
+	else inv_launch<TRANS, int32_t, int16_t>(L, lls, arena, out, po, q, st);
 }
 
 }  // namespace
@@ -1895,7 +1912,6 @@ void launch_fwdq_level(const Pyramid& P, int l, const void* src, long sp, int ve
 {
 	const Level& L = P.L[l];
 	FqArgs a;
-	a.cu_ctr = nullptr;
 	a.wgt = nullptr;
 	a.src = (const int16_t*)src; a.sp = sp; a.W = L.w; a.H = L.h;
 	a.vec8 = vec8; a.vec16 = vec16; a.nofast = dbg_nofast(); a.high = l == 0;
@@ -1928,7 +1944,6 @@ void launch_fwdq_gen_level(const Pyramid& P, int l, const void* src, long sp, in
 {
 	const Level& L = P.L[l];
 	FqArgs a;
-	a.cu_ctr = nullptr;
 	a.wgt = nullptr;
 	a.src = (const int16_t*)src; a.sp = sp; a.W = L.w; a.H = L.h;
 	a.vec8 = vec8; a.vec16 = 0; a.nofast = 1; a.high = l == 0;
@@ -1959,11 +1974,11 @@ void launch_fwdq_gen_level(const Pyramid& P, int l, const void* src, long sp, in
 }
 
 void launch_inv_level(const Level& L, const Band& lls, char* arena, void* out, long po, int out_is_int,
-                      int trans, hipStream_t st)
+                      int trans, hipStream_t st, const int* q)
 {
-	if (trans == CDF97) inv_dispatch<CDF97>(L, lls, arena, out, po, out_is_int, st);
-	else if (trans == CDF53) inv_dispatch<CDF53>(L, lls, arena, out, po, out_is_int, st);
-	else inv_dispatch<HAAR>(L, lls, arena, out, po, out_is_int, st);
+	if (trans == CDF97) inv_dispatch<CDF97>(L, lls, arena, out, po, out_is_int, q, st);
+	else if (trans == CDF53) inv_dispatch<CDF53>(L, lls, arena, out, po, out_is_int, q, st);
+	else inv_dispatch<HAAR>(L, lls, arena, out, po, out_is_int, q, st);
 }
 
 }  // namespace ric

@@ -27,9 +27,10 @@ void launch_fwdq_level(const Pyramid& P, int l, const void* src, long sp, int ve
 void launch_fwdq_gen_level(const Pyramid& P, int l, const void* src, long sp, int vec8, const QuantParams& qp,
                            int ll_on, int ll_iQ, int ll_T0, char* arena, hipStream_t st);
 // Inverse level: D/H/V bands + lls (the level's LL) -> out (pitch po elements),
-// typed int32 if out_is_int else int16.
+// typed int32 if out_is_int else int16.  q (optional): TSUQi multipliers of
+// D, H, V, LL applied to the loaded band values (fused dequantiser).
 void launch_inv_level(const Level& L, const Band& lls, char* arena, void* out, long po,
-                      int out_is_int, int trans, hipStream_t st);
+                      int out_is_int, int trans, hipStream_t st, const int* q = nullptr);
 
 // Per-band quantiser parameters computed on the host (float32 exactly as the
 // reference: src/lib/bandcodec.cpp:243-247, 149-157).

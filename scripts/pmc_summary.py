@@ -35,7 +35,8 @@ def grid(r):
 
 
 def fwd_l0(rs):
-    fw = [r for r in rs if "k_fwd" in r["Kernel_Name"]]
+    """The level-0 launches of the fused forward level kernel (largest grid)."""
+    fw = [r for r in rs if "k_fwdq_pc" in r["Kernel_Name"]]
     if not fw:
         return []
     g = max(grid(r) for r in fw)
@@ -55,6 +56,7 @@ def counter(tag, name):
 
 def main():
     tag = sys.argv[1]
+    # TAG_kt (kernel trace), TAG_pmc_fetch / TAG_pmc_write (counter passes)
     rnd = sys.argv[2] if len(sys.argv) > 2 else "r01"
     kt = os.path.join(REPO, "gpurun_out", tag + "_kt")
     os.makedirs(os.path.join(REPO, "profiles"), exist_ok=True)
@@ -86,7 +88,7 @@ def main():
         fetch_b = fe[0] * 1024.0
         write_b = wr[0] * 1024.0
         out.update({
-            "kernel": "k_fwd level 0 (largest-grid k_fwd launch)",
+            "kernel": "k_fwdq_pc level 0 (largest-grid launch of the fused forward DWT + quantiser)",
             "fetch_size_kib_raw": round(fe[0], 1), "write_size_kib_raw": round(wr[0], 1),
             "launches": [fe[1], wr[1]],
             "read_bytes_corrected": 2 * fetch_b, "write_bytes": write_b,
