@@ -277,6 +277,37 @@ struct GeoM {                                                   // CGeomCodec
 	}
 };
 
+// One CGeomCodec context held in registers for the run of coefficients of a
+// block (all of a block's magnitudes share one context): the model state is
+// not re-read from memory after every coefficient store (a band store may
+// alias the uint16_t model words for the compiler).
+struct GeoReg {
+	uint32_t freq, idx;
+	RIC_AI void load(const GeoM& g, int c) { freq = g.freq[c]; idx = g.idx[c]; }
+	RIC_AI void store(GeoM& g, int c) const { g.freq[c] = (uint16_t)freq; g.idx[c] = (uint8_t)idx; }
+	RIC_AI int decode_signed(DecCore& d)                         // GeoM::decode_signed
+	{
+		const uint32_t k = kGeoKD[idx], f = freq;
+		const int s = kGeoShiftD[idx];
+		uint32_t fr = freq, l = 0;
+		while (d.get_bit(f)) {
+			fr -= fr >> (3 + s);
+			if (++l > (1u << 20)) break;            // corrupt-stream guard
+		}
+		const uint32_t v = d.bits(k + 1);
+		const uint32_t sym = (l << k) | (v >> 1);
+		fr = (uint16_t)(fr + ((4096 - fr) >> (3 + s)));             // adapt
+		if ((uint16_t)(fr - kGeoThresD[s - 1]) > kGeoThresD[s] - kGeoThresD[s - 1]) {
+			if (fr < kGeoThresD[s - 1]) { if (idx < 24) idx++; }
+			else if (idx > 0) idx--;
+			if (idx >= 9) fr = 2048;
+		}
+		freq = fr;
+		const int mag = (int)sym + 1;
+		return (v & 1) ? -mag : mag;
+	}
+};
+
 template <typename P>
 RIC_AI int max_len2_dec(const P* p, long st)                    // maxLen<2, decode>
 {
@@ -301,12 +332,15 @@ RIC_AI int block_full_dec(DecCore& d, GeoM& g, C* blk, long st, int idx)
 	if (HIGH || k != 0) {
 		uint32_t sig = k != 16 ? d.enum16(k) : 0xFFFFu;
 		const int gc = (int)k - 1;
+		GeoReg r;
+		r.load(g, gc);
 		while (sig) {
 			const int b = 31 - __builtin_clz(sig);      // bit 15 = raster position 0
 			sig &= ~(1u << b);
 			const int i = 15 - b;
-			blk[(i >> 2) * st + (i & 3)] = (C)tr<SH>(g.decode_signed(d, gc));
+			blk[(i >> 2) * st + (i & 3)] = (C)tr<SH>(r.decode_signed(d));
 		}
+		r.store(g, gc);
 	}
 	return (int)k - (HIGH ? 1 : 0);
 }

@@ -754,8 +754,6 @@ __global__ void __launch_bounds__(256) k_fwd(FwdArgs<TI, TO> a)
 // fence orders it).
 constexpr int kFqStrip = (kLanes - 2) * 8;   // 496 output columns per wave
 
-__constant__ SymTables kSymDevF __attribute__((aligned(16))) = RIC_SYM_TABLES_INIT;
-__constant__ EnumSplit kEnumDevF __attribute__((aligned(16))) = make_enum_split();
 
 // format tables staged in LDS once per workgroup
 struct FqTables {
@@ -1114,22 +1112,49 @@ __device__ __forceinline__ void fq_seg(const FqArgs& a, const int (*thr)[16], co
 
 // A packed level covers whole 496 x S tiles: one wave per (strip, segment),
 // the waves on the image border (fq_seg<S, true>) included.
+// One __constant__ image of the format tables, copied as 16-byte words.
+__constant__ FqTables kFqDev __attribute__((aligned(16))) = {RIC_SYM_TABLES_INIT, make_enum_split()};
+
+// Stages the thresholds and format tables in LDS.  NT = the block size: the
+// copy is unrolled so that every thread issues all of its global loads before
+// its first LDS store -- one memory round trip for the whole staging (a
+// strided loop of load-store pairs pays one per iteration).
+template <int NT>
 __device__ __forceinline__ void fq_stage_tables(const FqArgs& a, int (*s_thres)[16], FqTables& s_F, uint32_t (*s_tpk)[17 * 8])
 {
-	if (threadIdx.x < 48) s_thres[threadIdx.x / 16][threadIdx.x % 16] = a.thres[threadIdx.x / 16][threadIdx.x % 16];
-	for (int i = threadIdx.x; i < 3 * 17 * 8; i += blockDim.x) {
-		const int b = i / (17 * 8), c = (i >> 3) % 17, p = i & 7;
-		const uint32_t lo = c + p < 16 ? (uint32_t)a.thres[b][c + p] & 0xFFFFu : 0xFFFFu;
-		const uint32_t hi = c + p + 8 < 16 ? (uint32_t)a.thres[b][c + p + 8] & 0xFFFFu : 0xFFFFu;
-		s_tpk[b][i % (17 * 8)] = lo | (hi << 16);
+	static_assert(sizeof(FqTables) % 16 == 0, "table words");
+	constexpr int NW = (int)(sizeof(FqTables) / 16);
+	constexpr int PER = (NW + NT - 1) / NT;
+	constexpr int NTP = 3 * 17 * 8;
+	constexpr int PT = (NTP + NT - 1) / NT;
+	const uint4* src = reinterpret_cast<const uint4*>(&kFqDev);
+	uint4 v[PER];
+#pragma unroll
+	for (int k = 0; k < PER; k++) {
+		const int i = threadIdx.x + k * NT;
+		v[k] = src[i < NW ? i : NW - 1];
 	}
-	static_assert(sizeof(SymTables) % 4 == 0 && sizeof(EnumSplit) % 4 == 0, "table words");
-	const uint32_t* sw = reinterpret_cast<const uint32_t*>(&kSymDevF);
-	uint32_t* dw = reinterpret_cast<uint32_t*>(&s_F.T);
-	for (int i = threadIdx.x; i < (int)(sizeof(SymTables) / 4); i += blockDim.x) dw[i] = sw[i];
-	sw = reinterpret_cast<const uint32_t*>(&kEnumDevF);
-	dw = reinterpret_cast<uint32_t*>(&s_F.E);
-	for (int i = threadIdx.x; i < (int)(sizeof(EnumSplit) / 4); i += blockDim.x) dw[i] = sw[i];
+	int th = threadIdx.x < 48 ? a.thres[threadIdx.x / 16][threadIdx.x % 16] : 0;
+	uint32_t lo[PT], hi[PT];
+#pragma unroll
+	for (int k = 0; k < PT; k++) {
+		const int i = threadIdx.x + k * NT;
+		const int b = min(i / (17 * 8), 2), c = (i >> 3) % 17, q = i & 7;
+		lo[k] = c + q < 16 ? (uint32_t)a.thres[b][min(c + q, 15)] & 0xFFFFu : 0xFFFFu;
+		hi[k] = c + q + 8 < 16 ? (uint32_t)a.thres[b][min(c + q + 8, 15)] & 0xFFFFu : 0xFFFFu;
+	}
+	uint4* dst = reinterpret_cast<uint4*>(&s_F);
+#pragma unroll
+	for (int k = 0; k < PER; k++) {
+		const int i = threadIdx.x + k * NT;
+		if (i < NW) dst[i] = v[k];
+	}
+	if (threadIdx.x < 48) s_thres[threadIdx.x / 16][threadIdx.x % 16] = th;
+#pragma unroll
+	for (int k = 0; k < PT; k++) {
+		const int i = threadIdx.x + k * NT;
+		if (i < NTP) s_tpk[i / (17 * 8)][i % (17 * 8)] = lo[k] | (hi[k] << 16);
+	}
 }
 
 // grid (ceil(W / 496), ceil(nseg / 4)), one wave per segment
@@ -1139,7 +1164,7 @@ __global__ void __launch_bounds__(256, 3) k_fwdq_fast(FqArgs a)
 	__shared__ int s_thres[3][16];
 	__shared__ FqTables s_F __attribute__((aligned(16)));
 	__shared__ uint32_t s_tpk[3][17 * 8];
-	fq_stage_tables(a, s_thres, s_F, s_tpk);
+	fq_stage_tables<256>(a, s_thres, s_F, s_tpk);
 	__syncthreads();
 	const int lane = threadIdx.x & 63;
 	const int seg = blockIdx.y * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1207,7 +1232,7 @@ __global__ void __launch_bounds__(256, 4) k_fwdq_pc(FqArgs a, int S, int dbg)
 	if ((dbg & 32) && edge) return;   // timing experiment: interior workgroups only (results invalid)
 	const int nit = m.bottom ? (a.H - y0) / 8 + 1 : S / 8 + 1;
 	auto stage = [&]() {
-		fq_stage_tables(a, s_thres, s_F, s_tpk);
+		fq_stage_tables<256>(a, s_thres, s_F, s_tpk);
 		__syncthreads();
 	};
 	if (wave == 0) {
@@ -1240,6 +1265,173 @@ __global__ void __launch_bounds__(256, 4) k_fwdq_pc(FqArgs a, int S, int dbg)
 		wgt[2 + w] = __builtin_amdgcn_s_memrealtime();
 		if (wave == 0) wgt[6] = ((uint64_t)__builtin_amdgcn_s_getreg(kHwRegHwId) << 32) |
 		                        (uint32_t)__builtin_amdgcn_s_memtime();
+		if (w == 0) wgt[7] = (uint64_t)wgi | ((uint64_t)__builtin_amdgcn_s_getreg(kHwRegXcc) << 32);
+	}
+}
+
+// ------------------------------------ two-producer fused level (k_fwdq_pc2)
+// The producer of k_fwdq_pc is the segment's critical path: one wave lifts
+// 8 columns per lane, and a wave alone on its SIMD issues one VALU op per
+// 4 cycles, so an 8-row iteration costs it ~2.5 us even on an idle chip.
+// Here two producer waves split the 496-column strip into 248-column halves
+// (4 columns per lane, the packed lifting of fwd97p_seg, one halo lane per
+// side) and run on two SIMDs at once; the three consumer waves are those of
+// k_fwdq_pc.  Producer half h, lane l (1..62) holds band columns
+// h*124 + 2(l-1) + {0, 1} of the strip: word (l-1) & 1 of consumer block
+// h*31 + (l-1)/2 + 1 in the LDS hand-off buffer.
+template <bool EDGE, typename Stage>
+__device__ __forceinline__ void fq2_producer(const FqArgs& a, int x, int lane, int h, int y0, const FqBorder& mb,
+                                             int S, uint2 (*pcbuf)[3][4][kLanes], int dbg, uint64_t* tr,
+                                             const Stage& stage)
+{
+	const bool out_lane = lane >= 1 && lane <= kLanes - 2 && (!EDGE || x < a.W);
+	const EdgeMasks em = edge_masks(x, a.W);
+	const bool ld = !EDGE || (x >= 0 && x < a.W);
+	int16_t* pL = a.d[BL] + (long)(y0 >> 1) * a.p[BL] + (x >> 1);
+	const int L = h * (kLanes / 2 - 1) + ((lane - 1) >> 1) + 1, word = (lane - 1) & 1;
+	constexpr int PF = 4, DEPTH = 2;
+	const int nit = (EDGE && mb.bottom) ? (a.H - y0) / 8 + 1 : S / 8 + 1;
+	const int kend = (EDGE && mb.bottom) ? 2 : PF;
+	uint2 ring[DEPTH][2 * PF];
+	int yl = y0 - 4;
+	// unconditional loads from a wave-uniform clamped row (see fq_seg)
+	const int ylast = min(y0 + S + 3, a.H - 1);
+	const int xcl = EDGE ? min(max(x, 0), a.W - 4) : x;
+	auto load_next = [&](uint2& dst) {
+		const int yc = min(max(yl, 0), ylast);
+		dst = *reinterpret_cast<const uint2*>(a.src + (long)yc * a.sp + xcl);
+		yl++;
+	};
+#pragma unroll
+	for (int d = 0; d < DEPTH; d++) {
+#pragma unroll
+		for (int j = 0; j < 2 * PF; j++) load_next(ring[d][j]);
+	}
+	stage();
+	const v2s z = {0, 0};
+	PRow w0 = {z, z}, w1 = {z, z}, w2 = {z, z}, w3 = {z, z}, w4, w5;
+	int cur = 0;
+	auto emit = [&](int k) {                    // rows e-4 (D, H) and e-3 (V, L) are final
+		if (out_lane && !(dbg & 16)) {
+			reinterpret_cast<uint32_t*>(&pcbuf[cur][BD][k][L])[word] = as_u32(w0.e);
+			reinterpret_cast<uint32_t*>(&pcbuf[cur][BH][k][L])[word] = as_u32(w0.o);
+			reinterpret_cast<uint32_t*>(&pcbuf[cur][BV][k][L])[word] = as_u32(w1.e);
+			*reinterpret_cast<uint32_t*>(pL) = as_u32(w1.o);
+		}
+		pL += a.p[BL];
+	};
+	auto iteration = [&](int it, uint2 (&rg)[2 * PF]) {
+		const bool last = it + 1 == nit;
+		cur = it & 1;
+#pragma unroll
+		for (int k = 0; k < PF; k++) {
+			if (EDGE && last && k >= kend) break;
+			const int e = y0 - 4 + 2 * (it * PF + k);   // the pair's even row
+			uint2 u0 = rg[2 * k], u1 = rg[2 * k + 1];
+			if (EDGE && !ld) { u0 = make_uint2(0, 0); u1 = u0; }
+			w4 = prow_from_u2(u0);
+			w5 = prow_from_u2(u1);
+			load_next(rg[2 * k]);
+			load_next(rg[2 * k + 1]);
+			if (EDGE && e < 0) continue;                 // above the image (top segment)
+			row_fwd97p2<EDGE>(w4, w5, em);
+			// P1 at e, U1 at e-1, P2 at e-2, U2 at e-3 (src/lib/wavelet2d.cpp:425-454)
+			if (EDGE && e == 0) {
+				w4.e -= mul3(w5.e); w4.o -= mul3(w5.o);
+			} else {
+				v2s te = w3.e + w5.e, to = w3.o + w5.o;
+				w4.e -= te + (te >> 1); w4.o -= to + (to >> 1);
+			}
+			if (!EDGE || e >= 1) { w3.e -= avg16(w2.e, w4.e); w3.o -= avg16(w2.o, w4.o); }
+			if (EDGE && e == 2) {
+				v2s me = mult08p(w3.e), mo = mult08p(w3.o);
+				w2.e += me + me; w2.o += mo + mo;
+			} else if (!EDGE || e >= 4) {
+				w2.e += mult08p(w1.e + w3.e); w2.o += mult08p(w1.o + w3.o);
+			}
+			if (!EDGE || e >= 4) {
+				v2s te = w0.e + w2.e, to = w0.o + w2.o;
+				w1.e += (te >> 1) - (te >> 5); w1.o += (to >> 1) - (to >> 5);
+			}
+			if (it >= 1) emit(k);
+			w0 = w2; w1 = w3; w2 = w4; w3 = w5;
+		}
+		if (EDGE && last && mb.bottom) {
+			// even H: the window holds rows H-4 .. H-1 (src/lib/wavelet2d.cpp:476-491)
+			w3.e -= w2.e >> 3; w3.o -= w2.o >> 3;
+			w2.e += mult08p(w1.e + w3.e); w2.o += mult08p(w1.o + w3.o);
+			v2s te = w0.e + w2.e, to = w0.o + w2.o;
+			w1.e += (te >> 1) - (te >> 5); w1.o += (to >> 1) - (to >> 5);
+			w3.e += w2.e - (w2.e >> 4); w3.o += w2.o - (w2.o >> 4);
+			emit(2);
+			w0 = w2; w1 = w3;
+			emit(3);
+		}
+		pc_barrier(dbg, tr ? tr + 2 * min(it, kWgIt - 1) : nullptr);   // the consumers take the block row
+	};
+	int it = 0;
+#pragma unroll 1
+	for (; it + 1 < nit; it += 2) {
+		iteration(it, ring[0]);
+		iteration(it + 1, ring[1]);
+	}
+	if (it < nit) iteration(it, ring[0]);
+}
+
+// grid (strips, segments), 5 waves: 0, 1 = producers of the two halves,
+// 2..4 = the D, H, V consumers
+__global__ void __launch_bounds__(320) k_fwdq_pc2(FqArgs a, int S, int dbg)
+{
+	__shared__ int s_thres[3][16];
+	__shared__ FqTables s_F __attribute__((aligned(16)));
+	__shared__ uint32_t s_tpk[3][17 * 8];
+	__shared__ uint2 s_buf[2][3][4][kLanes];
+	const int wgi = blockIdx.y * gridDim.x + blockIdx.x;
+	uint64_t* wgt = ((dbg & 128) && a.wgt && wgi < kWgTraceMax) ? a.wgt + kWgRec * wgi : nullptr;
+	if (wgt && threadIdx.x == 0) {
+		wgt[0] = __builtin_amdgcn_s_memrealtime();
+		wgt[1] = __builtin_amdgcn_s_memtime();
+	}
+	const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+	const int lane = threadIdx.x & 63;
+	const int strip = (dbg & 4) ? ((dbg & 64) ? 0 : 1) : blockIdx.x, seg = (dbg & 4) ? 2 : blockIdx.y;
+	const int y0 = seg * S;
+	const int SX = strip * kFqStrip;                            // first output column of the strip
+	FqBorder mb;
+	mb.top = y0 == 0;
+	mb.bottom = y0 + S >= a.H;
+	const bool edge = SX == 0 || SX - 8 + kLanes * 8 >= a.W || mb.top || mb.bottom;
+	const int nit = mb.bottom ? (a.H - y0) / 8 + 1 : S / 8 + 1;
+	auto stage = [&]() {
+		fq_stage_tables<320>(a, s_thres, s_F, s_tpk);
+		__syncthreads();
+	};
+	if (w < 2) {
+		if (!(dbg & 2048)) __builtin_amdgcn_s_setprio(2);
+		const int x = SX + w * (kStripValid) - kCols + lane * kCols;   // 4 columns per lane
+		uint64_t* tr = (wgt && w == 0) ? wgt + 8 : nullptr;        // trace roles: producer 0, D, H, V
+		if (edge) fq2_producer<true>(a, x, lane, w, y0, mb, S, s_buf, dbg, tr, stage);
+		else fq2_producer<false>(a, x, lane, w, y0, mb, S, s_buf, dbg, tr, stage);
+	} else {
+		stage();
+		const int b = w - 2;
+		const int xc = SX - 8 + lane * 8;                        // the block's 8 image columns
+		const int kx = strip * (kFqStrip / 8) + lane - 1;
+		const bool out_lane = lane >= 1 && lane <= kLanes - 2 && xc < a.W;
+#pragma unroll 1
+		for (int it = 0; it < nit; it++) {
+			pc_barrier(dbg, wgt ? wgt + 8 + (w - 1) * 2 * kWgIt + 2 * min(it, kWgIt - 1) : nullptr);
+			if (it == 0 || (dbg & 3) == 2) continue;     // dbg 2: timing of the lifting alone
+			uint2 buf[4];
+#pragma unroll
+			for (int r = 0; r < 4; r++) buf[r] = s_buf[it & 1][b][r][lane];
+			fq_block_regs(a, s_thres[b], s_tpk[b], s_F, b, buf, kx, (y0 >> 3) + it - 1, out_lane);
+		}
+	}
+	if (wgt && lane == 0) {
+		wgt[2 + (w < 4 ? w : 3)] = __builtin_amdgcn_s_memrealtime();
+		if (w == 0) wgt[6] = ((uint64_t)__builtin_amdgcn_s_getreg(kHwRegHwId) << 32) |
+		                     (uint32_t)__builtin_amdgcn_s_memtime();
 		if (w == 0) wgt[7] = (uint64_t)wgi | ((uint64_t)__builtin_amdgcn_s_getreg(kHwRegXcc) << 32);
 	}
 }
@@ -1303,8 +1495,20 @@ void fq_launch_pc(FqArgs& a, hipStream_t st)
 	int dbg = fq_pc();
 	a.wgt = nullptr;
 	if ((dbg & 128) && a.high && !(a.wgt = fq_wgtrace())) dbg &= ~128;
-	if (onewg) hipLaunchKernelGGL(k_fwdq_pc, dim3(1, 1), dim3(256), 0, st, a, S, dbg | 4);
-	else hipLaunchKernelGGL(k_fwdq_pc, dim3(nstrip, a.nseg), dim3(256), 0, st, a, S, dbg);
+	// the two-producer form on the coarser levels (their segments are short
+	// and latency-bound); level 0 is VALU-throughput-bound, where the
+	// one-producer form's 8-column rows cost fewer instructions.
+	// RIC_FQ_PC2=0/1 forces either form.
+	static const int force2 = [] { const char* e = getenv("RIC_FQ_PC2"); return e ? atoi(e) : -1; }();
+	const bool two = force2 >= 0 ? force2 != 0 : !a.high;
+	if (two) {
+		if (onewg) hipLaunchKernelGGL(k_fwdq_pc2, dim3(1, 1), dim3(320), 0, st, a, S, dbg | 4);
+		else hipLaunchKernelGGL(k_fwdq_pc2, dim3(nstrip, a.nseg), dim3(320), 0, st, a, S, dbg);
+	} else if (onewg) {
+		hipLaunchKernelGGL(k_fwdq_pc, dim3(1, 1), dim3(256), 0, st, a, S, dbg | 4);
+	} else {
+		hipLaunchKernelGGL(k_fwdq_pc, dim3(nstrip, a.nseg), dim3(256), 0, st, a, S, dbg);
+	}
 }
 
 // ------------------------------ generic fused forward level + quantiser
@@ -1381,7 +1585,7 @@ __global__ void __launch_bounds__(256) k_fwdq_gen(FqArgs a, GenLL ll, int nseg)
 	__shared__ int s_thres[3][16];
 	__shared__ FqTables s_F __attribute__((aligned(16)));
 	__shared__ uint32_t s_tpk[3][17 * 8];
-	fq_stage_tables(a, s_thres, s_F, s_tpk);
+	fq_stage_tables<256>(a, s_thres, s_F, s_tpk);
 	__syncthreads();
 	const int lane = threadIdx.x & 63;
 	const int seg = blockIdx.y * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);

@@ -114,6 +114,33 @@ struct GeoE {                                             // CGeomCodec::code
 	}
 };
 
+// One CGeomCodec context in registers for the run of a block's magnitudes
+// (they share one context): no model reload after every band access.
+struct GeoRegE {
+	uint32_t freq, idx;
+	RIC_AI void load(const GeoE& g, int c) { freq = g.freq[c]; idx = g.idx[c]; }
+	RIC_AI void store(GeoE& g, int c) const { g.freq[c] = (uint16_t)freq; g.idx[c] = (uint8_t)idx; }
+	RIC_AI void code_signed(EncCore& e, uint32_t sym, uint32_t sign)   // GeoE::code_signed
+	{
+		const uint32_t k = kGeoKE[idx], f = freq;
+		const int s = kGeoShiftE[idx];
+		uint32_t fr = freq;
+		for (uint32_t l = sym >> k; l > 0; l--) {
+			e.bin(f, 1);
+			fr -= fr >> (3 + s);
+		}
+		e.bin(f, 0);
+		e.bits(((sym & ((1u << k) - 1)) << 1) | sign, k + 1);
+		fr = (uint16_t)(fr + ((4096 - fr) >> (3 + s)));
+		if ((uint16_t)(fr - kGeoThresE[s - 1]) > kGeoThresE[s] - kGeoThresE[s - 1]) {
+			if (fr < kGeoThresE[s - 1]) { if (idx < 24) idx++; }
+			else if (idx > 0) idx--;
+			if (idx >= 9) fr = 2048;
+		}
+		freq = fr;
+	}
+};
+
 template <typename C, bool HIGH, bool PAR>
 void tree_rec_fast(Mux& m, const uint64_t* rec, const uint8_t* pin, const BandView& b)
 {
@@ -163,12 +190,15 @@ void tree_rec_fast(Mux& m, const uint64_t* rec, const uint8_t* pin, const BandVi
 				const uint32_t rl = BlockRec::rawlen(r);
 				e.bits(((uint32_t)(h >> 5) << rl) | BlockRec::raw(r), (h & 31) + rl);
 				const int gc = (int)k - 1;
+				GeoRegE gr;
+				gr.load(g, gc);
 				while (mask) {
 					const int i = __builtin_ctz(mask);
 					mask &= mask - 1;
 					const int v = blk[(i >> 2) * st + (i & 3)];
-					g.code_signed(e, (uc<SH>(v) >> 1) - 1, v & 1, gc);
+					gr.code_signed(e, (uc<SH>(v) >> 1) - 1, v & 1);
 				}
+				gr.store(g, gc);
 				const uint32_t kk = k - (HIGH ? 1 : 0);
 				kmean[ctx] = (uint16_t)(kmean[ctx] + (kk << 7) - (kmean[ctx] >> 3));
 			}

@@ -73,10 +73,146 @@ __global__ void k_rgb_out(const int16_t* __restrict__ in, long pi, int w, int h,
 	if (pix) { pix[i] = (uint8_t)clip255(R); pix[n + i] = (uint8_t)clip255(G); pix[2 * n + i] = (uint8_t)clip255(B); }
 }
 
+// Vector forms: 8 pixels per thread (8-byte pixel loads / stores, 16-byte
+// plane loads / stores), used when every row starts aligned (w % 8 == 0 and
+// aligned buffers, checked on the host).  Same arithmetic as the scalar
+// kernels above.
+__device__ __forceinline__ void unpack8(uint2 u, int (&p)[8])
+{
+#pragma unroll
+	for (int i = 0; i < 4; i++) { p[i] = (u.x >> (8 * i)) & 255; p[4 + i] = (u.y >> (8 * i)) & 255; }
+}
+__device__ __forceinline__ uint4 pack8s(const int16_t (&v)[8])
+{
+	return make_uint4((uint16_t)v[0] | ((uint32_t)(uint16_t)v[1] << 16), (uint16_t)v[2] | ((uint32_t)(uint16_t)v[3] << 16),
+	                  (uint16_t)v[4] | ((uint32_t)(uint16_t)v[5] << 16), (uint16_t)v[6] | ((uint32_t)(uint16_t)v[7] << 16));
+}
+__device__ __forceinline__ void unpack8s(uint4 u, int16_t (&v)[8])
+{
+	const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+	for (int i = 0; i < 4; i++) { v[2 * i] = (int16_t)(w[i] & 0xFFFF); v[2 * i + 1] = (int16_t)(w[i] >> 16); }
+}
+__device__ __forceinline__ uint2 pack8b(const int16_t (&v)[8])
+{
+	uint2 r = {0, 0};
+#pragma unroll
+	for (int i = 0; i < 4; i++) {
+		r.x |= (uint32_t)(uint8_t)clip255(v[i]) << (8 * i);
+		r.y |= (uint32_t)(uint8_t)clip255(v[4 + i]) << (8 * i);
+	}
+	return r;
+}
+
+__global__ void k_gray_in8(const uint8_t* __restrict__ pix, int16_t* __restrict__ out, int w, long po, int q)
+{
+	const int x = (blockIdx.x * blockDim.x + threadIdx.x) * 8, y = blockIdx.y;
+	if (x >= w) return;
+	int p[8];
+	unpack8(*reinterpret_cast<const uint2*>(pix + (long)y * w + x), p);
+	int16_t v[8];
+#pragma unroll
+	for (int i = 0; i < 8; i++) v[i] = q ? (int16_t)((p[i] - 128) << kShift) : (int16_t)(p[i] - 128);
+	*reinterpret_cast<uint4*>(out + (long)y * po + x) = pack8s(v);
+}
+
+__global__ void k_rgb_in8(const uint8_t* __restrict__ pix, int16_t* __restrict__ out, int w, int h, long po, int q)
+{
+	const int x = (blockIdx.x * blockDim.x + threadIdx.x) * 8, y = blockIdx.y;
+	if (x >= w) return;
+	const long n = (long)w * h, i0 = (long)y * w + x;
+	int r[8], g[8], b[8];
+	unpack8(*reinterpret_cast<const uint2*>(pix + i0), r);
+	unpack8(*reinterpret_cast<const uint2*>(pix + n + i0), g);
+	unpack8(*reinterpret_cast<const uint2*>(pix + 2 * n + i0), b);
+	int16_t Y[8], Cg[8], Co[8];
+#pragma unroll
+	for (int i = 0; i < 8; i++) {
+		int16_t R = (int16_t)r[i], G = (int16_t)g[i], B = (int16_t)b[i];
+		R = (int16_t)(R - B);
+		B = (int16_t)(B + (R >> 1));
+		G = (int16_t)(G - B);
+		B = (int16_t)(B + ((G >> 1) - 128));
+		if (q) { R = (int16_t)(R << (kShift - 1)); G = (int16_t)(G << (kShift - 1)); B = (int16_t)(B << kShift); }
+		Y[i] = B; Cg[i] = G; Co[i] = R;
+	}
+	const long o = (long)y * po + x, ps = po * h;
+	*reinterpret_cast<uint4*>(out + o) = pack8s(Y);
+	*reinterpret_cast<uint4*>(out + ps + o) = pack8s(Cg);
+	*reinterpret_cast<uint4*>(out + 2 * ps + o) = pack8s(Co);
+}
+
+__global__ void k_gray_out8(const int16_t* __restrict__ in, long pi, int w, int q, uint8_t* __restrict__ pix,
+                            int16_t* __restrict__ planes)
+{
+	const int x = (blockIdx.x * blockDim.x + threadIdx.x) * 8, y = blockIdx.y;
+	if (x >= w) return;
+	int16_t v[8];
+	unpack8s(*reinterpret_cast<const uint4*>(in + (long)y * pi + x), v);
+#pragma unroll
+	for (int i = 0; i < 8; i++) {
+		if (q == 0) v[i] = (int16_t)(v[i] + 128);
+		else v[i] = clip255((int16_t)(128 + ((v[i] + (1 << (kShift - 1))) >> kShift)));
+	}
+	const long i0 = (long)y * w + x;
+	if (planes) *reinterpret_cast<uint4*>(planes + i0) = pack8s(v);
+	if (pix) *reinterpret_cast<uint2*>(pix + i0) = pack8b(v);
+}
+
+__global__ void k_rgb_out8(const int16_t* __restrict__ in, long pi, int w, int h, int q, uint8_t* __restrict__ pix,
+                           int16_t* __restrict__ planes)
+{
+	const int x = (blockIdx.x * blockDim.x + threadIdx.x) * 8, y = blockIdx.y;
+	if (x >= w) return;
+	const long o = (long)y * pi + x, ps = pi * h;
+	int16_t Bv[8], Gv[8], Rv[8];
+	unpack8s(*reinterpret_cast<const uint4*>(in + o), Bv);               // Y
+	unpack8s(*reinterpret_cast<const uint4*>(in + ps + o), Gv);          // Cg
+	unpack8s(*reinterpret_cast<const uint4*>(in + 2 * ps + o), Rv);      // Co
+#pragma unroll
+	for (int i = 0; i < 8; i++) {
+		int16_t B = Bv[i], G = Gv[i], R = Rv[i];
+		if (q) {
+			R = (int16_t)((R + (1 << (kShift - 2))) >> (kShift - 1));
+			G = (int16_t)((G + (1 << (kShift - 2))) >> (kShift - 1));
+			B = (int16_t)((B + (1 << (kShift - 1))) >> kShift);
+		}
+		B = (int16_t)(B - ((G >> 1) - 128));
+		G = (int16_t)(G + B);
+		B = (int16_t)(B - (R >> 1));
+		R = (int16_t)(R + B);
+		if (q) { R = clip255(R); G = clip255(G); B = clip255(B); }
+		Rv[i] = R; Gv[i] = G; Bv[i] = B;
+	}
+	const long n = (long)w * h, i0 = (long)y * w + x;
+	if (planes) {
+		*reinterpret_cast<uint4*>(planes + i0) = pack8s(Rv);
+		*reinterpret_cast<uint4*>(planes + n + i0) = pack8s(Gv);
+		*reinterpret_cast<uint4*>(planes + 2 * n + i0) = pack8s(Bv);
+	}
+	if (pix) {
+		*reinterpret_cast<uint2*>(pix + i0) = pack8b(Rv);
+		*reinterpret_cast<uint2*>(pix + n + i0) = pack8b(Gv);
+		*reinterpret_cast<uint2*>(pix + 2 * n + i0) = pack8b(Bv);
+	}
+}
+
+bool vec8_ok(const void* pix, const void* planes, const void* planes2, int w, long pitch)
+{
+	return w % 8 == 0 && pitch % 8 == 0 && ((uintptr_t)pix % 8) == 0 && ((uintptr_t)planes % 16) == 0 &&
+	       ((uintptr_t)planes2 % 16) == 0;
+}
+
 }  // namespace
 
 void launch_pix_in(const uint8_t* pix, int16_t* planes, int w, int h, long po, int channels, int q, hipStream_t st)
 {
+	if (vec8_ok(pix, planes, nullptr, w, po)) {
+		dim3 grid8((w / 8 + 255) / 256, h);
+		if (channels == 3) hipLaunchKernelGGL(k_rgb_in8, grid8, dim3(256), 0, st, pix, planes, w, h, po, q);
+		else hipLaunchKernelGGL(k_gray_in8, grid8, dim3(256), 0, st, pix, planes, w, po, q);
+		return;
+	}
 	dim3 grid((w + 255) / 256, h);
 	if (channels == 3) hipLaunchKernelGGL(k_rgb_in, grid, dim3(256), 0, st, pix, planes, w, h, po, q);
 	else hipLaunchKernelGGL(k_gray_in, grid, dim3(256), 0, st, pix, planes, w, h, po, q);
@@ -85,6 +221,12 @@ void launch_pix_in(const uint8_t* pix, int16_t* planes, int w, int h, long po, i
 void launch_pix_out(const int16_t* planes_in, long pi, int w, int h, int channels, int q,
                     uint8_t* pix, int16_t* planes_out, hipStream_t st)
 {
+	if (vec8_ok(pix, planes_in, planes_out, w, pi)) {
+		dim3 grid8((w / 8 + 255) / 256, h);
+		if (channels == 3) hipLaunchKernelGGL(k_rgb_out8, grid8, dim3(256), 0, st, planes_in, pi, w, h, q, pix, planes_out);
+		else hipLaunchKernelGGL(k_gray_out8, grid8, dim3(256), 0, st, planes_in, pi, w, q, pix, planes_out);
+		return;
+	}
 	dim3 grid((w + 255) / 256, h);
 	if (channels == 3) hipLaunchKernelGGL(k_rgb_out, grid, dim3(256), 0, st, planes_in, pi, w, h, q, pix, planes_out);
 	else hipLaunchKernelGGL(k_gray_out, grid, dim3(256), 0, st, planes_in, pi, w, h, q, pix, planes_out);

@@ -5,8 +5,8 @@ Independent frames (C5) and tiles (C4) are independent .ric streams, so ranks
 share no state while coding: frame f goes to rank f mod N, tile (tx, ty) of a
 2x2 grid to rank 2*ty + tx.  The only exchange is the final gather of the
 variable-size compressed streams to rank 0: an all_gather of the stream sizes
-(int64) and then of the size-padded payloads (RCCL over xGMI with the "nccl"
-backend on GPUs, gloo on CPU).
+(int64), then a gather of the size-padded payloads to rank 0 (RCCL over xGMI
+with the "nccl" backend on GPUs, gloo on CPU).
 
 Tile container ("RTL1", our extension -- the reference has no tile syntax):
   "RTL1" | u16 W | u16 H | u8 nx | u8 ny | nx*ny u32 LE stream sizes |
@@ -86,8 +86,10 @@ def gather_streams(local, dist, device=None, to_host=True):
     if n_local:
         payload = np.frombuffer(b"".join(local), np.uint8)
         buf[:payload.size] = torch.from_numpy(payload.copy()).to(dev)
-    all_buf = [torch.zeros_like(buf) for _ in range(world)]
-    dist.all_gather(all_buf, buf)
+    # payloads go to rank 0 only (a gather, not an all_gather: the other
+    # ranks never need them)
+    all_buf = [torch.zeros_like(buf) for _ in range(world)] if rank == 0 else None
+    dist.gather(buf, gather_list=all_buf, dst=0)
     if rank != 0:
         return None
     if not to_host:
