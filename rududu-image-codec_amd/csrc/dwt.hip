@@ -773,6 +773,8 @@ struct FqArgs {
 	int Q[3], iQ[3];
 	int thres[3][16];
 	uint64_t* wgt;                     // diagnostics: per-workgroup timestamps (dbg 128), or null
+	int pk;                            // k_fwdq_gen: short bands whose thresholds pass pk_ok
+	int level;
 };
 
 struct PRow8 { v2s q[4]; };            // (c0,c2) (c4,c6) | (c1,c3) (c5,c7)
@@ -1487,7 +1489,12 @@ uint64_t* fq_wgtrace()
 
 void fq_launch_pc(FqArgs& a, hipStream_t st)
 {
-	const int S = pc_seg_rows(a.W, a.H);
+	// tuning knobs RIC_FQ_SL0..2: segment rows of level 0..2 (multiples of 8)
+	static const int sl[3] = {[] { const char* e = getenv("RIC_FQ_SL0"); return e ? atoi(e) : 0; }(),
+	                          [] { const char* e = getenv("RIC_FQ_SL1"); return e ? atoi(e) : 0; }(),
+	                          [] { const char* e = getenv("RIC_FQ_SL2"); return e ? atoi(e) : 0; }()};
+	int S = pc_seg_rows(a.W, a.H);
+	if (a.level < 3 && sl[a.level] >= 8 && sl[a.level] % 8 == 0) S = sl[a.level];
 	a.nseg = (a.H + S - 1) / S;
 	const int nstrip = (a.W + kFqStrip - 1) / kFqStrip;
 	static const int onewg = [] { const char* e = getenv("RIC_FQ_ONEWG"); return e ? atoi(e) : 0; }();
@@ -1530,8 +1537,8 @@ struct GenLL {
 };
 
 template <typename TO>
-__device__ __forceinline__ void gen_block(const FqArgs& a, const int* thr, const FqTables& F, const TO* const* d, int b,
-                                          int kx, int ky)
+__device__ __forceinline__ void gen_block(const FqArgs& a, const int* thr, const uint32_t* tpk, const FqTables& F,
+                                          const TO* const* d, int b, int kx, int ky)
 {
 	constexpr bool SH = sizeof(TO) == 2;
 	const int x0 = 4 * kx, y0 = 4 * ky, dx = a.dx[b], dy = a.dy[b];
@@ -1539,23 +1546,52 @@ __device__ __forceinline__ void gen_block(const FqArgs& a, const int* thr, const
 	const bool full = wdt == 4 && hgt == 4;
 	const long pb = a.p[b];
 	TO* base = const_cast<TO*>(d[b]) + (long)y0 * pb + x0;
-	// clamped addresses: all 16 loads issue back to back, no divergent branch
+	// clamped addresses; the block's 16 values and the children's pRD are all
+	// loaded before one pin of the whole batch: one memory round trip per
+	// block (a pin per load waits for each load in turn)
 	int v[16];
 #pragma unroll
 	for (int i = 0; i < 16; i++) {
 		const int r = min(i >> 2, hgt - 1), c = min(i & 3, wdt - 1);
-		const int x = pinned((int)base[r * pb + c]);
-		v[i] = ((i >> 2) < hgt && (i & 3) < wdt) ? x : 0;
+		v[i] = (int)base[r * pb + c];
 	}
-	uint32_t csum = 0;   // children pRD (u32 sum, as k_quant_level)
-	if (full && a.crd[b]) {
-		const uint32_t* c0 = a.crd[b] + (long)(2 * ky) * a.cbw[b] + 2 * kx;
-		const uint32_t* c1 = c0 + a.cbw[b];
-		csum = c0[0] + c0[1] + c1[0] + c1[1];
+	uint32_t cr[4] = {0u, 0u, 0u, 0u};
+	const uint32_t* crd = a.crd[b];
+	if (crd) {
+		const int cw = a.cbw[b], ch = a.cph[b];
+		const int cy0 = min(2 * ky, ch - 1), cy1 = min(2 * ky + 1, ch - 1);
+		const int cx0 = min(2 * kx, cw - 1), cx1 = min(2 * kx + 1, cw - 1);
+		cr[0] = crd[(long)cy0 * cw + cx0]; cr[1] = crd[(long)cy0 * cw + cx1];
+		cr[2] = crd[(long)cy1 * cw + cx0]; cr[3] = crd[(long)cy1 * cw + cx1];
 	}
+	asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7]),
+	                  "+v"(v[8]), "+v"(v[9]), "+v"(v[10]), "+v"(v[11]), "+v"(v[12]), "+v"(v[13]), "+v"(v[14]), "+v"(v[15]));
+	asm volatile("" : "+v"(cr[0]), "+v"(cr[1]), "+v"(cr[2]), "+v"(cr[3]));
+#pragma unroll
+	for (int i = 0; i < 16; i++) v[i] = ((i >> 2) < hgt && (i & 3) < wdt) ? v[i] : 0;
+	// children pRD: u32 sum, as k_quant_level (full blocks only)
+	const uint32_t csum = (full && crd) ? cr[0] + cr[1] + cr[2] + cr[3] : 0u;
 	uint32_t dist;
 	if (full) {
-		const uint64_t dd = (uint64_t)tsuq_full<SH>(v, a.Q[b], a.iQ[b], thr) + csum;
+		int cnt;
+		if (SH && a.pk) {
+			// the packed quantiser (same result when the thresholds pass pk_ok)
+			uint32_t w[8];
+#pragma unroll
+			for (int r = 0; r < 4; r++) {
+				w[2 * r] = (uint32_t)(uint16_t)v[4 * r] | ((uint32_t)(uint16_t)v[4 * r + 1] << 16);
+				w[2 * r + 1] = (uint32_t)(uint16_t)v[4 * r + 2] | ((uint32_t)(uint16_t)v[4 * r + 3] << 16);
+			}
+			cnt = tsuq_full_pk(w, a.Q[b], a.iQ[b], thr[0], tpk);
+#pragma unroll
+			for (int r = 0; r < 4; r++) {
+				v[4 * r] = (int16_t)(w[2 * r] & 0xFFFFu); v[4 * r + 1] = (int16_t)(w[2 * r] >> 16);
+				v[4 * r + 2] = (int16_t)(w[2 * r + 1] & 0xFFFFu); v[4 * r + 3] = (int16_t)(w[2 * r + 1] >> 16);
+			}
+		} else {
+			cnt = tsuq_full<SH>(v, a.Q[b], a.iQ[b], thr);
+		}
+		const uint64_t dd = (uint64_t)cnt + csum;
 		dist = dd > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)dd;
 	} else {
 		dist = (uint32_t)tsuq_edge<SH>(v, wdt, hgt, a.Q[b], a.iQ[b]);   // children ignored
@@ -1598,14 +1634,17 @@ __global__ void __launch_bounds__(256) k_fwdq_gen(FqArgs a, GenLL ll, int nseg)
 	for (int b = 0; b < 4; b++) { f.d[b] = reinterpret_cast<TO*>(a.d[b]); f.p[b] = a.p[b]; }
 	f.nseg = nseg; f.vec = a.vec8; f.nofast = 1;
 	const int X0 = strip * kStripValid - kCols;
-	fwd_seg<CDF97, TI, TO, kGenRows, false>(f, X0 + lane * kCols, lane, y0);
+	if constexpr (sizeof(TI) == 2 && sizeof(TO) == 2)
+		fwd97p_seg<kGenRows, false>(f, X0 + lane * kCols, lane, y0);     // packed 16-bit lifting
+	else
+		fwd_seg<CDF97, TI, TO, kGenRows, false>(f, X0 + lane * kCols, lane, y0);
 	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
 	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 	const TO* d[3] = {f.d[0], f.d[1], f.d[2]};
 	const int ky = y0 >> 3;
 	for (int i = lane; i < 3 * kGenBlocks; i += kLanes) {
 		const int b = i / kGenBlocks, kx = strip * kGenBlocks + (i - b * kGenBlocks);
-		if (kx < a.bw[b] && ky < a.bh[b]) gen_block<TO>(a, s_thres[b], s_F, d, b, kx, ky);
+		if (kx < a.bw[b] && ky < a.bh[b]) gen_block<TO>(a, s_thres[b], s_tpk[b], s_F, d, b, kx, ky);
 	}
 	if (ll.on) {
 		// CBand::TSUQ with Thres 0.5 on this wave's LL samples: all loads first
@@ -2012,7 +2051,9 @@ int seg_rows(int H)
 {
 	static const int forced = [] { const char* e = getenv("RIC_DWT_S"); return e ? atoi(e) : 0; }();
 	if (forced == 8 || forced == 16 || ((forced == 32 || forced == 64) && sizeof(T) == 2)) return forced;
-	return (sizeof(T) == 2 && H >= 4096) ? 32 : H >= 1024 ? 16 : 8;
+	// (16 rather than 32 rows on the 8K level: two rounds of waves balance
+	// better, k_inv level 0 44 -> 39 us)
+	return H >= 1024 ? 16 : 8;
 }
 // tuning knob: RIC_DWT_NOFAST=1 runs every wave on the checked path
 int dbg_nofast()
@@ -2118,7 +2159,7 @@ void launch_fwdq_level(const Pyramid& P, int l, const void* src, long sp, int ve
 	FqArgs a;
 	a.wgt = nullptr;
 	a.src = (const int16_t*)src; a.sp = sp; a.W = L.w; a.H = L.h;
-	a.vec8 = vec8; a.vec16 = vec16; a.nofast = dbg_nofast(); a.high = l == 0;
+	a.vec8 = vec8; a.vec16 = vec16; a.nofast = dbg_nofast(); a.high = l == 0; a.level = l; a.pk = 1;
 	for (int b = 0; b < 4; b++) { a.d[b] = (int16_t*)(arena + L.b[b].off); a.p[b] = L.b[b].pitch; }
 	for (int b = 0; b < 3; b++) {
 		const Band& B = L.b[b];
@@ -2150,7 +2191,8 @@ void launch_fwdq_gen_level(const Pyramid& P, int l, const void* src, long sp, in
 	FqArgs a;
 	a.wgt = nullptr;
 	a.src = (const int16_t*)src; a.sp = sp; a.W = L.w; a.H = L.h;
-	a.vec8 = vec8; a.vec16 = 0; a.nofast = 1; a.high = l == 0;
+	a.vec8 = vec8; a.vec16 = 0; a.nofast = 1; a.high = l == 0; a.level = l;
+	a.pk = !L.is_int && pk_ok(qp.thres[0]) && pk_ok(qp.thres[1]) && pk_ok(qp.thres[2]);
 	for (int b = 0; b < 4; b++) { a.d[b] = (int16_t*)(arena + L.b[b].off); a.p[b] = L.b[b].pitch; }
 	for (int b = 0; b < 3; b++) {
 		const Band& B = L.b[b];
