@@ -37,7 +37,9 @@ def _compile(src, hdr_mtime):
     if src.endswith(".hip"):
         cmd = [os.path.join(ROCM, "bin", "hipcc"), "--offload-arch=" + ARCH] + COMMON + ["-c", path, "-o", obj]
     else:
-        cmd = ["g++"] + COMMON + ["-Wall", "-D__HIP_PLATFORM_AMD__", "-I" + os.path.join(ROCM, "include"),
+        # host sources (the serial coder): x86-64-v3 (AVX2/BMI2/LZCNT, present on the
+        # GPU boxes' EPYC and this container's Xeon): encoder -7 %
+        cmd = ["g++"] + COMMON + ["-march=x86-64-v3", "-Wall", "-D__HIP_PLATFORM_AMD__", "-I" + os.path.join(ROCM, "include"),
                                   "-c", path, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
