@@ -1615,17 +1615,21 @@ __device__ __forceinline__ void gen_block(const FqArgs& a, const int* thr, const
 	}
 }
 
+// One workgroup per 8-row segment of a 248-column strip: wave 0 lifts the
+// segment (its loads are issued before the table staging) while the other
+// waves stage the tables; then all 256 threads quantise the segment's
+// 3 x 31 blocks (one round) and run the coarsest level's LL TSUQ.  The levels
+// that take this kernel are small and latency-bound: the wide block phase
+// replaces the two dependent rounds of a wave-per-segment form.
 template <typename TI, typename TO>
 __global__ void __launch_bounds__(256) k_fwdq_gen(FqArgs a, GenLL ll, int nseg)
 {
 	__shared__ int s_thres[3][16];
 	__shared__ FqTables s_F __attribute__((aligned(16)));
 	__shared__ uint32_t s_tpk[3][17 * 8];
-	fq_stage_tables<256>(a, s_thres, s_F, s_tpk);
-	__syncthreads();
 	const int lane = threadIdx.x & 63;
-	const int seg = blockIdx.y * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-	if (seg >= nseg) return;
+	const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+	const int seg = blockIdx.y;
 	const int strip = blockIdx.x;
 	const int y0 = seg * kGenRows;
 	FwdArgs<TI, TO> f;
@@ -1633,31 +1637,36 @@ __global__ void __launch_bounds__(256) k_fwdq_gen(FqArgs a, GenLL ll, int nseg)
 #pragma unroll
 	for (int b = 0; b < 4; b++) { f.d[b] = reinterpret_cast<TO*>(a.d[b]); f.p[b] = a.p[b]; }
 	f.nseg = nseg; f.vec = a.vec8; f.nofast = 1;
-	const int X0 = strip * kStripValid - kCols;
-	if constexpr (sizeof(TI) == 2 && sizeof(TO) == 2)
-		fwd97p_seg<kGenRows, false>(f, X0 + lane * kCols, lane, y0);     // packed 16-bit lifting
-	else
-		fwd_seg<CDF97, TI, TO, kGenRows, false>(f, X0 + lane * kCols, lane, y0);
+	if (w == 0) {
+		const int X0 = strip * kStripValid - kCols;
+		if constexpr (sizeof(TI) == 2 && sizeof(TO) == 2)
+			fwd97p_seg<kGenRows, false>(f, X0 + lane * kCols, lane, y0);     // packed 16-bit lifting
+		else
+			fwd_seg<CDF97, TI, TO, kGenRows, false>(f, X0 + lane * kCols, lane, y0);
+	}
+	fq_stage_tables<256>(a, s_thres, s_F, s_tpk);
+	// the bands wave 0 wrote are read by the whole workgroup
 	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+	__syncthreads();
 	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 	const TO* d[3] = {f.d[0], f.d[1], f.d[2]};
 	const int ky = y0 >> 3;
-	for (int i = lane; i < 3 * kGenBlocks; i += kLanes) {
+	for (int i = threadIdx.x; i < 3 * kGenBlocks; i += 256) {
 		const int b = i / kGenBlocks, kx = strip * kGenBlocks + (i - b * kGenBlocks);
 		if (kx < a.bw[b] && ky < a.bh[b]) gen_block<TO>(a, s_thres[b], s_tpk[b], s_F, d, b, kx, ky);
 	}
 	if (ll.on) {
-		// CBand::TSUQ with Thres 0.5 on this wave's LL samples: all loads first
+		// CBand::TSUQ with Thres 0.5 on this segment's LL samples: all loads first
 		constexpr bool SH = sizeof(TO) == 2;
 		constexpr int NLL = (kGenRows / 2) * (kStripValid / 2);
-		constexpr int PER = (NLL + kLanes - 1) / kLanes;
+		constexpr int PER = (NLL + 255) / 256;
 		const int ldx = a.W >> 1, ldy = a.H >> 1, c0 = strip * (kStripValid / 2), r0 = y0 >> 1;
 		int val[PER];
 		TO* q[PER];
 		bool in[PER];
 #pragma unroll
 		for (int k = 0; k < PER; k++) {
-			const int i = lane + k * kLanes;
+			const int i = threadIdx.x + k * 256;
 			const int r = r0 + i / (kStripValid / 2), c = c0 + i % (kStripValid / 2);
 			in[k] = i < NLL && r < ldy && c < ldx;
 			q[k] = f.d[BL] + (long)min(r, ldy - 1) * f.p[BL] + min(c, ldx - 1);
@@ -2213,7 +2222,7 @@ void launch_fwdq_gen_level(const Pyramid& P, int l, const void* src, long sp, in
 	GenLL ll = {ll_on, ll_iQ, ll_T0};
 	const int nseg = (L.h + kGenRows - 1) / kGenRows;
 	a.nseg = nseg;
-	dim3 grid((L.w + kStripValid - 1) / kStripValid, (nseg + kWavesPerBlock - 1) / kWavesPerBlock);
+	dim3 grid((L.w + kStripValid - 1) / kStripValid, nseg);   // one workgroup per segment
 	if (!L.in_is_int && !L.is_int) hipLaunchKernelGGL((k_fwdq_gen<int16_t, int16_t>), grid, dim3(256), 0, st, a, ll, nseg);
 	else if (!L.in_is_int) hipLaunchKernelGGL((k_fwdq_gen<int16_t, int32_t>), grid, dim3(256), 0, st, a, ll, nseg);
 	else hipLaunchKernelGGL((k_fwdq_gen<int32_t, int32_t>), grid, dim3(256), 0, st, a, ll, nseg);
