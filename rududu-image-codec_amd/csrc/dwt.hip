@@ -1782,19 +1782,67 @@ __device__ __forceinline__ void inv_seg(const InvArgs<TB, TL, TO>& a, int x, int
 	} else {
 		constexpr int R = S + 8;                 // band rows of image rows y0-4 .. y0+S+3
 		R2 rlo[R], rhi[R];
+		if constexpr (!FAST && TRANS == CDF97) {
+			// border waves: every raw element (clamped row of the same parity,
+			// clamped columns) is loaded first and the batch pinned at once, then
+			// the out-of-band rows / columns are zeroed -- one memory round trip
+			// for the segment (a pin per load waits for each load in turn)
+			int ra[R][4];
+			const int hiD = max(dxD - 1, 0), hiH = max(dxH - 1, 0);
+			const int cD0 = min(max(bx, 0), hiD), cD1 = min(max(bx + 1, 0), hiD);
+			const int cH0 = min(max(bx, 0), hiH), cH1 = min(max(bx + 1, 0), hiH);
 #pragma unroll
-		for (int i = 0; i < R; i++) {
-			const int y = y0 - 4 + i;
-			if (FAST) {
-				load_pair(y, rlo[i], rhi[i]);
-			} else {
-				// rows outside the image read as 0: the nearest row of the same
-				// parity (same bands), then a select -- no divergent branch
+			for (int i = 0; i < R; i++) {
+				const int y = y0 - 4 + i;
 				const int yc = y < 0 ? (y & 1) : y >= H ? H - 1 - ((H - 1 - y) & 1) : y;
-				R2 lo, hi;
-				load_pair(yc, lo, hi);
+				const long by = yc >> 1;
+				const TB* lo = (i & 1) ? a.d[BV] + by * a.p[BV] : a.d[BD] + by * a.p[BD];
+				if (i & 1) {
+					const TL* hl = a.ll + by * a.pl;
+					ra[i][2] = (int)hl[cH0]; ra[i][3] = (int)hl[cH1];
+				} else {
+					const TB* hh = a.d[BH] + by * a.p[BH];
+					ra[i][2] = (int)hh[cH0]; ra[i][3] = (int)hh[cH1];
+				}
+				ra[i][0] = (int)lo[cD0]; ra[i][1] = (int)lo[cD1];
+			}
+#pragma unroll
+			for (int i = 0; i < R; i += 4)
+				asm volatile("" : "+v"(ra[i][0]), "+v"(ra[i][1]), "+v"(ra[i][2]), "+v"(ra[i][3]),
+				                  "+v"(ra[i + 1][0]), "+v"(ra[i + 1][1]), "+v"(ra[i + 1][2]), "+v"(ra[i + 1][3]),
+				                  "+v"(ra[i + 2][0]), "+v"(ra[i + 2][1]), "+v"(ra[i + 2][2]), "+v"(ra[i + 2][3]),
+				                  "+v"(ra[i + 3][0]), "+v"(ra[i + 3][1]), "+v"(ra[i + 3][2]), "+v"(ra[i + 3][3]));
+			const bool iD0 = bx >= 0 && bx < dxD, iD1 = bx + 1 >= 0 && bx + 1 < dxD;
+			const bool iH0 = bx >= 0 && bx < dxH, iH1 = bx + 1 >= 0 && bx + 1 < dxH;
+#pragma unroll
+			for (int i = 0; i < R; i++) {
+				const int y = y0 - 4 + i;
 				const bool in = y >= 0 && y < H;
-				rlo[i] = in ? lo : R2{}; rhi[i] = in ? hi : R2{};
+				const int l0 = in && iD0 ? ra[i][0] : 0, l1 = in && iD1 ? ra[i][1] : 0;
+				const int h0 = in && iH0 ? ra[i][2] : 0, h1 = in && iH1 ? ra[i][3] : 0;
+				if constexpr (sizeof(TB) == 2) {
+					rlo[i] = (uint32_t)(uint16_t)l0 | ((uint32_t)l1 << 16);
+					rhi[i] = (uint32_t)(uint16_t)h0 | ((uint32_t)h1 << 16);
+				} else {
+					rlo[i] = make_int2(l0, l1);
+					rhi[i] = make_int2(h0, h1);
+				}
+			}
+		} else {
+#pragma unroll
+			for (int i = 0; i < R; i++) {
+				const int y = y0 - 4 + i;
+				if (FAST) {
+					load_pair(y, rlo[i], rhi[i]);
+				} else {
+					// rows outside the image read as 0: the nearest row of the same
+					// parity (same bands), then a select -- no divergent branch
+					const int yc = y < 0 ? (y & 1) : y >= H ? H - 1 - ((H - 1 - y) & 1) : y;
+					R2 lo, hi;
+					load_pair(yc, lo, hi);
+					const bool in = y >= 0 && y < H;
+					rlo[i] = in ? lo : R2{}; rhi[i] = in ? hi : R2{};
+				}
 			}
 		}
 		int w0[4] = {0, 0, 0, 0}, w1[4] = {0, 0, 0, 0}, w2[4] = {0, 0, 0, 0}, w3[4] = {0, 0, 0, 0};
