@@ -955,6 +955,27 @@ __device__ __forceinline__ void pc_barrier(int dbg, uint64_t* tr = nullptr)
 	if (tr && threadIdx.x % 64 == 0) tr[1] = __builtin_amdgcn_s_memrealtime();
 }
 
+// Decoupled hand-off (k_fwdq_pc<true>): a ring of kRing block-row slots in
+// LDS with counters instead of one workgroup barrier per block row, so the
+// producer may run up to kRing block rows ahead of the slowest consumer and
+// neither side waits for the other's slowest iteration.  ring[0] = block rows
+// published by the producer, ring[1 + b] = block rows consumer b has taken.
+// A publish first waits for the wave's own LDS writes (lgkmcnt(0)), so a
+// consumer that reads the new count and then the slot sees the slot's data.
+constexpr int kRing = 4;
+__device__ __forceinline__ int ring_get(int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+__device__ __forceinline__ void ring_put(int* p, int v)
+{
+	asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+	__hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// bounded spin (~30 ms): a protocol error ends in wrong output, never a hang
+__device__ __forceinline__ void ring_wait_ge(int* p, int need)
+{
+	for (int n = 0; ring_get(p) < need && n < (1 << 20); n++) __builtin_amdgcn_s_sleep(1);
+	asm volatile("" ::: "memory");
+}
+
 // One wave's segment: the forward 9/7 of rows [y0, y0 + S) of a 496-column
 // strip and the quantiser, records and parent info of the block rows they
 // make, all in registers.  EDGE: the wave touches an image border (m).
@@ -971,7 +992,7 @@ template <bool EDGE, bool PC = false, typename Stage = NoStage>
 __device__ __forceinline__ void fq_seg(const FqArgs& a, const int (*thr)[16], const uint32_t (*tpk)[17 * 8],
                                        const FqTables& F, int x, int lane, int y0, int kx, const FqBorder& m, int S,
                                        uint2 (*pcbuf)[3][4][kLanes] = nullptr, int dbg = 0, uint64_t* tr = nullptr,
-                                       const Stage& stage = Stage())
+                                       const Stage& stage = Stage(), int* hring = nullptr)
 {
 	const bool out_lane = lane >= 1 && lane <= kLanes - 2 && (!EDGE || x < a.W);
 	int16_t* pL = a.d[BL] + (long)(y0 >> 1) * a.p[BL] + (x >> 1);
@@ -1039,7 +1060,19 @@ __device__ __forceinline__ void fq_seg(const FqArgs& a, const int (*thr)[16], co
 	};
 	auto iteration = [&](int it, uint4 (&rg)[2 * PF]) {
 		const bool last = it + 1 == nit;
-		cur = it & 1;
+		if (PC && hring) {
+			// block row it - 1 goes to slot (it - 1) % kRing, free once every
+			// consumer has taken block row it - 1 - kRing
+			cur = (it - 1) & (kRing - 1);
+			const int need = it - kRing;
+			if (need > 0) {
+				ring_wait_ge(hring + 1, need);
+				ring_wait_ge(hring + 2, need);
+				ring_wait_ge(hring + 3, need);
+			}
+		} else {
+			cur = it & 1;
+		}
 #pragma unroll
 		for (int k = 0; k < PF; k++) {
 			if (EDGE && last && k >= kend) break;
@@ -1093,8 +1126,12 @@ __device__ __forceinline__ void fq_seg(const FqArgs& a, const int (*thr)[16], co
 			w0 = w2; w1 = w3;
 			emit(3);
 		}
-		if constexpr (PC) pc_barrier(dbg, tr ? tr + 2 * min(it, kWgIt - 1) : nullptr);   // the consumers take the block row
-		else if (it >= 1) quant_row((y0 >> 3) + it - 1);   // a block row is complete
+		if constexpr (PC) {
+			if (hring) { if (it >= 1) ring_put(hring, it); }   // block row it - 1 published
+			else pc_barrier(dbg, tr ? tr + 2 * min(it, kWgIt - 1) : nullptr);   // the consumers take the block row
+		} else if (it >= 1) {
+			quant_row((y0 >> 3) + it - 1);   // a block row is complete
+		}
 	};
 	if constexpr (DEPTH == 1) {
 #pragma unroll 1
@@ -1204,12 +1241,15 @@ constexpr int kWgTraceMax = 8192;
 // producers on distinct SIMDs by HW_ID made no measurable difference, and a
 // role known before the first barrier lets the producer issue its prologue
 // row loads before the workgroup stages the format tables.
+template <bool ASYNC>
 __global__ void __launch_bounds__(256, 4) k_fwdq_pc(FqArgs a, int S, int dbg)
 {
 	__shared__ int s_thres[3][16];
 	__shared__ FqTables s_F __attribute__((aligned(16)));
 	__shared__ uint32_t s_tpk[3][17 * 8];
-	__shared__ uint2 s_buf[2][3][4][kLanes];
+	__shared__ uint2 s_buf[ASYNC ? kRing : 2][3][4][kLanes];
+	__shared__ int s_ring[4];
+	if (ASYNC && threadIdx.x < 4) s_ring[threadIdx.x] = 0;     // ordered by the staging barrier
 	// dbg 128 (diagnostics, level 0 only): per-workgroup record of kWgRec u64 --
 	// start realtime (100 MHz), start shader clock, the end realtime of waves
 	// 0-3, producer hw id << 32 | end shader clock of wave 0, workgroup index,
@@ -1245,22 +1285,37 @@ __global__ void __launch_bounds__(256, 4) k_fwdq_pc(FqArgs a, int S, int dbg)
 			m.eL0 = x == 0 ? 0x0000FFFFu : 0u;
 			m.oR3 = x + 7 == a.W - 1 ? 0xFFFF0000u : 0u;
 			m.ld = x >= 0 && x < a.W;
-			fq_seg<true, true>(a, s_thres, s_tpk, s_F, x, lane, y0, kx, m, S, s_buf, dbg, wgt ? wgt + 8 : nullptr, stage);
+			fq_seg<true, true>(a, s_thres, s_tpk, s_F, x, lane, y0, kx, m, S, s_buf, dbg, wgt ? wgt + 8 : nullptr, stage,
+			                   ASYNC ? s_ring : nullptr);
 		} else {
-			fq_seg<false, true>(a, s_thres, s_tpk, s_F, x, lane, y0, kx, m, S, s_buf, dbg, wgt ? wgt + 8 : nullptr, stage);
+			fq_seg<false, true>(a, s_thres, s_tpk, s_F, x, lane, y0, kx, m, S, s_buf, dbg, wgt ? wgt + 8 : nullptr, stage,
+			                    ASYNC ? s_ring : nullptr);
 		}
 	} else {
 		stage();
 		const int b = wave - 1;
 		const bool out_lane = lane >= 1 && lane <= kLanes - 2 && x < a.W;
+		if constexpr (ASYNC) {
 #pragma unroll 1
-		for (int it = 0; it < nit; it++) {
-			pc_barrier(dbg, wgt ? wgt + 8 + wave * 2 * kWgIt + 2 * min(it, kWgIt - 1) : nullptr);   // matches the producer's iteration `it`
-			if (it == 0 || (dbg & 3) == 2) continue;     // dbg 2: timing of the lifting alone
-			uint2 buf[4];
+			for (int j = 0; j + 1 < nit; j++) {          // block row j = the producer's iteration j + 1
+				ring_wait_ge(s_ring, j + 1);
+				uint2 buf[4];
 #pragma unroll
-			for (int r = 0; r < 4; r++) buf[r] = s_buf[it & 1][b][r][lane];
-			fq_block_regs(a, s_thres[b], s_tpk[b], s_F, b, buf, kx, (y0 >> 3) + it - 1, out_lane);
+				for (int r = 0; r < 4; r++) buf[r] = s_buf[j & (kRing - 1)][b][r][lane];
+				ring_put(s_ring + 1 + b, j + 1);            // (after the slot reads completed)
+				if ((dbg & 3) == 2) continue;
+				fq_block_regs(a, s_thres[b], s_tpk[b], s_F, b, buf, kx, (y0 >> 3) + j, out_lane);
+			}
+		} else {
+#pragma unroll 1
+			for (int it = 0; it < nit; it++) {
+				pc_barrier(dbg, wgt ? wgt + 8 + wave * 2 * kWgIt + 2 * min(it, kWgIt - 1) : nullptr);   // matches the producer's iteration `it`
+				if (it == 0 || (dbg & 3) == 2) continue;     // dbg 2: timing of the lifting alone
+				uint2 buf[4];
+#pragma unroll
+				for (int r = 0; r < 4; r++) buf[r] = s_buf[it & 1][b][r][lane];
+				fq_block_regs(a, s_thres[b], s_tpk[b], s_F, b, buf, kx, (y0 >> 3) + it - 1, out_lane);
+			}
 		}
 	}
 	if (wgt && lane == 0) {
@@ -1511,10 +1566,12 @@ void fq_launch_pc(FqArgs& a, hipStream_t st)
 	if (two) {
 		if (onewg) hipLaunchKernelGGL(k_fwdq_pc2, dim3(1, 1), dim3(320), 0, st, a, S, dbg | 4);
 		else hipLaunchKernelGGL(k_fwdq_pc2, dim3(nstrip, a.nseg), dim3(320), 0, st, a, S, dbg);
-	} else if (onewg) {
-		hipLaunchKernelGGL(k_fwdq_pc, dim3(1, 1), dim3(256), 0, st, a, S, dbg | 4);
 	} else {
-		hipLaunchKernelGGL(k_fwdq_pc, dim3(nstrip, a.nseg), dim3(256), 0, st, a, S, dbg);
+		static const int async = [] { const char* e = getenv("RIC_FQ_ASYNC"); return e ? atoi(e) : 1; }();
+		const dim3 grid = onewg ? dim3(1, 1) : dim3(nstrip, a.nseg);
+		if (onewg) dbg |= 4;
+		if (async) hipLaunchKernelGGL(k_fwdq_pc<true>, grid, dim3(256), 0, st, a, S, dbg & ~128);
+		else hipLaunchKernelGGL(k_fwdq_pc<false>, grid, dim3(256), 0, st, a, S, dbg);
 	}
 }
 
