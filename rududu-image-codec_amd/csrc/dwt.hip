@@ -1339,7 +1339,7 @@ __global__ void __launch_bounds__(256, 4) k_fwdq_pc(FqArgs a, int S, int dbg)
 template <bool EDGE, typename Stage>
 __device__ __forceinline__ void fq2_producer(const FqArgs& a, int x, int lane, int h, int y0, const FqBorder& mb,
                                              int S, uint2 (*pcbuf)[3][4][kLanes], int dbg, uint64_t* tr,
-                                             const Stage& stage)
+                                             const Stage& stage, int* hring)
 {
 	const bool out_lane = lane >= 1 && lane <= kLanes - 2 && (!EDGE || x < a.W);
 	const EdgeMasks em = edge_masks(x, a.W);
@@ -1379,7 +1379,19 @@ __device__ __forceinline__ void fq2_producer(const FqArgs& a, int x, int lane, i
 	};
 	auto iteration = [&](int it, uint2 (&rg)[2 * PF]) {
 		const bool last = it + 1 == nit;
-		cur = it & 1;
+		if (hring) {
+			// ring hand-off (see ring_put): hring[h] = block rows published by
+			// this half, hring[2 + b] = block rows consumer b has taken
+			cur = (it - 1) & (kRing - 1);
+			const int need = it - kRing;
+			if (need > 0) {
+				ring_wait_ge(hring + 2, need);
+				ring_wait_ge(hring + 3, need);
+				ring_wait_ge(hring + 4, need);
+			}
+		} else {
+			cur = it & 1;
+		}
 #pragma unroll
 		for (int k = 0; k < PF; k++) {
 			if (EDGE && last && k >= kend) break;
@@ -1424,7 +1436,8 @@ __device__ __forceinline__ void fq2_producer(const FqArgs& a, int x, int lane, i
 			w0 = w2; w1 = w3;
 			emit(3);
 		}
-		pc_barrier(dbg, tr ? tr + 2 * min(it, kWgIt - 1) : nullptr);   // the consumers take the block row
+		if (hring) { if (it >= 1) ring_put(hring + h, it); }
+		else pc_barrier(dbg, tr ? tr + 2 * min(it, kWgIt - 1) : nullptr);   // the consumers take the block row
 	};
 	int it = 0;
 #pragma unroll 1
@@ -1437,12 +1450,15 @@ __device__ __forceinline__ void fq2_producer(const FqArgs& a, int x, int lane, i
 
 // grid (strips, segments), 5 waves: 0, 1 = producers of the two halves,
 // 2..4 = the D, H, V consumers
+template <bool ASYNC>
 __global__ void __launch_bounds__(320) k_fwdq_pc2(FqArgs a, int S, int dbg)
 {
 	__shared__ int s_thres[3][16];
 	__shared__ FqTables s_F __attribute__((aligned(16)));
 	__shared__ uint32_t s_tpk[3][17 * 8];
-	__shared__ uint2 s_buf[2][3][4][kLanes];
+	__shared__ uint2 s_buf[ASYNC ? kRing : 2][3][4][kLanes];
+	__shared__ int s_ring[5];
+	if (ASYNC && threadIdx.x < 5) s_ring[threadIdx.x] = 0;     // ordered by the staging barrier
 	const int wgi = blockIdx.y * gridDim.x + blockIdx.x;
 	uint64_t* wgt = ((dbg & 128) && a.wgt && wgi < kWgTraceMax) ? a.wgt + kWgRec * wgi : nullptr;
 	if (wgt && threadIdx.x == 0) {
@@ -1467,22 +1483,37 @@ __global__ void __launch_bounds__(320) k_fwdq_pc2(FqArgs a, int S, int dbg)
 		if (!(dbg & 2048)) __builtin_amdgcn_s_setprio(2);
 		const int x = SX + w * (kStripValid) - kCols + lane * kCols;   // 4 columns per lane
 		uint64_t* tr = (wgt && w == 0) ? wgt + 8 : nullptr;        // trace roles: producer 0, D, H, V
-		if (edge) fq2_producer<true>(a, x, lane, w, y0, mb, S, s_buf, dbg, tr, stage);
-		else fq2_producer<false>(a, x, lane, w, y0, mb, S, s_buf, dbg, tr, stage);
+		int* hr = ASYNC ? s_ring : nullptr;
+		if (edge) fq2_producer<true>(a, x, lane, w, y0, mb, S, s_buf, dbg, tr, stage, hr);
+		else fq2_producer<false>(a, x, lane, w, y0, mb, S, s_buf, dbg, tr, stage, hr);
 	} else {
 		stage();
 		const int b = w - 2;
 		const int xc = SX - 8 + lane * 8;                        // the block's 8 image columns
 		const int kx = strip * (kFqStrip / 8) + lane - 1;
 		const bool out_lane = lane >= 1 && lane <= kLanes - 2 && xc < a.W;
+		if constexpr (ASYNC) {
 #pragma unroll 1
-		for (int it = 0; it < nit; it++) {
-			pc_barrier(dbg, wgt ? wgt + 8 + (w - 1) * 2 * kWgIt + 2 * min(it, kWgIt - 1) : nullptr);
-			if (it == 0 || (dbg & 3) == 2) continue;     // dbg 2: timing of the lifting alone
-			uint2 buf[4];
+			for (int j = 0; j + 1 < nit; j++) {          // block row j: both halves published
+				ring_wait_ge(s_ring, j + 1);
+				ring_wait_ge(s_ring + 1, j + 1);
+				uint2 buf[4];
 #pragma unroll
-			for (int r = 0; r < 4; r++) buf[r] = s_buf[it & 1][b][r][lane];
-			fq_block_regs(a, s_thres[b], s_tpk[b], s_F, b, buf, kx, (y0 >> 3) + it - 1, out_lane);
+				for (int r = 0; r < 4; r++) buf[r] = s_buf[j & (kRing - 1)][b][r][lane];
+				ring_put(s_ring + 2 + b, j + 1);
+				if ((dbg & 3) == 2) continue;
+				fq_block_regs(a, s_thres[b], s_tpk[b], s_F, b, buf, kx, (y0 >> 3) + j, out_lane);
+			}
+		} else {
+#pragma unroll 1
+			for (int it = 0; it < nit; it++) {
+				pc_barrier(dbg, wgt ? wgt + 8 + (w - 1) * 2 * kWgIt + 2 * min(it, kWgIt - 1) : nullptr);
+				if (it == 0 || (dbg & 3) == 2) continue;     // dbg 2: timing of the lifting alone
+				uint2 buf[4];
+#pragma unroll
+				for (int r = 0; r < 4; r++) buf[r] = s_buf[it & 1][b][r][lane];
+				fq_block_regs(a, s_thres[b], s_tpk[b], s_F, b, buf, kx, (y0 >> 3) + it - 1, out_lane);
+			}
 		}
 	}
 	if (wgt && lane == 0) {
@@ -1564,8 +1595,11 @@ void fq_launch_pc(FqArgs& a, hipStream_t st)
 	static const int force2 = [] { const char* e = getenv("RIC_FQ_PC2"); return e ? atoi(e) : -1; }();
 	const bool two = force2 >= 0 ? force2 != 0 : !a.high;
 	if (two) {
-		if (onewg) hipLaunchKernelGGL(k_fwdq_pc2, dim3(1, 1), dim3(320), 0, st, a, S, dbg | 4);
-		else hipLaunchKernelGGL(k_fwdq_pc2, dim3(nstrip, a.nseg), dim3(320), 0, st, a, S, dbg);
+		static const int async2 = [] { const char* e = getenv("RIC_FQ_ASYNC"); return e ? atoi(e) : 1; }();
+		const dim3 grid2 = onewg ? dim3(1, 1) : dim3(nstrip, a.nseg);
+		const int dbg2 = onewg ? dbg | 4 : dbg;
+		if (async2) hipLaunchKernelGGL(k_fwdq_pc2<true>, grid2, dim3(320), 0, st, a, S, dbg2 & ~128);
+		else hipLaunchKernelGGL(k_fwdq_pc2<false>, grid2, dim3(320), 0, st, a, S, dbg2);
 	} else {
 		static const int async = [] { const char* e = getenv("RIC_FQ_ASYNC"); return e ? atoi(e) : 1; }();
 		const dim3 grid = onewg ? dim3(1, 1) : dim3(nstrip, a.nseg);
