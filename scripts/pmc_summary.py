@@ -36,7 +36,7 @@ def grid(r):
 
 def fwd_l0(rs):
     """The level-0 launches of the fused forward level kernel (largest grid)."""
-    fw = [r for r in rs if "k_fwdq_pc" in r["Kernel_Name"]]
+    fw = [r for r in rs if "k_fwdq_pc<" in r["Kernel_Name"] or r["Kernel_Name"].startswith("ric::(anonymous namespace)::k_fwdq_pc(")]
     if not fw:
         return []
     g = max(grid(r) for r in fw)
