@@ -76,7 +76,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=0, help="frames per GPU per step (default: 4 per host thread)")
+    ap.add_argument("--batch", type=int, default=0, help="frames per GPU per step (default: 8 per host thread)")
     ap.add_argument("--threads", type=int, default=0, help="host coder threads per GPU (default 16)")
     ap.add_argument("--width", type=int, default=7680)
     ap.add_argument("--height", type=int, default=4320)
@@ -149,10 +149,12 @@ def main():
     import shard
     W, H = a.width, a.height
     threads = a.threads or 16
-    # 4 frames per host coder thread: the threads drift apart after their
+    # 8 frames per host coder thread: the threads drift apart after their
     # first frame, so their exclusive GPU sections stop queueing behind one
-    # another (16 frames per step: 1490-1750 Mpix/s, 64: 1990 on one box)
-    batch = a.batch or 4 * threads
+    # another, and the idle tail at the end of a step (threads waiting for the
+    # last frames) shrinks with the frames per thread (one box, 16 threads:
+    # 16 frames per step 1490-1750 Mpix/s, 64: 2023, 128: 2072, 256: 2089)
+    batch = a.batch or 8 * threads
     threads = min(threads, batch)
 
     # synthetic frames, uploaded to HBM before timing

@@ -43,12 +43,12 @@ template <typename T>
 __device__ __forceinline__ void load4(const T* __restrict__ row, int x, int W, bool vec, int (&c)[4])
 {
 	(void)vec;
+	int v[4];
 #pragma unroll
-	for (int j = 0; j < 4; j++) {
-		const int xj = x + j;
-		const int v = pinned((int)row[min(max(xj, 0), W - 1)]);
-		c[j] = (xj >= 0 && xj < W) ? v : 0;
-	}
+	for (int j = 0; j < 4; j++) v[j] = (int)row[min(max(x + j, 0), W - 1)];
+	asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]));   // one wait for the four loads
+#pragma unroll
+	for (int j = 0; j < 4; j++) c[j] = (x + j >= 0 && x + j < W) ? v[j] : 0;
 }
 
 // store two consecutive band values (band columns bx, bx+1), bounded by dx
@@ -70,7 +70,8 @@ template <typename T>
 __device__ __forceinline__ void load2(const T* __restrict__ row, int bx, int dx, int& a, int& b)
 {
 	const int hi = dx > 0 ? dx - 1 : 0;
-	const int v0 = pinned((int)row[min(max(bx, 0), hi)]), v1 = pinned((int)row[min(max(bx + 1, 0), hi)]);
+	int v0 = (int)row[min(max(bx, 0), hi)], v1 = (int)row[min(max(bx + 1, 0), hi)];
+	asm volatile("" : "+v"(v0), "+v"(v1));   // one wait for both loads
 	a = (bx >= 0 && bx < dx) ? v0 : 0;
 	b = (bx + 1 >= 0 && bx + 1 < dx) ? v1 : 0;
 }
@@ -532,12 +533,47 @@ __device__ __forceinline__ void fwd_seg(const FwdArgs<TI, TO>& a, int x, int lan
 		constexpr int R = S + 8;                 // input rows y0-4 .. y0+S+3
 		using RT = typename Raw4<TI>::type;
 		RT raw[R];
+		if constexpr (FAST) {
 #pragma unroll
-		for (int i = 0; i < R; i++) {
-			const int y = y0 - 4 + i;
-			const int yc = FAST ? y : min(max(y, 0), H - 1);      // rows outside the image read as 0
-			const RT r = load_row4<TI, EDGE>(a.src + (long)yc * a.sp, x, W, a.vec != 0);
-			raw[i] = (FAST || (y >= 0 && y < H)) ? r : RT{};
+			for (int i = 0; i < R; i++) raw[i] = load_row4<TI, false>(a.src + (long)(y0 - 4 + i) * a.sp, x, W, a.vec != 0);
+		} else {
+			// batches of 16 rows: every element of the batch (clamped row and
+			// columns) is loaded before one pin per 4 rows, then the rows and
+			// columns outside the image are zeroed -- one memory round trip per
+			// batch (a pin or a select right after each load waits for it)
+			const int xc[4] = {min(max(x, 0), W - 1), min(max(x + 1, 0), W - 1), min(max(x + 2, 0), W - 1),
+			                   min(max(x + 3, 0), W - 1)};
+			constexpr int RB = 16;
+			static_assert(R % 4 == 0, "segment rows");
+#pragma unroll
+			for (int i0 = 0; i0 < R; i0 += RB) {
+				int ev[RB][4];
+#pragma unroll
+				for (int i = 0; i < RB; i++) {
+					if (i0 + i >= R) break;
+					const TI* row = a.src + (long)min(max(y0 - 4 + i0 + i, 0), H - 1) * a.sp;
+#pragma unroll
+					for (int j = 0; j < 4; j++) ev[i][j] = (int)row[xc[j]];
+				}
+#pragma unroll
+				for (int i = 0; i < RB; i += 4) {
+					if (i0 + i >= R) break;
+					asm volatile("" : "+v"(ev[i][0]), "+v"(ev[i][1]), "+v"(ev[i][2]), "+v"(ev[i][3]),
+					                  "+v"(ev[i + 1][0]), "+v"(ev[i + 1][1]), "+v"(ev[i + 1][2]), "+v"(ev[i + 1][3]),
+					                  "+v"(ev[i + 2][0]), "+v"(ev[i + 2][1]), "+v"(ev[i + 2][2]), "+v"(ev[i + 2][3]),
+					                  "+v"(ev[i + 3][0]), "+v"(ev[i + 3][1]), "+v"(ev[i + 3][2]), "+v"(ev[i + 3][3]));
+				}
+#pragma unroll
+				for (int i = 0; i < RB; i++) {
+					if (i0 + i >= R) break;
+					const int y = y0 - 4 + i0 + i;
+					const bool in = y >= 0 && y < H;
+					int c[4];
+#pragma unroll
+					for (int j = 0; j < 4; j++) c[j] = in && x + j >= 0 && x + j < W ? ev[i][j] : 0;
+					raw[i0 + i] = pack4<TI>(c);
+				}
+			}
 		}
 		int w0[4] = {0, 0, 0, 0}, w1[4] = {0, 0, 0, 0}, w2[4] = {0, 0, 0, 0};
 		int w3[4] = {0, 0, 0, 0}, w4[4], w5[4] = {0, 0, 0, 0};
@@ -636,18 +672,36 @@ __device__ __forceinline__ void fwd97p_seg(const FwdArgs<int16_t, int16_t>& a, i
 	// body (PF pairs) stays small enough to live in the instruction cache.
 	constexpr int NP = (S + 8) / 2, PF = 4;
 	static_assert(NP % PF == 0, "segment rows");
-	uint2 ring[2 * PF];
+	// Border waves: a slot holds the raw elements of clamped columns of a
+	// clamped row, loaded unconditionally and masked when the slot is taken (a
+	// select or a pin right after a load is waited for at once: one memory
+	// round trip per element).  Rows outside the image are never consumed:
+	// pairs with e < 0 or e >= H are skipped, and row e + 1 >= H is unused.
+	struct FRaw { int c0, c1, c2, c3; };
+	using Slot = typename std::conditional<FAST, uint2, FRaw>::type;
+	Slot ring[2 * PF];
 	const int16_t* rp = a.src + (long)(y0 - 4) * a.sp;   // wave-uniform row pointer
 	int yl = y0 - 4;
-	auto load_next = [&](uint2& dst) {
-		if (FAST) {
+	const int xc0 = min(max(x, 0), W - 1), xc1 = min(max(x + 1, 0), W - 1);
+	const int xc2 = min(max(x + 2, 0), W - 1), xc3 = min(max(x + 3, 0), W - 1);
+	const uint32_t cm0 = (x >= 0 && x < W ? 0xFFFFu : 0u) | (x + 1 >= 0 && x + 1 < W ? 0xFFFF0000u : 0u);
+	const uint32_t cm1 = (x + 2 >= 0 && x + 2 < W ? 0xFFFFu : 0u) | (x + 3 >= 0 && x + 3 < W ? 0xFFFF0000u : 0u);
+	auto load_next = [&](Slot& dst) {
+		if constexpr (FAST) {
 			dst = load_row4<int16_t, false>(rp, x, W, true);
 		} else {
-			// rows outside the image read as 0 (clamped row, then a select)
-			const uint2 r = load_row4<int16_t, true>(a.src + (long)min(max(yl, 0), H - 1) * a.sp, x, W, a.vec != 0);
-			dst = (yl >= 0 && yl < H) ? r : make_uint2(0, 0);
+			const int16_t* r = a.src + (long)min(max(yl, 0), H - 1) * a.sp;
+			dst.c0 = r[xc0]; dst.c1 = r[xc1]; dst.c2 = r[xc2]; dst.c3 = r[xc3];
 		}
 		rp += a.sp; yl++;
+	};
+	auto take = [&](const Slot& r) -> PRow {
+		if constexpr (FAST) {
+			return prow_from_u2(r);
+		} else {
+			return prow_from_u2(make_uint2(((uint32_t)(uint16_t)r.c0 | ((uint32_t)r.c1 << 16)) & cm0,
+			                               ((uint32_t)(uint16_t)r.c2 | ((uint32_t)r.c3 << 16)) & cm1));
+		}
 	};
 #pragma unroll
 	for (int j = 0; j < 2 * PF; j++) load_next(ring[j]);
@@ -662,7 +716,7 @@ __device__ __forceinline__ void fwd97p_seg(const FwdArgs<int16_t, int16_t>& a, i
 		// unpack the slot first, so its registers are free for the refill
 		// (a refill into fresh registers would need a copy at the back-edge,
 		// and that copy waits for the load)
-		const PRow n0 = prow_from_u2(ring[2 * k]), n1 = prow_from_u2(ring[2 * k + 1]);
+		const PRow n0 = take(ring[2 * k]), n1 = take(ring[2 * k + 1]);
 		if (it + 1 < NP / PF) { load_next(ring[2 * k]); load_next(ring[2 * k + 1]); }
 		if (!FAST && (e < 0 || e >= H)) continue;
 		w4 = n0;
@@ -871,16 +925,41 @@ __device__ __forceinline__ void fq_child_pin_pk(const FqArgs& a, int b, const ui
 	}
 }
 
+// The children pRD of block (kx, ky), loaded ahead of the block (consumer
+// waves prefetch the next block row's): unconditional loads at clamped
+// addresses -- a level without children reads its own pRD array's first word
+// -- masked by `on` when summed (u32 sum, then widened, as fq_dist).
+struct FqCrd { uint32_t c[4]; bool on; };
+__device__ __forceinline__ FqCrd fq_crd_load(const FqArgs& a, int b, int kx, int ky)
+{
+	FqCrd r;
+	r.on = a.crd[b] != nullptr;
+	const uint32_t* crd = r.on ? a.crd[b] : a.rd[b];
+	const int cw = r.on ? a.cbw[b] : 1, ch = r.on ? a.cph[b] : 1;
+	const int cy0 = min(max(2 * ky, 0), ch - 1), cy1 = min(max(2 * ky + 1, 0), ch - 1);
+	const int cx0 = min(max(2 * kx, 0), cw - 1), cx1 = min(max(2 * kx + 1, 0), cw - 1);
+	r.c[0] = crd[(long)cy0 * cw + cx0]; r.c[1] = crd[(long)cy0 * cw + cx1];
+	r.c[2] = crd[(long)cy1 * cw + cx0]; r.c[3] = crd[(long)cy1 * cw + cx1];
+	return r;
+}
+__device__ __forceinline__ uint32_t fq_dist_pre(int cnt, const FqCrd& cr)
+{
+	const uint64_t d = (uint64_t)cnt + (cr.on ? (uint32_t)(cr.c[0] + cr.c[1] + cr.c[2] + cr.c[3]) : 0u);
+	return d > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)d;
+}
+
 // one full block from the register buffer (4 band rows of 4 shorts = 8
-// packed words, row r = words 2r, 2r + 1)
+// packed words, row r = words 2r, 2r + 1); cr = its children's pRD
+// (fq_crd_load), or null to load them here
 __device__ __forceinline__ void fq_block_regs(const FqArgs& a, const int* thr, const uint32_t* tpk, const FqTables& F,
-                                              int b, const uint2 (&buf)[4], int kx, int ky, bool out_lane)
+                                              int b, const uint2 (&buf)[4], int kx, int ky, bool out_lane,
+                                              const FqCrd* cr = nullptr)
 {
 	uint32_t w[8];
 #pragma unroll
 	for (int r = 0; r < 4; r++) { w[2 * r] = buf[r].x; w[2 * r + 1] = buf[r].y; }
 	const int cnt = tsuq_full_pk(w, a.Q[b], a.iQ[b], thr[0], tpk);   // levels are fused only when pk_ok
-	const uint32_t dist = fq_dist(a, b, cnt, kx, ky);
+	const uint32_t dist = cr ? fq_dist_pre(cnt, *cr) : fq_dist(a, b, cnt, kx, ky);
 	if (dist == 0) w[0] = (w[0] & 0xFFFF0000u) | 0x8000u;   // INSIGNIF_BLOCK
 	if (!out_lane) return;
 	const long pb = a.p[b];
@@ -1159,8 +1238,10 @@ __constant__ FqTables kFqDev __attribute__((aligned(16))) = {RIC_SYM_TABLES_INIT
 // its first LDS store -- one memory round trip for the whole staging (a
 // strided loop of load-store pairs pays one per iteration).
 template <int NT>
-__device__ __forceinline__ void fq_stage_tables(const FqArgs& a, int (*s_thres)[16], FqTables& s_F, uint32_t (*s_tpk)[17 * 8])
+__device__ __forceinline__ void fq_stage_tables(const FqArgs& a, int (*s_thres)[16], FqTables& s_F, uint32_t (*s_tpk)[17 * 8],
+                                                int t = -1)
 {
+	const int tid = t >= 0 ? t : (int)threadIdx.x;
 	static_assert(sizeof(FqTables) % 16 == 0, "table words");
 	constexpr int NW = (int)(sizeof(FqTables) / 16);
 	constexpr int PER = (NW + NT - 1) / NT;
@@ -1170,14 +1251,14 @@ __device__ __forceinline__ void fq_stage_tables(const FqArgs& a, int (*s_thres)[
 	uint4 v[PER];
 #pragma unroll
 	for (int k = 0; k < PER; k++) {
-		const int i = threadIdx.x + k * NT;
+		const int i = tid + k * NT;
 		v[k] = src[i < NW ? i : NW - 1];
 	}
-	int th = threadIdx.x < 48 ? a.thres[threadIdx.x / 16][threadIdx.x % 16] : 0;
+	int th = tid < 48 ? a.thres[tid / 16][tid % 16] : 0;
 	uint32_t lo[PT], hi[PT];
 #pragma unroll
 	for (int k = 0; k < PT; k++) {
-		const int i = threadIdx.x + k * NT;
+		const int i = tid + k * NT;
 		const int b = min(i / (17 * 8), 2), c = (i >> 3) % 17, q = i & 7;
 		lo[k] = c + q < 16 ? (uint32_t)a.thres[b][min(c + q, 15)] & 0xFFFFu : 0xFFFFu;
 		hi[k] = c + q + 8 < 16 ? (uint32_t)a.thres[b][min(c + q + 8, 15)] & 0xFFFFu : 0xFFFFu;
@@ -1185,15 +1266,57 @@ __device__ __forceinline__ void fq_stage_tables(const FqArgs& a, int (*s_thres)[
 	uint4* dst = reinterpret_cast<uint4*>(&s_F);
 #pragma unroll
 	for (int k = 0; k < PER; k++) {
-		const int i = threadIdx.x + k * NT;
+		const int i = tid + k * NT;
 		if (i < NW) dst[i] = v[k];
 	}
-	if (threadIdx.x < 48) s_thres[threadIdx.x / 16][threadIdx.x % 16] = th;
+	if (tid < 48) s_thres[tid / 16][tid % 16] = th;
 #pragma unroll
 	for (int k = 0; k < PT; k++) {
-		const int i = threadIdx.x + k * NT;
+		const int i = tid + k * NT;
 		if (i < NTP) s_tpk[i / (17 * 8)][i % (17 * 8)] = lo[k] | (hi[k] << 16);
 	}
+}
+
+// A consumer wave of the ring hand-off (k_fwdq_pc<true>, k_fwdq_pc2<true>):
+// stage this wave's share t of the format tables (the 3 consumer waves stage
+// them together: flags ring[st + 0..2]), then quantise block rows ky0 ..
+// ky0 + nrows - 1 of band b as the producers publish them (ring[0 .. npub-1]
+// count the block rows published, ring[took] those this wave has taken).
+// The children's pRD of the next block row load while this one is quantised:
+// two rows per pass, so the loop-carried registers need no copy (a copy
+// waits for its load).
+__device__ __forceinline__ void fq_consume(const FqArgs& a, int (*s_thres)[16], FqTables& s_F, uint32_t (*s_tpk)[17 * 8],
+                                           uint2 (*buf)[3][4][kLanes], int* ring, int took, int st, int npub, int b,
+                                           int kx, int ky0, int nrows, int lane, bool out_lane, int t, int dbg,
+                                           uint64_t* lt)
+{
+	FqCrd c0 = fq_crd_load(a, b, kx, ky0);
+	fq_stage_tables<192>(a, s_thres, s_F, s_tpk, t);
+	ring_put(ring + st + b, 1);
+	ring_wait_ge(ring + st, 1); ring_wait_ge(ring + st + 1, 1); ring_wait_ge(ring + st + 2, 1);
+	if (lt && lane == 0) lt[3 + b] = __builtin_amdgcn_s_memrealtime();
+	auto row = [&](int j, const FqCrd& cr) {
+		ring_wait_ge(ring, j + 1);
+		if (npub > 1) ring_wait_ge(ring + 1, j + 1);
+		uint2 v[4];
+#pragma unroll
+		for (int r = 0; r < 4; r++) v[r] = buf[j & (kRing - 1)][b][r][lane];
+		ring_put(ring + took, j + 1);            // (after the slot reads completed)
+		if (lt && lane == 0 && j < 20) lt[16 + 20 * b + j] = __builtin_amdgcn_s_memrealtime();
+		if ((dbg & 3) == 2) return;
+		fq_block_regs(a, s_thres[b], s_tpk[b], s_F, b, v, kx, ky0 + j, out_lane, &cr);
+		if (lt && lane == 0 && j < 20) lt[96 + 20 * b + j] = __builtin_amdgcn_s_memrealtime();
+	};
+	int j = 0;
+#pragma unroll 1
+	for (; j + 1 < nrows; j += 2) {
+		const FqCrd c1 = fq_crd_load(a, b, kx, ky0 + j + 1);
+		row(j, c0);
+		c0 = fq_crd_load(a, b, kx, ky0 + j + 2);
+		row(j + 1, c1);
+	}
+	if (j < nrows) row(j, c0);
+	if (lt && lane == 0) lt[6 + b] = __builtin_amdgcn_s_memrealtime();
 }
 
 // grid (ceil(W / 496), ceil(nseg / 4)), one wave per segment
@@ -1248,8 +1371,13 @@ __global__ void __launch_bounds__(256, 4) k_fwdq_pc(FqArgs a, int S, int dbg)
 	__shared__ FqTables s_F __attribute__((aligned(16)));
 	__shared__ uint32_t s_tpk[3][17 * 8];
 	__shared__ uint2 s_buf[ASYNC ? kRing : 2][3][4][kLanes];
-	__shared__ int s_ring[4];
-	if (ASYNC && threadIdx.x < 4) s_ring[threadIdx.x] = 0;     // ordered by the staging barrier
+	// ASYNC: [0] block rows published, [1 + b] taken by consumer b, [4 + b]
+	// consumer b staged its share of the tables
+	__shared__ int s_ring[7];
+	if (ASYNC && threadIdx.x < 7) s_ring[threadIdx.x] = 0;
+	// ASYNC: this is the only barrier; the consumers stage the tables among
+	// themselves while the producer lifts (it does not read them)
+	if constexpr (ASYNC) __syncthreads();
 	// dbg 128 (diagnostics, level 0 only): per-workgroup record of kWgRec u64 --
 	// start realtime (100 MHz), start shader clock, the end realtime of waves
 	// 0-3, producer hw id << 32 | end shader clock of wave 0, workgroup index,
@@ -1274,8 +1402,10 @@ __global__ void __launch_bounds__(256, 4) k_fwdq_pc(FqArgs a, int S, int dbg)
 	if ((dbg & 32) && edge) return;   // timing experiment: interior workgroups only (results invalid)
 	const int nit = m.bottom ? (a.H - y0) / 8 + 1 : S / 8 + 1;
 	auto stage = [&]() {
-		fq_stage_tables<256>(a, s_thres, s_F, s_tpk);
-		__syncthreads();
+		if constexpr (!ASYNC) {
+			fq_stage_tables<256>(a, s_thres, s_F, s_tpk);
+			__syncthreads();
+		}
 	};
 	if (wave == 0) {
 		// the lifting chain is the segment's critical path: it issues ahead
@@ -1292,21 +1422,14 @@ __global__ void __launch_bounds__(256, 4) k_fwdq_pc(FqArgs a, int S, int dbg)
 			                    ASYNC ? s_ring : nullptr);
 		}
 	} else {
-		stage();
 		const int b = wave - 1;
 		const bool out_lane = lane >= 1 && lane <= kLanes - 2 && x < a.W;
 		if constexpr (ASYNC) {
-#pragma unroll 1
-			for (int j = 0; j + 1 < nit; j++) {          // block row j = the producer's iteration j + 1
-				ring_wait_ge(s_ring, j + 1);
-				uint2 buf[4];
-#pragma unroll
-				for (int r = 0; r < 4; r++) buf[r] = s_buf[j & (kRing - 1)][b][r][lane];
-				ring_put(s_ring + 1 + b, j + 1);            // (after the slot reads completed)
-				if ((dbg & 3) == 2) continue;
-				fq_block_regs(a, s_thres[b], s_tpk[b], s_F, b, buf, kx, (y0 >> 3) + j, out_lane);
-			}
+			// block row j = the producer's iteration j + 1
+			fq_consume(a, s_thres, s_F, s_tpk, s_buf, s_ring, 1 + b, 4, 1, b, kx, y0 >> 3, nit - 1, lane, out_lane,
+			           (wave - 1) * 64 + lane, dbg, nullptr);
 		} else {
+			stage();
 #pragma unroll 1
 			for (int it = 0; it < nit; it++) {
 				pc_barrier(dbg, wgt ? wgt + 8 + wave * 2 * kWgIt + 2 * min(it, kWgIt - 1) : nullptr);   // matches the producer's iteration `it`
@@ -1457,14 +1580,22 @@ __global__ void __launch_bounds__(320) k_fwdq_pc2(FqArgs a, int S, int dbg)
 	__shared__ FqTables s_F __attribute__((aligned(16)));
 	__shared__ uint32_t s_tpk[3][17 * 8];
 	__shared__ uint2 s_buf[ASYNC ? kRing : 2][3][4][kLanes];
-	__shared__ int s_ring[5];
-	if (ASYNC && threadIdx.x < 5) s_ring[threadIdx.x] = 0;     // ordered by the staging barrier
+	// ASYNC: [h] block rows published by producer h, [2 + b] taken by consumer
+	// b, [5 + b] consumer b staged its share of the tables
+	__shared__ int s_ring[8];
+	if (ASYNC && threadIdx.x < 8) s_ring[threadIdx.x] = 0;
+	if constexpr (ASYNC) __syncthreads();   // the only barrier (see k_fwdq_pc)
 	const int wgi = blockIdx.y * gridDim.x + blockIdx.x;
 	uint64_t* wgt = ((dbg & 128) && a.wgt && wgi < kWgTraceMax) ? a.wgt + kWgRec * wgi : nullptr;
 	if (wgt && threadIdx.x == 0) {
 		wgt[0] = __builtin_amdgcn_s_memrealtime();
 		wgt[1] = __builtin_amdgcn_s_memtime();
 	}
+	// diagnostics (RIC_LVL_TRACE=level, async form): [0] start, [1 + h]
+	// producer h done, [3 + b] consumer b staged, [6 + b] consumer b done,
+	// [16 + 20 b + j] consumer b took block row j, [96 + 20 b + j] finished it
+	uint64_t* lt = (ASYNC && !(dbg & 128) && a.wgt && wgi < kWgTraceMax) ? a.wgt + kWgRec * wgi : nullptr;
+	if (lt && threadIdx.x == 0) lt[0] = __builtin_amdgcn_s_memrealtime();
 	const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 	const int lane = threadIdx.x & 63;
 	const int strip = (dbg & 4) ? ((dbg & 64) ? 0 : 1) : blockIdx.x, seg = (dbg & 4) ? 2 : blockIdx.y;
@@ -1476,8 +1607,10 @@ __global__ void __launch_bounds__(320) k_fwdq_pc2(FqArgs a, int S, int dbg)
 	const bool edge = SX == 0 || SX - 8 + kLanes * 8 >= a.W || mb.top || mb.bottom;
 	const int nit = mb.bottom ? (a.H - y0) / 8 + 1 : S / 8 + 1;
 	auto stage = [&]() {
-		fq_stage_tables<320>(a, s_thres, s_F, s_tpk);
-		__syncthreads();
+		if constexpr (!ASYNC) {
+			fq_stage_tables<320>(a, s_thres, s_F, s_tpk);
+			__syncthreads();
+		}
 	};
 	if (w < 2) {
 		if (!(dbg & 2048)) __builtin_amdgcn_s_setprio(2);
@@ -1486,25 +1619,18 @@ __global__ void __launch_bounds__(320) k_fwdq_pc2(FqArgs a, int S, int dbg)
 		int* hr = ASYNC ? s_ring : nullptr;
 		if (edge) fq2_producer<true>(a, x, lane, w, y0, mb, S, s_buf, dbg, tr, stage, hr);
 		else fq2_producer<false>(a, x, lane, w, y0, mb, S, s_buf, dbg, tr, stage, hr);
+		if (lt && lane == 0) lt[1 + w] = __builtin_amdgcn_s_memrealtime();
 	} else {
-		stage();
 		const int b = w - 2;
 		const int xc = SX - 8 + lane * 8;                        // the block's 8 image columns
 		const int kx = strip * (kFqStrip / 8) + lane - 1;
 		const bool out_lane = lane >= 1 && lane <= kLanes - 2 && xc < a.W;
 		if constexpr (ASYNC) {
-#pragma unroll 1
-			for (int j = 0; j + 1 < nit; j++) {          // block row j: both halves published
-				ring_wait_ge(s_ring, j + 1);
-				ring_wait_ge(s_ring + 1, j + 1);
-				uint2 buf[4];
-#pragma unroll
-				for (int r = 0; r < 4; r++) buf[r] = s_buf[j & (kRing - 1)][b][r][lane];
-				ring_put(s_ring + 2 + b, j + 1);
-				if ((dbg & 3) == 2) continue;
-				fq_block_regs(a, s_thres[b], s_tpk[b], s_F, b, buf, kx, (y0 >> 3) + j, out_lane);
-			}
+			// block row j: both halves published
+			fq_consume(a, s_thres, s_F, s_tpk, s_buf, s_ring, 2 + b, 5, 2, b, kx, y0 >> 3, nit - 1, lane, out_lane,
+			           b * 64 + lane, dbg, lt);
 		} else {
+			stage();
 #pragma unroll 1
 			for (int it = 0; it < nit; it++) {
 				pc_barrier(dbg, wgt ? wgt + 8 + (w - 1) * 2 * kWgIt + 2 * min(it, kWgIt - 1) : nullptr);
@@ -1586,8 +1712,9 @@ void fq_launch_pc(FqArgs& a, hipStream_t st)
 	static const int onewg = [] { const char* e = getenv("RIC_FQ_ONEWG"); return e ? atoi(e) : 0; }();
 	// RIC_FQ_ONEWG=1: one interior workgroup only (latency of one segment; results invalid)
 	int dbg = fq_pc();
-	a.wgt = nullptr;
-	if ((dbg & 128) && a.high && !(a.wgt = fq_wgtrace())) dbg &= ~128;
+	static const int ltrace = [] { const char* e = getenv("RIC_LVL_TRACE"); return e ? atoi(e) : -1; }();
+	a.wgt = ltrace == a.level ? fq_wgtrace() : nullptr;
+	if ((dbg & 128) && a.high && !a.wgt && !(a.wgt = fq_wgtrace())) dbg &= ~128;
 	// the two-producer form on the coarser levels (their segments are short
 	// and latency-bound); level 0 is VALU-throughput-bound, where the
 	// one-producer form's 8-column rows cost fewer instructions.
@@ -1728,24 +1855,32 @@ __global__ void __launch_bounds__(256) k_fwdq_gen(FqArgs a, GenLL ll, int nseg)
 #pragma unroll
 	for (int b = 0; b < 4; b++) { f.d[b] = reinterpret_cast<TO*>(a.d[b]); f.p[b] = a.p[b]; }
 	f.nseg = nseg; f.vec = a.vec8; f.nofast = 1;
+	// diagnostics (RIC_LVL_TRACE=level): phase stamps of every workgroup
+	const int wgi = blockIdx.y * gridDim.x + blockIdx.x;
+	uint64_t* wgt = (a.wgt && wgi < kWgTraceMax) ? a.wgt + kWgRec * wgi : nullptr;
+	if (wgt && threadIdx.x == 0) wgt[0] = __builtin_amdgcn_s_memrealtime();
 	if (w == 0) {
 		const int X0 = strip * kStripValid - kCols;
 		if constexpr (sizeof(TI) == 2 && sizeof(TO) == 2)
 			fwd97p_seg<kGenRows, false>(f, X0 + lane * kCols, lane, y0);     // packed 16-bit lifting
 		else
 			fwd_seg<CDF97, TI, TO, kGenRows, false>(f, X0 + lane * kCols, lane, y0);
+		if (wgt && lane == 0) wgt[1] = __builtin_amdgcn_s_memrealtime();
 	}
 	fq_stage_tables<256>(a, s_thres, s_F, s_tpk);
+	if (wgt && threadIdx.x == 64) wgt[2] = __builtin_amdgcn_s_memrealtime();
 	// the bands wave 0 wrote are read by the whole workgroup
 	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
 	__syncthreads();
 	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+	if (wgt && threadIdx.x == 0) wgt[3] = __builtin_amdgcn_s_memrealtime();
 	const TO* d[3] = {f.d[0], f.d[1], f.d[2]};
 	const int ky = y0 >> 3;
 	for (int i = threadIdx.x; i < 3 * kGenBlocks; i += 256) {
 		const int b = i / kGenBlocks, kx = strip * kGenBlocks + (i - b * kGenBlocks);
 		if (kx < a.bw[b] && ky < a.bh[b]) gen_block<TO>(a, s_thres[b], s_tpk[b], s_F, d, b, kx, ky);
 	}
+	if (wgt && lane == 0) wgt[4 + w] = __builtin_amdgcn_s_memrealtime();
 	if (ll.on) {
 		// CBand::TSUQ with Thres 0.5 on this segment's LL samples: all loads first
 		constexpr bool SH = sizeof(TO) == 2;
@@ -1770,6 +1905,7 @@ __global__ void __launch_bounds__(256) k_fwdq_gen(FqArgs a, GenLL ll, int nseg)
 				*q[k] = (uint32_t)(v + ll.T0) <= (uint32_t)(2 * ll.T0) ? (TO)0
 				        : (TO)tr<SH>((int)((uint32_t)v * (uint32_t)ll.iQ + 32768u) >> 16);
 		}
+		if (wgt && threadIdx.x == 0) wgt[8] = __builtin_amdgcn_s_memrealtime();
 	}
 }
 
@@ -2337,7 +2473,8 @@ void launch_fwdq_gen_level(const Pyramid& P, int l, const void* src, long sp, in
 {
 	const Level& L = P.L[l];
 	FqArgs a;
-	a.wgt = nullptr;
+	static const int gtrace = [] { const char* e = getenv("RIC_LVL_TRACE"); return e ? atoi(e) : -1; }();
+	a.wgt = gtrace == l ? fq_wgtrace() : nullptr;
 	a.src = (const int16_t*)src; a.sp = sp; a.W = L.w; a.H = L.h;
 	a.vec8 = vec8; a.vec16 = 0; a.nofast = 1; a.high = l == 0; a.level = l;
 	a.pk = !L.is_int && pk_ok(qp.thres[0]) && pk_ok(qp.thres[1]) && pk_ok(qp.thres[2]);

@@ -65,6 +65,63 @@ def wgtrace_summary(ric_amd, path):
     return summ
 
 
+def gentrace_summary(ric_amd):
+    """Phase stamps of the last traced k_fwdq_gen launch (RIC_LVL_TRACE=level):
+    median / max microseconds from each workgroup's start to the end of its
+    lifting, table staging, barrier, block phase and LL TSUQ."""
+    REC = 168
+    n = 8192 * REC
+    buf = np.zeros(n, np.uint64)
+    got = ric_amd.lib().ric_diag_wgtrace(0, buf.ctypes.data, n)
+    r = buf[:max(got, 0)].reshape(-1, REC)[:, :9].astype(np.float64)
+    r = r[r[:, 0] != 0]
+    if not len(r):
+        return None
+    t0 = r[:, 0].min()
+    out = {"wgs": int(len(r)), "start_us": [round(float(np.percentile((r[:, 0] - t0) / 100.0, p)), 2) for p in (50, 100)]}
+    names = ["lift", "stage", "barrier", "blocks_w0", "blocks_w1", "blocks_w2", "blocks_w3", "ll"]
+    for i, nm in enumerate(names, start=1):
+        v = r[:, i]
+        ok = v != 0
+        if ok.any():
+            d = (v[ok] - r[ok, 0]) / 100.0
+            out[nm] = [round(float(np.median(d)), 2), round(float(d.max()), 2)]
+    ends = r[:, 1:9].max(axis=1)
+    out["span_us"] = round(float((ends.max() - t0) / 100.0), 2)
+    return out
+
+
+def pc2trace_summary(ric_amd):
+    """Stamps of the last traced k_fwdq_pc2<true> launch (RIC_LVL_TRACE=1 or 2):
+    medians over workgroups, microseconds from the workgroup's start."""
+    REC = 168
+    n = 8192 * REC
+    buf = np.zeros(n, np.uint64)
+    got = ric_amd.lib().ric_diag_wgtrace(0, buf.ctypes.data, n)
+    r = buf[:max(got, 0)].reshape(-1, REC).astype(np.float64)
+    r = r[r[:, 0] != 0]
+    if not len(r):
+        return None
+    t0 = r[:, 0].min()
+    rel = lambda c: (c - r[:, 0]) / 100.0
+    med = lambda v: round(float(np.median(v)), 2)
+    out = {"wgs": int(len(r)), "start_us": [med((r[:, 0] - t0) / 100.0), round(float((r[:, 0].max() - t0) / 100.0), 2)],
+           "producers_done": [med(rel(r[:, 1])), med(rel(r[:, 2]))],
+           "consumers_staged": [med(rel(r[:, 3 + b])) for b in range(3)],
+           "consumers_done": [med(rel(r[:, 6 + b])) for b in range(3)],
+           "span_us": round(float((r[:, 1:9].max() - t0) / 100.0), 2)}
+    for b in range(3):
+        rows = []
+        for j in range(20):
+            tk, fn = r[:, 16 + 20 * b + j], r[:, 96 + 20 * b + j]
+            ok = (tk != 0) & (fn != 0)
+            if not ok.any():
+                break
+            rows.append([med((tk[ok] - r[ok, 0]) / 100.0), med((fn[ok] - r[ok, 0]) / 100.0)])
+        out["rows_b%d" % b] = rows
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
@@ -73,6 +130,7 @@ def main():
     ap.add_argument("--height", type=int, default=4320)
     ap.add_argument("--codec", action="store_true")
     ap.add_argument("--wgtrace", default="", help="write the level-0 workgroup trace summary (needs RIC_FQ_PC bit 128) to this json")
+    ap.add_argument("--gentrace", action="store_true", help="stamp summary of the level named by RIC_LVL_TRACE")
     a = ap.parse_args()
     import torch
     torch.cuda.init()
@@ -100,6 +158,9 @@ def main():
         out["wavelet_encode_GBps"] = round(9.851 * W * H / (enc * 1e-3) / 1e9, 1)
     if a.wgtrace:
         out["wgtrace"] = wgtrace_summary(ric_amd, a.wgtrace)
+    if a.gentrace:
+        lvl = int(os.environ.get("RIC_LVL_TRACE", "-1"))
+        out["lvltrace"] = pc2trace_summary(ric_amd) if lvl in (1, 2) else gentrace_summary(ric_amd)
     if a.codec:
         c = ric_amd.Codec(W, H, 1)
         dpix = torch.from_numpy(pix).cuda()
