@@ -126,6 +126,7 @@ struct ric_codec {
 	int16_t* d_out = nullptr;         // staging for host int16 output planes
 	long pitch = 0;
 	std::vector<uint8_t> stream;      // coder buffer
+	std::vector<uint8_t> dstream;     // decoder input (2 zero bytes + payload), reused per frame
 };
 
 namespace {
@@ -786,6 +787,7 @@ int ric_codec_create(ric_codec** out, int w, int h, int channels, int device)
 		return RIC_E_HIP;
 	}
 	c->stream.resize((size_t)w * h * channels * 2 + 65536);
+	c->dstream.resize((size_t)w * h * channels + 2 + 16);
 	*out = c;
 	return RIC_OK;
 }
@@ -868,10 +870,14 @@ int ric_codec_decode(ric_codec* c, const uint8_t* ric, size_t len, int dither,
 	// the reference reads W*H*C payload bytes at buf + 2 (ric.cpp:203-205)
 	const size_t npix = (size_t)c->w * c->h * c->channels;
 	const size_t pay = std::min(len - 9, npix);
-	std::vector<uint8_t> buf(pay + 2, 0);
-	memcpy(buf.data() + 2, ric + 9, pay);
+	// (the decoder's look-ahead past the end reads zeros: 16 zeroed tail bytes)
+	if (c->dstream.size() < pay + 2 + 16) c->dstream.resize(pay + 2 + 16);
+	uint8_t* buf = c->dstream.data();
+	buf[0] = buf[1] = 0;
+	memcpy(buf + 2, ric + 9, pay);
+	memset(buf + 2 + pay, 0, 16);
 	Mux m;
-	m.init_decoder(buf.data(), buf.size());
+	m.init_decoder(buf, pay + 2);
 	w->P.set_weight(trans);
 	const long plane = c->pitch * c->h;
 	for (int p = 0; p < c->channels; p++) {

@@ -168,6 +168,9 @@ long hc_decode(const uint8_t* in, long len, int nplanes, int w, int h, int level
 	double t = 0;
 	long off = 0;
 	for (int p = 0; p < nplanes; p++) {
+		// stale data in the bands (the product reuses its pinned arena across
+		// frames): the decoder must clear every coefficient itself
+		std::memset(hp.arena.data(), 0xA5, hp.arena.size());
 		double t0 = now();
 		hp.decode(m);
 		t += now() - t0;
