@@ -381,21 +381,9 @@ void tree_dec(Mux& m, const BandView& b, const BandView& par, bool has_child)
 	const int pdx = par.dx, pdy = par.dy;
 	const C mark = (C)tr<SH>(has_child ? kInsignif : 0);
 	C* band = (C*)b.p;
-	// Clear() (:503) block by block, just before each block is decoded: every
-	// coefficient belongs to exactly one full or edge block, and the band's
-	// cache lines are written once instead of by a separate clearing pass
-	// (a band narrower than one block leaves its even block rows unvisited,
-	// as the reference does: cleared up front instead)
-	const bool per_block = dx >= 4;
-	if (!per_block)
-		for (int j = 0; j < dy; j++) memset(band + j * st, 0, sizeof(C) * dx);
-	auto clear = [&](C* c, int w, int h) {
-		if (per_block)
-			for (int r = 0; r < h; r++) memset(c + r * st, 0, sizeof(C) * w);
-	};
+	for (int j = 0; j < dy; j++) memset(band + j * st, 0, sizeof(C) * dx);   // Clear(), :503
 
 	auto edge = [&](C* c1, int i, int w, int h, P* pp, bool chk_row, int j) {
-		clear(c1 + i, w, h);
 		if (pp && (i >> 1) < pdx && (!chk_row || (j >> 1) < pdy) && pp[i >> 1] == kInsignif) pp[i >> 1] = 0;
 		if (!bord.decode(d, 0)) block_edge_dec<C, HIGH>(d, g, c1 + i, st, w, h);
 	};
@@ -413,7 +401,6 @@ void tree_dec(Mux& m, const BandView& b, const BandView& par, bool has_child)
 			i += bs;
 		}
 		for (; i >= 0 && i + 4 <= dx; i += bs) {
-			clear(c1 + i, 4, 4);
 			int ctx = 15;
 			const int k = i >> 1;
 			if (pp) {
@@ -446,7 +433,6 @@ void tree_dec(Mux& m, const BandView& b, const BandView& par, bool has_child)
 			i += bs;
 		}
 		for (; i >= 0 && i + 4 <= dx; i += bs) {
-			clear(c1 + i, 4, h);
 			if (pp && (j >> 1) < pdy && pp[i >> 1] == kInsignif) pp[i >> 1] = 0;
 			if (!bord.decode(d, 0)) block_edge_dec<C, HIGH>(d, g, c1 + i, st, 4, h);
 		}
