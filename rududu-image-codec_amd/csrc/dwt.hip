@@ -544,7 +544,6 @@ __device__ __forceinline__ void fwd_seg(const FwdArgs<TI, TO>& a, int x, int lan
 			const int xc[4] = {min(max(x, 0), W - 1), min(max(x + 1, 0), W - 1), min(max(x + 2, 0), W - 1),
 			                   min(max(x + 3, 0), W - 1)};
 			constexpr int RB = 16;
-			static_assert(R % 4 == 0, "segment rows");
 #pragma unroll
 			for (int i0 = 0; i0 < R; i0 += RB) {
 				int ev[RB][4];
@@ -670,8 +669,8 @@ __device__ __forceinline__ void fwd97p_seg(const FwdArgs<int16_t, int16_t>& a, i
 	// Input rows y0-4 .. y0+S+3 stream through a ring of 2*PF registers:
 	// the loads of pair p+PF are issued before pair p is lifted, and the loop
 	// body (PF pairs) stays small enough to live in the instruction cache.
-	constexpr int NP = (S + 8) / 2, PF = 4;
-	static_assert(NP % PF == 0, "segment rows");
+	// (S = 2, k_fwdq_gen: the 5 pairs in one pass)
+	constexpr int NP = (S + 8) / 2, PF = NP % 4 == 0 ? 4 : NP;
 	// Border waves: a slot holds the raw elements of clamped columns of a
 	// clamped row, loaded unconditionally and masked when the slot is taken (a
 	// select or a pin right after a load is waited for at once: one memory
@@ -1833,10 +1832,10 @@ __device__ __forceinline__ void gen_block(const FqArgs& a, const int* thr, const
 	}
 }
 
-// One workgroup per 8-row segment of a 248-column strip: wave 0 lifts the
-// segment (its loads are issued before the table staging) while the other
-// waves stage the tables; then all 256 threads quantise the segment's
-// 3 x 31 blocks (one round) and run the coarsest level's LL TSUQ.  The levels
+// One workgroup per 8-row segment of a 248-column strip: each wave lifts two
+// of its rows, then the workgroup stages the tables, and all 256 threads
+// quantise the segment's 3 x 31 blocks (one round) and run the coarsest
+// level's LL TSUQ.  The levels
 // that take this kernel are small and latency-bound: the wide block phase
 // replaces the two dependent rounds of a wave-per-segment form.
 template <typename TI, typename TO>
@@ -1859,14 +1858,17 @@ __global__ void __launch_bounds__(256) k_fwdq_gen(FqArgs a, GenLL ll, int nseg)
 	const int wgi = blockIdx.y * gridDim.x + blockIdx.x;
 	uint64_t* wgt = (a.wgt && wgi < kWgTraceMax) ? a.wgt + kWgRec * wgi : nullptr;
 	if (wgt && threadIdx.x == 0) wgt[0] = __builtin_amdgcn_s_memrealtime();
-	if (w == 0) {
+	// the four waves lift two rows each (own halo rows): a lifting wave is
+	// instruction-latency-bound, and 5 row pairs per wave instead of 8
+	// shorten the chain that the whole segment waits for
+	if (y0 + 2 * w < a.H) {
 		const int X0 = strip * kStripValid - kCols;
 		if constexpr (sizeof(TI) == 2 && sizeof(TO) == 2)
-			fwd97p_seg<kGenRows, false>(f, X0 + lane * kCols, lane, y0);     // packed 16-bit lifting
+			fwd97p_seg<2, false>(f, X0 + lane * kCols, lane, y0 + 2 * w);     // packed 16-bit lifting
 		else
-			fwd_seg<CDF97, TI, TO, kGenRows, false>(f, X0 + lane * kCols, lane, y0);
-		if (wgt && lane == 0) wgt[1] = __builtin_amdgcn_s_memrealtime();
+			fwd_seg<CDF97, TI, TO, 2, false>(f, X0 + lane * kCols, lane, y0 + 2 * w);
 	}
+	if (wgt && lane == 0 && w == 0) wgt[1] = __builtin_amdgcn_s_memrealtime();
 	fq_stage_tables<256>(a, s_thres, s_F, s_tpk);
 	if (wgt && threadIdx.x == 64) wgt[2] = __builtin_amdgcn_s_memrealtime();
 	// the bands wave 0 wrote are read by the whole workgroup
