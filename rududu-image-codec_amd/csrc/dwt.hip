@@ -2036,11 +2036,14 @@ __device__ __forceinline__ void inv_seg(const InvArgs<TB, TL, TO>& a, int x, int
 				ra[i][0] = (int)lo[cD0]; ra[i][1] = (int)lo[cD1];
 			}
 #pragma unroll
-			for (int i = 0; i < R; i += 4)
+			for (int i = 0; i + 4 <= R; i += 4)
 				asm volatile("" : "+v"(ra[i][0]), "+v"(ra[i][1]), "+v"(ra[i][2]), "+v"(ra[i][3]),
 				                  "+v"(ra[i + 1][0]), "+v"(ra[i + 1][1]), "+v"(ra[i + 1][2]), "+v"(ra[i + 1][3]),
 				                  "+v"(ra[i + 2][0]), "+v"(ra[i + 2][1]), "+v"(ra[i + 2][2]), "+v"(ra[i + 2][3]),
 				                  "+v"(ra[i + 3][0]), "+v"(ra[i + 3][1]), "+v"(ra[i + 3][2]), "+v"(ra[i + 3][3]));
+			if constexpr (R % 4 == 2)        // (S = 2: rows R-2, R-1)
+				asm volatile("" : "+v"(ra[R - 2][0]), "+v"(ra[R - 2][1]), "+v"(ra[R - 2][2]), "+v"(ra[R - 2][3]),
+				                  "+v"(ra[R - 1][0]), "+v"(ra[R - 1][1]), "+v"(ra[R - 1][2]), "+v"(ra[R - 1][3]));
 			const bool iD0 = bx >= 0 && bx < dxD, iD1 = bx + 1 >= 0 && bx + 1 < dxD;
 			const bool iH0 = bx >= 0 && bx < dxH, iH1 = bx + 1 >= 0 && bx + 1 < dxH;
 #pragma unroll
@@ -2169,8 +2172,8 @@ __device__ __forceinline__ void inv97p_seg(const InvArgs<int16_t, int16_t, int16
 	};
 	// band rows of image rows y0-4 .. y0+S+3 (D/H feed even image rows, V/LL
 	// odd ones) stream through a ring of PF row pairs, as in fwd97p_seg
-	constexpr int NP = (S + 8) / 2, PF = 4;
-	static_assert(NP % PF == 0, "segment rows");
+	// (S = 2: the 5 pairs in one pass)
+	constexpr int NP = (S + 8) / 2, PF = NP % 4 == 0 ? 4 : NP;
 	// Ring slots: FAST, the (D, H, V, LL) words of one pair; border waves,
 	// the raw elements at clamped band columns, masked when consumed.  Every
 	// refill is unconditional, from a wave-uniform clamped band row (the
@@ -2182,7 +2185,7 @@ __device__ __forceinline__ void inv97p_seg(const InvArgs<int16_t, int16_t, int16
 	// FAST: two rings, alternate iterations (prefetch depth two iterations);
 	// a pass of the loop runs two iterations, so the ring registers are the
 	// same at the back-edge and no copy waits for a load in flight
-	constexpr int DEPTH = FAST ? 2 : 1;
+	constexpr int DEPTH = FAST && NP / PF > 1 ? 2 : 1;
 	Slot ring[DEPTH][PF];
 	int yl = y0 - 4;
 	const int byl = FAST ? min((y0 + S + 3) >> 1, (H >> 1) - 1) : 0;
@@ -2336,10 +2339,14 @@ template <typename T>
 int seg_rows(int H)
 {
 	static const int forced = [] { const char* e = getenv("RIC_DWT_S"); return e ? atoi(e) : 0; }();
-	if (forced == 8 || forced == 16 || ((forced == 32 || forced == 64) && sizeof(T) == 2)) return forced;
+	if (forced == 2 || forced == 8 || forced == 16 || ((forced == 32 || forced == 64) && sizeof(T) == 2)) return forced;
 	// (16 rather than 32 rows on the 8K level: two rounds of waves balance
-	// better, k_inv level 0 44 -> 39 us)
-	return H >= 1024 ? 16 : 8;
+	// better, k_inv level 0 44 -> 39 us; 2 rows on the small levels, whose
+	// waves are latency-bound: 5 row pairs per wave instead of 8)
+	// (tuning knobs RIC_DWT_S16 / RIC_DWT_S2: the height thresholds)
+	static const int t16 = [] { const char* e = getenv("RIC_DWT_S16"); return e ? atoi(e) : 2048; }();
+	static const int t2 = [] { const char* e = getenv("RIC_DWT_S2"); return e ? atoi(e) : 600; }();
+	return H >= t16 ? 16 : H >= t2 ? 8 : 2;
 }
 // tuning knob: RIC_DWT_NOFAST=1 runs every wave on the checked path
 int dbg_nofast()
@@ -2370,6 +2377,7 @@ void fwd_launch(const Level& L, const void* src, long sp, char* arena, int vec, 
 		if (S == 32) { fwd_launch_s<TRANS, TI, TO, 32>(L, src, sp, arena, vec, st); return; }
 	}
 	if (S == 16) fwd_launch_s<TRANS, TI, TO, 16>(L, src, sp, arena, vec, st);
+	else if (S == 2) fwd_launch_s<TRANS, TI, TO, 2>(L, src, sp, arena, vec, st);
 	else fwd_launch_s<TRANS, TI, TO, 8>(L, src, sp, arena, vec, st);
 }
 
@@ -2399,6 +2407,7 @@ void inv_launch(const Level& L, const Band& lls, char* arena, void* out, long po
 		if (S == 32) { inv_launch_s<TRANS, TB, TO, 32>(L, lls, arena, out, po, q, st); return; }
 	}
 	if (S == 16) inv_launch_s<TRANS, TB, TO, 16>(L, lls, arena, out, po, q, st);
+	else if (S == 2) inv_launch_s<TRANS, TB, TO, 2>(L, lls, arena, out, po, q, st);
 	else inv_launch_s<TRANS, TB, TO, 8>(L, lls, arena, out, po, q, st);
 }
 
