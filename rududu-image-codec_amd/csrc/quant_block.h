@@ -229,6 +229,13 @@ __device__ __forceinline__ int tsuq_full_pk(uint32_t (&w)[8], int Q, int iQ, int
 		accB = accB - as_v2u(as_w(mnz) & ~as_w(mlt));                              // + 1 per quantised value
 	}
 	const uint32_t cnt = (uint32_t)accB.x + accB.y;
+	// no RD candidate in any active lane of the wave (smooth areas): nothing
+	// to sort, no survivor -- the result below would leave w and the count as
+	// they are
+	uint32_t anyk = 0;
+#pragma unroll
+	for (int j = 0; j < 8; j++) anyk |= as_w(key[j]);
+	if (__builtin_amdgcn_ballot_w64(anyk != 0) == 0) return (int)cnt;
 	// sort layout: R[p] = (key p, key p + 8)
 	v2u R[8];
 #pragma unroll
