@@ -68,6 +68,9 @@ __device__ __forceinline__ int tsuq_full(int (&v)[16], int Q, int iQ, const int*
 		cnt += (!dz && !cand) ? 1 : 0;
 		ncand += cand ? 1 : 0;
 	}
+	// no RD candidate in any active lane of the wave: no survivor, v and the
+	// count stay as they are (same skip as tsuq_full_pk)
+	if (__builtin_amdgcn_ballot_w64(ncand != 0) == 0) return cnt;
 	uint32_t s[16];
 #pragma unroll
 	for (int i = 0; i < 16; i++) s[i] = key[i];
