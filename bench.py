@@ -1,24 +1,32 @@
 #!/usr/bin/env python3
-"""bench.py -- .ric encode+decode throughput on synthetic 8K grayscale frames.
+"""bench.py -- .ric encode+decode throughput on synthetic frames (MI355X).
 
-Workload (BASELINE.json configs[2]): 7680x4320 8-bit gray,
-5-level integer 9/7 wavelet, q=9, full .ric encode (DWT, RD quantiser,
-zerotree + range coder) followed by the full decode (entropy decode,
-dequantiser, inverse DWT, 8-bit output), bit-exact with the reference.
+Workloads (BASELINE.json configs):
+  C3 (default)  7680x4320 8-bit gray, 5-level integer 9/7, q=9: full .ric
+                encode (DWT, RD quantiser, zerotree records, range coder)
+                followed by the full decode (entropy decode, fused TSUQi +
+                inverse DWT, 8-bit output), bit-exact with the reference.
+                Each rank codes its own frames (weak scaling).
+  C5            64 independent 4096x4096 gray frames per step in total,
+                frame f on rank f mod N (strong scaling).
+  C4            one 7680x4320 RGB image as 2x2 tiles of 3840x2160, tile
+                (tx, ty) on rank 2*ty + tx (round robin when N < 4), the four
+                tile streams gathered to rank 0 into an RTL1 container.
 
-One step = every rank encodes and decodes its batch of frames (default 64
-per GPU, handed out dynamically to 16 host coder threads).  Frames are
-independent .ric streams, so ranks shard frames with no data-path collective
-("scaling": "weak"); host worker threads run the serial range coder of
-different frames concurrently while the GPU stages of all frames share the
-device.  Inputs are resident in HBM before the timed region; outputs (decoded
-frames) land in HBM.
+One step = every rank encodes and decodes its frames through ric_batch: the
+frames of a group (`--slots`, default one per host thread) go through every
+GPU level as one launch (blockIdx.z = frame), a native pool of host coder
+threads runs the serial range coder of different frames, and the GPU stages
+of one group overlap the host coding of the previous one.  Inputs are
+resident in HBM before the timed region; decoded frames land in HBM.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--threads T]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload C3|C4|C5]
+                    [--frames F] [--threads T] [--slots S]
 
 Multi-GPU: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 """
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -31,6 +39,9 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "rududu-image-codec_amd"))
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak (spec)
+# a reference C3 (8K gray q9) encode makes 19.24 M
+# codeBin and 19.26 M bitsCode calls -- the serial stage's event count
+C3_EVENTS = 19.24e6 + 19.26e6
 
 
 def wavelet_bytes(W, H, levels=5, level_chg=1):
@@ -76,47 +87,112 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=0, help="frames per GPU per step (default: 8 per host thread)")
-    ap.add_argument("--threads", type=int, default=0, help="host coder threads per GPU (default 16)")
-    ap.add_argument("--width", type=int, default=7680)
-    ap.add_argument("--height", type=int, default=4320)
+    ap.add_argument("--workload", default="C3", choices=["C3", "C4", "C5"])
+    ap.add_argument("--frames", type=int, default=0,
+                    help="C3: frames per GPU per step (default 8 per host thread); C5: frames per step in total (64)")
+    ap.add_argument("--batch", type=int, default=0, help="alias of --frames")
+    ap.add_argument("--threads", type=int, default=0, help="host coder threads per GPU (default: this rank's CPU share)")
+    ap.add_argument("--slots", type=int, default=0, help="frames per GPU launch group (default: --threads)")
     ap.add_argument("--q", type=int, default=9)
     ap.add_argument("--trans", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-gather", action="store_true", help="N>1: skip the per-step stream gather to rank 0")
-    ap.add_argument("--cpu-frames", type=int, default=16)
+    ap.add_argument("--no-split", action="store_true", help="skip the encode-only / decode-only timing")
     return ap.parse_args()
 
 
-def cpu_baseline(w, h, q, trans, frames, threads):
-    """Reference CPU path (oracle/_ref, the reference library compiled from its
-    own sources; the clean-room port if absent), timed on this host's cores:
-    `frames` independent 8K encode+decode round trips on `threads` threads."""
+def host_info():
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count()
+    return {"nproc": os.cpu_count(), "affinity_cpus": aff, "model": model,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+
+
+def default_threads(world):
+    """This rank's share of the host: OMP_NUM_THREADS when the launcher sets
+    it (16 per GPU on the GPU boxes), else the affinity mask split over the
+    ranks of the node."""
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        return int(omp)
+    hi = host_info()
+    return max(1, min(32, (hi["affinity_cpus"] or 1) // max(world, 1)))
+
+
+def cpu_baseline(W, H, q, trans, threads, per_thread=2):
+    """The reference CPU path (oracle/_ref: the reference library compiled
+    from its own sources; the clean-room port if absent), on this host:
+    (i) one stream on one core (latency), (ii) `threads` independent streams
+    on `threads` threads (throughput); encode and decode timed separately,
+    `per_thread` frames per thread."""
     sys.path.insert(0, REPO)
     from oracle import oracle as O
     chk = O.ref() or O.port()
     kind = "reference" if O.ref() is not None else "port"
     import ric_amd
-    imgs = [ric_amd.synth(w, h, 1, 1000 + i) for i in range(frames)]
+    chk.decode_ric(chk.encode_ric(ric_amd.synth(64, 48, 1, 0), q, trans))   # lazy statics (init_lut) first
+    mpx = W * H / 1e6
 
-    def work(i):
-        r = chk.encode_ric(imgs[i], q, trans)
-        chk.decode_ric(r)
+    def run(nthreads):
+        imgs = [[ric_amd.synth(W, H, 1, 1000 + k * per_thread + i) for i in range(per_thread)] for k in range(nthreads)]
+        rics = [[None] * per_thread for _ in range(nthreads)]
 
-    t0 = time.perf_counter()
-    ths = []
-    for k in range(threads):
-        def run(k=k):
-            for i in range(k, frames, threads):
-                work(i)
-        ths.append(threading.Thread(target=run))
-        ths[-1].start()
-    for t in ths:
-        t.join()
-    dt = time.perf_counter() - t0
-    return {"value": round(frames * w * h / 1e6 / dt, 2), "unit": "Mpixel/s", "cores": threads, "kind": kind,
-            "sample": "%d independent %dx%d gray q%d encode+decode round trips on %d host threads (%.1f s wall)"
-                      % (frames, w, h, q, threads, dt)}
+        def enc(k):
+            for i in range(per_thread):
+                rics[k][i] = chk.encode_ric(imgs[k][i], q, trans)
+
+        def dec(k):
+            for i in range(per_thread):
+                chk.decode_ric(rics[k][i])
+
+        out = {}
+        for name, fn in (("encode", enc), ("decode", dec)):
+            ths = [threading.Thread(target=fn, args=(k,)) for k in range(nthreads)]
+            t0 = time.perf_counter()
+            for t in ths:
+                t.start()
+            for t in ths:
+                t.join()
+            out[name] = time.perf_counter() - t0
+        n = nthreads * per_thread
+        return {"encode_mpix_s": round(n * mpx / out["encode"], 2), "decode_mpix_s": round(n * mpx / out["decode"], 2),
+                "roundtrip_mpix_s": round(n * mpx / (out["encode"] + out["decode"]), 2),
+                "wall_s": round(out["encode"] + out["decode"], 2)}
+
+    lat = run(1)
+    tput = run(threads)
+    return {"value": tput["roundtrip_mpix_s"], "unit": "Mpixel/s", "cores": threads, "kind": kind,
+            "sample": "%d frames of %dx%d gray q%d per thread, encode then decode, on 1 thread (latency) and on %d "
+                      "threads (throughput; value); %.1f s + %.1f s wall" % (per_thread, W, H, q, threads,
+                                                                          lat["wall_s"], tput["wall_s"]),
+            "latency_1core": lat, "throughput": tput, "host": host_info()}
+
+
+def workload_frames(a, rank, world, threads):
+    """(W, H, channels, [(global index, synth frame, crop)], scaling)"""
+    if a.workload == "C3":
+        W, H = 7680, 4320
+        n = a.frames or a.batch or 8 * threads
+        return W, H, 1, [(rank * n + i, rank * n + i, None) for i in range(n)], "weak"
+    if a.workload == "C5":
+        W, H = 4096, 4096
+        total = a.frames or a.batch or 64
+        return W, H, 1, [(f, f, None) for f in range(rank, total, world)], "strong"
+    import shard
+    rects = shard.tile_rects(7680, 4320)
+    mine = [(i, 0, r) for i, r in enumerate(rects) if i % world == rank]
+    return 3840, 2160, 3, mine, "strong"
 
 
 def main():
@@ -132,9 +208,8 @@ def main():
     local = local % max(ndev, 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    # one process per GPU; barrier, max-over-ranks timing and the final stream
-    # gather go over RCCL ("nccl" is RCCL on ROCm; RIC_BENCH_BACKEND=gloo for a
-    # CPU-side rehearsal)
+    # barrier, max-over-ranks timing and the stream gather go over RCCL
+    # ("nccl" is RCCL on ROCm; RIC_BENCH_BACKEND=gloo for a CPU-side rehearsal)
     backend = os.environ.get("RIC_BENCH_BACKEND", "nccl")
     cdev = dev if backend == "nccl" else torch.device("cpu")
     if world > 1:
@@ -147,74 +222,44 @@ def main():
 
     import ric_amd
     import shard
-    W, H = a.width, a.height
-    threads = a.threads or 16
-    # 8 frames per host coder thread: the threads drift apart after their
-    # first frame, so their exclusive GPU sections stop queueing behind one
-    # another, and the idle tail at the end of a step (threads waiting for the
-    # last frames) shrinks with the frames per thread (one box, 16 threads:
-    # 16 frames per step 1490-1750 Mpix/s, 64: 2023, 128: 2072, 256: 2089)
-    batch = a.batch or 8 * threads
-    threads = min(threads, batch)
+    threads = a.threads or default_threads(world)
+    W, H, CH, mine, scaling = workload_frames(a, rank, world, threads)
+    nfr = len(mine)
+    slots = max(1, min(a.slots or threads, max(nfr, 1)))
 
     # synthetic frames, uploaded to HBM before timing
-    frames = []
-    for i in range(batch):
-        host = ric_amd.synth(W, H, 1, rank * batch + i)
+    frames, rgb = [], None
+    for (_, f, crop) in mine:
+        if crop is None:
+            host = ric_amd.synth(W, H, CH, f)
+        else:
+            if rgb is None:
+                rgb = ric_amd.synth(7680, 4320, 3, 0)
+            _, _, x0, y0, w, h = crop
+            host = np.ascontiguousarray(rgb[:, y0:y0 + h, x0:x0 + w])
         frames.append(torch.from_numpy(host).to(dev))
-    outs = [torch.empty((1, H, W), dtype=torch.uint8, device=dev) for _ in range(batch)]
+    outs = [torch.empty((CH, H, W), dtype=torch.uint8, device=dev) for _ in range(nfr)]
     torch.cuda.synchronize()
 
-    codecs = [ric_amd.Codec(W, H, 1, device=local) for _ in range(threads)]
-    sizes = [0] * batch
-    errors = []
-
-    # frames are handed out dynamically (next free frame), so the host coder
-    # threads drift apart after their first frame and their exclusive GPU
-    # sections interleave with the other threads' host work
-    next_frame = [0]
-    lock = threading.Lock()
-
-    def run_frames(k):
-        c = codecs[k]
-        try:
-            while True:
-                with lock:
-                    i = next_frame[0]
-                    next_frame[0] += 1
-                if i >= batch:
-                    break
-                ric = c.compress(frames[i], q=a.q, trans=a.trans, on_device=True)
-                sizes[i] = len(ric)
-                streams[i] = ric
-                c.decompress(ric, pix_out=outs[i])
-        except Exception as e:  # surfaced after join
-            errors.append(e)
-
+    b = ric_amd.Batch(W, H, CH, slots=slots, threads=threads, device=local) if nfr else None
     gather = world > 1 and not a.no_gather
-    streams = [b""] * batch
     gathered = [0]
 
     def step():
-        next_frame[0] = 0
-        ths = [threading.Thread(target=run_frames, args=(k,)) for k in range(threads)]
-        for t in ths:
-            t.start()
-        for t in ths:
-            t.join()
-        if errors:
-            raise errors[0]
+        if b is not None:
+            b.roundtrip(frames, outs, q=a.q, trans=a.trans)
         if gather:
             # the path's one exchange: every rank's .ric streams to rank 0
             # (SURVEY.md §8(e)); rank 0 keeps them on the device
+            streams = [b.stream(i) for i in range(nfr)] if b is not None else []
             got = shard.gather_streams(streams, dist, device=cdev, to_host=False)
             if rank == 0:
                 gathered[0] = int(sum(int(s[1:1 + int(s[0])].sum()) for s in got[1]))
 
     for _ in range(a.warmup):
         step()
-    for c in codecs:
-        c.prof_enable(True)
+    if b is not None:
+        b.prof_enable(True)
 
     barrier()
     torch.cuda.synchronize()
@@ -229,43 +274,107 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt[0])
 
-    # stage timers (HIP events on each codec's stream, summed over codecs)
-    prof = {}
-    for c in codecs:
-        for k, (ms, n) in c.prof_read().items():
-            s = prof.setdefault(k, [0.0, 0])
-            s[0] += ms
-            s[1] += n
-    stage_ms = {k: round(v[0] / v[1], 4) for k, v in prof.items() if v[1]}
+    # ---- verification (outside the timed region): this rank's first frame
+    # against the oracle, rank 0's against the reference's golden SHA-256
+    verified, vnote = None, "skipped"
+    if not a.no_verify:
+        ok = True
+        notes = []
+        if b is not None:
+            sys.path.insert(0, REPO)
+            from oracle import oracle as O
+            r0 = b.stream(0)
+            host0 = frames[0].cpu().numpy()
+            chk = O.port()
+            ok &= r0 == chk.encode_ric(host0, a.q, a.trans)
+            ok &= bool(np.array_equal(outs[0].cpu().numpy(), chk.decode_ric(r0)[0]))
+            notes.append("frame %d vs oracle port" % mine[0][0])
+            gold = json.load(open(os.path.join(REPO, "tests", "golden", "golden.json")))["large"]
+            want = None
+            if a.q == 9 and a.trans == 0:
+                if a.workload == "C3" and mine[0][1] == 0:
+                    want = "C3_7680x4320_q9"
+                elif a.workload == "C5" and mine[0][1] in (0, 1):
+                    want = {0: "C2_4096x4096_q9", 1: "C5_frame1_4096x4096_q9"}[mine[0][1]]
+                elif a.workload == "C4":
+                    tx, ty = mine[0][2][0], mine[0][2][1]
+                    want = "C4_tile_%d_%d" % (tx, ty)
+            if want:
+                e = [g for g in gold if g["name"] == want][0]
+                ok &= hashlib.sha256(r0).hexdigest() == e["ric_sha256"]
+                ok &= hashlib.sha256(outs[0].cpu().numpy().tobytes()).hexdigest() == e["decoded_sha256"]
+                notes.append("%s sha256" % want)
+        if world > 1:
+            t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=cdev)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            ok = bool(int(t[0]))
+        verified, vnote = bool(ok), "; ".join(notes)
+        if not ok:
+            print(json.dumps({"error": "bench output mismatch", "rank": rank, "checked": vnote}), file=sys.stderr)
+            sys.exit(3)
 
-    # roofline of the dominant GPU kernel: the level-0 launch of the fused
-    # forward 9/7 DWT + RD quantiser + zerotree records (dwt.hip k_fwdq_pc).
-    # Algorithmic bytes = SURVEY.md §8(d)'s per-unit figures for the work that
-    # one launch does: the level-0 DWT (4 B/px) plus the level-0 quantiser
-    # (read + write every s16 coefficient, 4 B/coef, + 8 B per 4x4 block).
+    # ---- stage timers (HIP events on the batch stream; host clocks)
+    prof = b.prof_read() if b is not None else {}
+    per_frame = {k: v[0] / v[1] for k, v in prof.items() if v[1]}
+    per_launch = {k: v[0] / v[2] for k, v in prof.items() if v[2]}
     bm = wavelet_bytes(W, H)
+    nlev = len(bm["dwt"])
     l0_bytes = bm["dwt"][0] + bm["quant"][0]
-    t_fwd0 = stage_ms.get("fwd_l0")
-    achieved = l0_bytes / (t_fwd0 * 1e-3) / 1e9 if t_fwd0 else None
+    fwd = [per_frame.get("fwd_l%d" % l) for l in range(nlev)]
+    inv = [per_frame.get("inv_l%d" % l) for l in range(nlev)]
+    enc_bytes = sum(bm["dwt"]) + sum(bm["quant"]) + bm["ll"]
+    dec_bytes = sum(bm["dwt"]) + sum(bm["deq"])
+    enc_ms = sum(fwd) if all(fwd) else None
+    dec_ms = sum(inv) if all(inv) else None
+    t_l0 = per_frame.get("fwd_l0")
+    achieved = l0_bytes / (t_l0 * 1e-3) / 1e9 if t_l0 else None
     traffic = None
-    pmc = os.path.join(REPO, "profiles", "pmc_fwd_l0.json")
+    pmc = os.path.join(REPO, "profiles", "pmc_fwd_l0_batch.json")
     if os.path.exists(pmc):
         try:
             p = json.load(open(pmc))
-            if p.get("kernel", "").startswith("k_fwdq_pc"):
-                traffic = p.get("hbm_bytes_per_launch")
+            if p.get("kernel", "").startswith("k_fwdq_pc_z") and p.get("W") == W and p.get("H") == H:
+                traffic = p.get("hbm_bytes_per_frame")
         except Exception:
             traffic = None
-    # the whole GPU wavelet encode (every forward level + quantiser + LL TSUQ):
-    # the §8(d) DWT + quant model, 326.8 MB at C3
-    enc_bytes = sum(bm["dwt"]) + sum(bm["quant"]) + bm["ll"]
-    enc_gpu = (stage_ms.get("fwd", 0) + stage_ms.get("quant", 0)) or None
-    # the GPU decode stages: dequantiser (r + w) + inverse DWT (= forward bytes)
-    dec_bytes = sum(bm["dwt"]) + sum(bm["deq"])
-    dec_gpu = (stage_ms.get("dequant", 0) + stage_ms.get("inv", 0)) or None
 
-    total_px = world * batch * W * H * a.steps
-    value = total_px / 1e6 / dt
+    # ---- encode-only and decode-only rates of the same path (rank 0, after timing)
+    split = None
+    if rank == 0 and b is not None and not a.no_split:
+        streams = [b.stream(i) for i in range(nfr)]
+        torch.cuda.synchronize()
+        te = time.perf_counter()
+        for g in range(0, nfr, slots):
+            b.compress(frames[g:g + slots], a.q, a.trans, on_device=True)
+        te = time.perf_counter() - te
+        td = time.perf_counter()
+        for g in range(0, nfr, slots):
+            b.decompress(streams[g:g + slots], pix_out=outs[g:g + slots])
+        torch.cuda.synchronize()
+        td = time.perf_counter() - td
+        mpx = nfr * W * H / 1e6
+        split = {"encode_mpix_s": round(mpx / te, 2), "decode_mpix_s": round(mpx / td, 2),
+                 "note": "rank 0, %d frames in groups of %d, groups not pipelined" % (nfr, slots)}
+
+    total_px = sum_px = nfr * W * H
+    if world > 1:
+        t = torch.tensor([total_px], dtype=torch.float64, device=cdev)
+        dist.all_reduce(t)
+        sum_px = float(t[0])
+    value = sum_px * a.steps / 1e6 / dt
+    wl = {"C3": "C3: 7680x4320 gray, 5-level cdf97, q=%d, .ric encode+decode round trip, bit-exact" % a.q,
+          "C5": "C5: %d x 4096x4096 gray frames per step, 5-level cdf97, q=%d, encode+decode, frame f on rank f mod N"
+                % (a.frames or a.batch or 64, a.q),
+          "C4": "C4: 7680x4320 RGB as 2x2 tiles of 3840x2160, q=%d, encode+decode, tile (tx,ty) on rank 2ty+tx, "
+                "RCCL gather of the tile streams" % a.q}[a.workload]
+    hs = None
+    if a.workload == "C3" and a.q == 9 and a.trans == 0 and per_frame.get("host_enc"):
+        hs = {"events_per_frame": C3_EVENTS,
+              "encode_Mevents_s_per_thread": round(C3_EVENTS / per_frame["host_enc"] / 1e3, 1),
+              "decode_Mevents_s_per_thread": round(C3_EVENTS / per_frame["host_dec"] / 1e3, 1),
+              "note": "reference codeBin + bitsCode call count of a C3 frame (SURVEY.md §6) over this path's host "
+                      "coder time per frame; the survey's replay of those events through CMuxCodec alone: 216 "
+                      "Mevents/s on one core"}
     out = {
         "metric": "encode+decode Mpixel/s on 8K gray, 5-level wavelet; % HBM roofline",
         "value": round(value, 2),
@@ -275,34 +384,43 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": round(dt / a.steps * 1e3, 2),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "int16",
         "data": "synthetic (SURVEY.md §8(d) generator), resident in HBM",
-        "config": {"workload": "C3: %dx%d gray, 5-level cdf97, q=%d, .ric encode+decode round trip, bit-exact"
-                               % (W, H, a.q),
-                   "frames_per_gpu_per_step": batch, "host_coder_threads_per_gpu": threads,
-                   "parallelism": "frames sharded over %d GPU(s)" % world},
+        "config": {"workload": wl, "frames_per_gpu_per_step": nfr, "frames_per_launch": slots,
+                   "host_coder_threads_per_gpu": threads, "parallelism": "frames sharded over %d GPU(s)" % world},
+        "verified": verified,
+        "verified_against": vnote,
         "roofline": {"bound": "hbm",
-                     "kernel": "k_fwdq_pc level 0 (fused forward 9/7 DWT + RD quantiser + block records)",
+                     "kernel": "k_fwdq_pc_z level 0 (fused forward 9/7 DWT + RD quantiser + block records, "
+                               "%d frames per launch)" % slots,
                      "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                     "traffic": traffic, "algorithmic_bytes_per_launch": l0_bytes,
-                     "avg_launch_ms": t_fwd0},
-        "gpu_wavelet_encode": _frac(enc_gpu, enc_bytes),
-        "gpu_wavelet_decode": _frac(dec_gpu, dec_bytes),
-        "stage_ms": stage_ms,
-        "bytes_per_frame": int(np.mean(sizes)),
+                     "traffic": traffic * slots if traffic else None,
+                     "algorithmic_bytes_per_launch": l0_bytes * slots,
+                     "avg_launch_ms": round(per_launch["fwd_l0"], 4) if "fwd_l0" in per_launch else None},
+        "gpu_wavelet_encode": _frac(enc_ms, enc_bytes),
+        "gpu_wavelet_decode": _frac(dec_ms, dec_bytes),
+        "per_level_us_per_frame": {"fwd": [round(x * 1e3, 2) if x else None for x in fwd],
+                                   "inv": [round(x * 1e3, 2) if x else None for x in inv]},
+        "stage_ms_per_frame": {k: round(v, 4) for k, v in per_frame.items()},
+        "bytes_per_frame": int(np.mean([len(b.stream(i)) for i in range(nfr)])) if b is not None else None,
     }
+    if hs:
+        out["host_serial"] = hs
+    if split:
+        out["gpu_path_split"] = split
     if gather:
         out["gather"] = {"backend": backend, "bytes_to_rank0_per_step": gathered[0]}
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         try:
-            out["cpu_baseline"] = cpu_baseline(W, H, a.q, a.trans, a.cpu_frames, min(16, a.cpu_frames))
+            out["cpu_baseline"] = cpu_baseline(W, H, a.q, a.trans, threads)   # gray frames of the workload's size
         except Exception as e:
             out["cpu_baseline"] = {"error": str(e)}
     if rank == 0:
         print(json.dumps(out))
+    del b
     if world > 1:
         dist.destroy_process_group()
 

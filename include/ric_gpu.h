@@ -129,6 +129,42 @@ int ric_codec_encode(ric_codec* c, const uint8_t* pix, int pix_on_device, int q,
  * pix_on_device, may be NULL). */
 int ric_codec_decode(ric_codec* c, const uint8_t* ric, size_t len, int dither,
                      uint8_t* pix_out, int16_t* planes_out, int pix_on_device);
+/* ----------------------------------------------------------- ric_batch */
+/* CompressImage / DecompressImage (src/ric/ric.cpp:123-251) over batches of
+ * frames of one geometry -- the serving form of ric_codec, byte-identical to
+ * it.  The frames of a group (at most `slots`) are coded together: every GPU
+ * stage is one launch per level over the whole group (the small coarse levels
+ * of one frame leave the chip mostly idle; a group fills it), and a native
+ * pool of `threads` host threads runs the serial coder of different frames in
+ * parallel.  Two sets of slots: ric_batch_roundtrip overlaps the GPU stages of
+ * one group with the host coding of the previous one.  One call at a time per
+ * object. */
+typedef struct ric_batch ric_batch;
+int ric_batch_create(ric_batch** out, int w, int h, int channels, int slots, int threads, int device);
+void ric_batch_destroy(ric_batch* b);
+/* n <= slots frames: pix[i] = channels planes of w*h bytes (device pointers
+ * if pix_on_device); the .ric file of frame i is written to out[i] (cap[i]
+ * bytes, host), its size to len[i]. */
+int ric_batch_encode(ric_batch* b, const uint8_t* const* pix, int n, int pix_on_device, int q, int trans,
+                     uint8_t* const* out, const size_t* cap, size_t* len);
+/* n <= slots .ric files (host bytes) of this geometry and one transform;
+ * frame i's pixels to pix_out[i] (device if pix_on_device).  RIC_E_STREAM
+ * when a stream ran past its end (the frames are still written). */
+int ric_batch_decode(ric_batch* b, const uint8_t* const* ric, const size_t* len, int n, uint8_t* const* pix_out,
+                     int pix_on_device);
+/* encode then decode n frames (any n, device pixels in and out; .ric files
+ * to host out[i]), in groups of `slots` frames, pipelined. */
+int ric_batch_roundtrip(ric_batch* b, const uint8_t* const* pix, int n, int q, int trans, uint8_t* const* out,
+                        const size_t* cap, size_t* len, uint8_t* const* pix_out);
+/* Stage timers of the batch (no reference counterpart): 0 pixel conversion
+ * in, 1..8 forward level 0..7 (fused DWT + quantiser + records), 9 D2H of
+ * bands + records, 10 host encode, 11 host decode, 12 H2D of the bands,
+ * 13..20 inverse level 0..7 (fused TSUQi), 21 pixel conversion out.  ms are
+ * sums; frames = frames covered; launches = GPU launches (host: frames). */
+#define RIC_BATCH_STAGES 22
+int ric_batch_prof_enable(ric_batch* b, int on);
+int ric_batch_prof_read(ric_batch* b, double* ms, long* frames, long* launches, int n);
+
 /* .ric header fields (src/ric/ric.cpp:114-121, 187-200) */
 int ric_read_header(const uint8_t* ric, size_t len, int* w, int* h, int* channels, int* q, int* trans);
 /* src/ric/ric.cpp:42-49 */
@@ -150,6 +186,12 @@ ric_wavelet* ric_codec_wavelet(ric_codec* c);
  * XCC_ID << 32 | workgroup index, then per role (producer, D, H, V) 20
  * (barrier arrival, departure) realtime pairs; copies up to n u64. */
 int ric_diag_wgtrace(int device, uint64_t* out, int n);
+/* Fault injection (tests): while on, the consumer waves of the fused level
+ * kernels' LDS ring hand-off wait for a block row that never comes; the wait
+ * gives up, raises the device status word, and the call that syncs next
+ * (CodeBand, Quantize, TransformQuantize, the codec's encode) returns
+ * RIC_E_HIP instead of a corrupt result. */
+int ric_diag_fault(int on);
 /* SURVEY.md §8(d) synthetic image: channels planes of w*h bytes */
 void ric_synth_image(int w, int h, int channels, int frame, uint8_t* out);
 

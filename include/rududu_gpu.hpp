@@ -15,8 +15,9 @@
 //   * CMuxCodec takes an explicit capacity (the reference has none) and throws
 //     rududu::RicError on overflow or on any HIP failure -- there is no CPU
 //     fallback;
-//   * after CodeBand the bands hold the buildTree state (quantised
-//     sign-magnitude + INSIGNIF markers) rather than the scan's final state.
+//   * after CodeBand the bands hold the reference's post-CodeBand state
+//     (quantised sign-magnitude, the markers the zerotree scan consumes
+//     cleared), so TSUQi / TransformI after CodeBand match the reference.
 #pragma once
 
 #include <cstdint>

@@ -99,6 +99,20 @@ class Checker:
         assert n > 0
         return out[:n].tobytes()
 
+    def closed_loop(self, plane, levels, lc, trans, quant, lam, dq):
+        """Transform -> CodeBand -> TSUQi(dq) -> TransformI on one int16 plane
+        (src/lib/rududucodec.cpp:67-74): (reconstructed plane, bands after TSUQi)."""
+        plane = np.ascontiguousarray(plane, np.int16)
+        h, w = plane.shape
+        lay = self.layout(w, h, levels, lc)
+        bands = np.zeros(int((lay[:, 0] * lay[:, 1]).sum()), np.int32)
+        out = np.zeros((h, w), np.int16)
+        f = self._f("closed_loop")
+        f.restype = _L
+        f.argtypes = [_P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P]
+        f(_ptr(plane), w, h, levels, lc, trans, quant, lam, dq, _ptr(out), _ptr(bands))
+        return out, split_bands(bands, lay)
+
     def decode_ric(self, ric, dither=False):
         b = np.frombuffer(ric, np.uint8).copy()
         dims = np.zeros(5, np.int32)

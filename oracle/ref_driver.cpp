@@ -127,6 +127,28 @@ long ricref_bands(const int16_t* img, int w, int h, int levels, int lc, int tran
 	return dump_all(wav, out);
 }
 
+// The video driver's closed loop on one plane (src/lib/rududucodec.cpp:67-74):
+// Transform, CodeBand, TSUQi on the bands CodeBand left, TransformI.  Dumps
+// the bands after TSUQi (bands_out, optional) and the reconstructed plane.
+long ricref_closed_loop(const int16_t* img, int w, int h, int levels, int lc, int trans, int quant, int lambda,
+                        int dq, int16_t* plane_out, int32_t* bands_out)
+{
+	const size_t n = (size_t)w * h;
+	std::vector<short> buf(img, img + n);
+	CWavelet2D wav(w, h, levels, lc);
+	wav.SetWeight((rududu::trans)trans);
+	wav.Transform(buf.data(), w, (rududu::trans)trans);
+	std::vector<unsigned char> s(n * 4 + 4096);
+	CMuxCodec codec(s.data(), 0);
+	wav.CodeBand(&codec, quant, lambda);
+	wav.TSUQi(dq);
+	long nb = bands_out ? dump_all(wav, bands_out) : 0;
+	std::fill(buf.begin(), buf.end(), 0);
+	wav.TransformI(buf.data() + n, w, (rududu::trans)trans);
+	std::copy(buf.begin(), buf.end(), plane_out);
+	return nb;
+}
+
 // Encodes nplanes int16 planes (coded in the given order) into one stream.
 // Returns the full coder buffer length (endCoding() - buf, including the two
 // leading bytes that the .ric file drops), or -needed if cap is too small.

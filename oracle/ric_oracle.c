@@ -1236,6 +1236,30 @@ long ricor_inverse(const int32_t* bands, int w, int h, int levels, int lc, int t
 	return 0;
 }
 
+/* The video driver's closed loop on one plane (src/lib/rududucodec.cpp:67-74):
+ * Transform, CodeBand (the bands keep the scan's final sign-magnitude state),
+ * TSUQi on that state, TransformI.  Dumps the bands after TSUQi (bands_out,
+ * optional) and the reconstructed plane. */
+long ricor_closed_loop(const int16_t* img, int w, int h, int levels, int lc, int trans, int quant, int lambda,
+                       int dq, int16_t* plane_out, int32_t* bands_out)
+{
+	once();
+	pyr_t p; pyr_init(&p, w, h, levels, lc); pyr_weights(&p, trans);
+	int32_t* x = malloc(sizeof(int32_t) * (size_t)w * h);
+	for (long i = 0; i < (long)w * h; i++) x[i] = img[i];
+	pyr_forward(&p, x, trans);
+	uint8_t* s = calloc((size_t)w * h * 4 + 4096, 1);
+	mux_t m; mux_enc_init(&m, s);
+	code_bands(&p, &m, quant, lambda);
+	free(s);
+	pyr_tsuqi(&p, dq);
+	long n = bands_out ? dump(&p, bands_out) : 0;
+	pyr_inverse(&p, trans, x);
+	for (long i = 0; i < (long)w * h; i++) plane_out[i] = (int16_t)x[i];
+	free(x); pyr_free(&p);
+	return n;
+}
+
 /* src/ric/ric.cpp:42-49 */
 short ricor_quants(int idx)
 {

@@ -33,6 +33,10 @@ long ricor_decode_ric(const uint8_t* ric, long len, int dither_on, int16_t* plan
 /* inverse transform only: bands (canonical order, already dequantised) -> plane */
 long ricor_inverse(const int32_t* bands, int w, int h, int levels, int lc, int trans,
                    int16_t* plane_out);
+/* Transform -> CodeBand -> TSUQi(dq) -> TransformI on one plane
+ * (src/lib/rududucodec.cpp:67-74); bands_out (optional) after TSUQi */
+long ricor_closed_loop(const int16_t* img, int w, int h, int levels, int lc, int trans, int quant, int lambda,
+                       int dq, int16_t* plane_out, int32_t* bands_out);
 /* SURVEY.md §8(d) synthetic generator: channels planes of w*h bytes */
 void ricor_synth(int w, int h, int channels, int frame, uint8_t* out);
 short ricor_quants(int idx);

@@ -1,0 +1,702 @@
+// batch.cpp -- ric_batch (include/ric_gpu.h): CompressImage / DecompressImage
+// (src/ric/ric.cpp:123-251) over a batch of frames of one geometry.
+//
+// The frames of a group sit in fixed-stride slots of one device arena, one
+// pinned host mirror and one set of coding planes, so every GPU stage is one
+// launch per level over the whole group (blockIdx.z = frame, dwt.hip *_z
+// kernels): the small coarse levels that leave most of the chip idle for a
+// single frame fill it for a batch.  A native pool of host threads runs the
+// serial coder (entropy.cpp / encoder.cpp / decoder.cpp) of different frames
+// in parallel.  Two sets of slots let ric_batch_roundtrip overlap the GPU
+// stages of one group with the host coding of the previous one.
+//
+// Output is byte-identical to ric_codec (the same kernels' arithmetic and the
+// same host coder), i.e. to the reference.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <functional>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "ric_gpu.h"
+#include "ric_types.h"
+#include "ric_kernels.h"
+#include "ric_image.h"
+#include "entropy.h"
+#include "codec_params.h"
+
+using namespace ric;
+
+namespace {
+
+bool bfail(hipError_t e, const char* what)
+{
+	if (e == hipSuccess) return false;
+	set_last_error(std::string(what) + ": " + hipGetErrorString(e));
+	return true;
+}
+#define BCHK(x) do { if (bfail((x), #x)) return RIC_E_HIP; } while (0)
+
+double now_ms()
+{
+	return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// A fixed pool of host coder threads with a FIFO of tasks.
+class Pool {
+public:
+	explicit Pool(int n)
+	{
+		for (int i = 0; i < n; i++) th_.emplace_back([this] { run(); });
+	}
+	~Pool()
+	{
+		{
+			std::lock_guard<std::mutex> g(mu_);
+			stop_ = true;
+		}
+		cv_.notify_all();
+		for (auto& t : th_) t.join();
+	}
+	void submit(std::function<void()> f)
+	{
+		{
+			std::lock_guard<std::mutex> g(mu_);
+			q_.push_back(std::move(f));
+		}
+		cv_.notify_one();
+	}
+	int size() const { return (int)th_.size(); }
+
+private:
+	void run()
+	{
+		for (;;) {
+			std::function<void()> f;
+			{
+				std::unique_lock<std::mutex> lk(mu_);
+				cv_.wait(lk, [this] { return stop_ || !q_.empty(); });
+				if (q_.empty()) return;
+				f = std::move(q_.front());
+				q_.pop_front();
+			}
+			f();
+		}
+	}
+	std::vector<std::thread> th_;
+	std::deque<std::function<void()>> q_;
+	std::mutex mu_;
+	std::condition_variable cv_;
+	bool stop_ = false;
+};
+
+// counts down the tasks of one group
+class Latch {
+public:
+	void reset(int n) { std::lock_guard<std::mutex> g(mu_); left_ = n; }
+	void done()
+	{
+		std::lock_guard<std::mutex> g(mu_);
+		if (--left_ == 0) cv_.notify_all();
+	}
+	void wait()
+	{
+		std::unique_lock<std::mutex> lk(mu_);
+		cv_.wait(lk, [this] { return left_ <= 0; });
+	}
+
+private:
+	std::mutex mu_;
+	std::condition_variable cv_;
+	int left_ = 0;
+};
+
+// Stage timers: GPU stages by event pairs on the batch's stream (harvested
+// after the call's final sync), host stages by a steady clock per frame.
+// Stage order: pix_in, fwd level 0..7, d2h, host_enc, host_dec, h2d,
+// inv level 0..7, pix_out (RIC_BATCH_STAGES).
+enum { B_PIXIN = 0, B_FWD = 1, B_D2H = 9, B_HENC = 10, B_HDEC = 11, B_H2D = 12, B_INV = 13, B_PIXOUT = 21, B_COUNT = 22 };
+
+struct BProf {
+	bool on = false;
+	struct Rec { int stage; hipEvent_t a, b; int frames; };
+	std::vector<Rec> pending;
+	std::vector<hipEvent_t> spare;
+	double ms[B_COUNT] = {};
+	long frames[B_COUNT] = {}, launches[B_COUNT] = {};
+	std::mutex mu;
+
+	hipEvent_t ev()
+	{
+		if (!spare.empty()) { hipEvent_t e = spare.back(); spare.pop_back(); return e; }
+		hipEvent_t e = nullptr;
+		(void)hipEventCreate(&e);
+		return e;
+	}
+	// brackets one GPU stage of `frames` frames
+	struct Span { BProf* p; int stage, frames; hipEvent_t a = nullptr; hipStream_t st; };
+	Span begin(int stage, int nfr, hipStream_t st)
+	{
+		Span s{this, stage, nfr, nullptr, st};
+		if (!on) return s;
+		s.a = ev();
+		(void)hipEventRecord(s.a, st);
+		return s;
+	}
+	void end(const Span& s)
+	{
+		if (!s.a) return;
+		hipEvent_t b = ev();
+		(void)hipEventRecord(b, s.st);
+		pending.push_back({s.stage, s.a, b, s.frames});
+	}
+	void harvest()   // after a stream sync
+	{
+		for (auto& r : pending) {
+			float t = 0;
+			if (hipEventElapsedTime(&t, r.a, r.b) == hipSuccess) {
+				ms[r.stage] += t; frames[r.stage] += r.frames; launches[r.stage]++;
+			}
+			spare.push_back(r.a); spare.push_back(r.b);
+		}
+		pending.clear();
+	}
+	void host(int stage, double t)
+	{
+		if (!on) return;
+		std::lock_guard<std::mutex> g(mu);
+		ms[stage] += t; frames[stage]++; launches[stage]++;
+	}
+	void reset()
+	{
+		for (int i = 0; i < B_COUNT; i++) { ms[i] = 0; frames[i] = 0; launches[i] = 0; }
+	}
+	void destroy()
+	{
+		for (auto& r : pending) { spare.push_back(r.a); spare.push_back(r.b); }
+		pending.clear();
+		for (hipEvent_t e : spare) (void)hipEventDestroy(e);
+		spare.clear();
+	}
+};
+
+}  // namespace
+
+struct ric_batch {
+	int device = 0, w = 0, h = 0, channels = 1, slots = 0;
+	Pyramid P;
+	size_t astride = 0, hstride = 0, pstride = 0;   // bytes per slot: device arena, host mirror, coding planes
+	long pitch = 0;                                // coding plane row pitch (elements)
+	char* d_arena = nullptr;                       // 2 * slots slots
+	char* h_arena = nullptr;
+	int16_t* d_planes = nullptr;
+	uint8_t* d_stage = nullptr;                    // host pixels in / out, w*h*channels per slot
+	hipStream_t st = nullptr;
+	ZArgs zf[2][kMaxLevels], zi[2][kMaxLevels];    // per set: forward / inverse argument arrays
+	std::vector<Mux> enc, dec;                     // per slot
+	Pool* pool = nullptr;
+	BProf prof;
+
+	int nslot() const { return 2 * slots; }
+	char* arena(int s) const { return d_arena + (size_t)s * astride; }
+	char* harena(int s) const { return h_arena + (size_t)s * hstride; }
+	int16_t* plane(int s, int p) const { return d_planes + (size_t)s * (pstride / 2) + (size_t)p * pitch * h; }
+	uint8_t* stage(int s) const { return d_stage + (size_t)s * w * h * channels; }
+	BandView view(int s, const Band& B) const
+	{
+		BandView v;
+		v.p = harena(s) + B.off; v.pitch = B.pitch; v.dx = B.dx; v.dy = B.dy; v.is_int = B.is_int;
+		return v;
+	}
+};
+
+namespace {
+
+int set_dev(int device) { return bfail(hipSetDevice(device), "hipSetDevice") ? RIC_E_HIP : RIC_OK; }
+
+int quant_of(int q, int p) { return q ? quants(q + 20 + (p ? 8 : 0)) : 0; }    // Y, then chroma +C_Q_BOOST (ric.cpp:164-168)
+int lambda_of(int q, int p) { return q ? quants(q + 13 + (p ? 8 : 0)) : 0; }
+
+// The GPU half of CompressImage for plane p of n frames of set `set`: pixel
+// conversion (p == 0), every forward level + quantiser + block records as one
+// launch per level over the group, then the bands + records of every frame
+// to the host mirrors (one strided copy).  pix: device pixels of each frame.
+int gpu_encode_plane(ric_batch* b, int set, int n, int p, const uint8_t* const* pix, int q, int trans)
+{
+	Pyramid& P = b->P;
+	const int s0 = set * b->slots;
+	if (p == 0) {
+		auto sp = b->prof.begin(B_PIXIN, n, b->st);
+		for (int i = 0; i < n; i++) launch_pix_in(pix[i], b->plane(s0 + i, 0), b->w, b->h, b->pitch, b->channels, q, b->st);
+		b->prof.end(sp);
+	}
+	const int quant = quant_of(q, p), lambda = lambda_of(q, p);
+	P.set_weight(trans);
+	bool fused[kMaxLevels] = {};
+	bool ll_done = false;
+	int qin = quant;
+	for (int l = 0; l < P.nlev; l++) {
+		ZFrames fr;
+		fr.arena = b->arena(s0); fr.astride = b->astride; fr.nz = n;
+		if (l == 0) {
+			fr.src = b->plane(s0, p); fr.sstride = b->pstride; fr.sp = b->pitch;
+		} else {
+			const Band& LL = P.L[l - 1].b[BL];
+			fr.src = b->arena(s0) + LL.off; fr.sstride = b->astride; fr.sp = LL.pitch;
+		}
+		// coding planes: 64-element row pitch, 256-byte aligned slots
+		const int vec8 = 1, vec16 = 1;
+		QuantParams qp = level_qp(P, l, qin, lambda);
+		const int mode = fwdq_mode(P.L[l], trans, qp, vec16);
+		fused[l] = mode != FQ_NONE;
+		auto sp = b->prof.begin(B_FWD + std::min(l, 7), n, b->st);
+		if (mode == FQ_PACKED) {
+			if (launch_fwdq_level_z(P, l, fr, vec8, vec16, qp, b->zf[set][l], b->st)) return RIC_E_HIP;
+		} else if (mode == FQ_GENERIC) {
+			const bool coarsest = l + 1 == P.nlev;
+			int llQ = 0, lliQ = 0, llT0 = 0;
+			if (coarsest) { ll_params(P, quant, llQ, lliQ, llT0); ll_done = true; }
+			if (launch_fwdq_gen_level_z(P, l, fr, vec8, qp, coarsest, lliQ, llT0, b->zf[set][l], b->st)) return RIC_E_HIP;
+		} else {
+			// unfused levels (5/3, Haar): the per-frame kernels
+			for (int i = 0; i < n; i++) {
+				char* ar = b->arena(s0 + i);
+				launch_fwd_level(P.L[l], (const char*)fr.src + i * fr.sstride, fr.sp, ar, trans, vec8, b->st);
+				launch_quant_level(P, l, qp, ar, b->st);
+			}
+		}
+		b->prof.end(sp);
+	}
+	for (int i = 0; i < n; i++) {
+		char* ar = b->arena(s0 + i);
+		if (!ll_done) {
+			int Q, iQ, T0;
+			ll_params(P, quant, Q, iQ, T0);
+			launch_quant_ll(P, Q, iQ, T0, ar, b->st);
+		}
+		for (int l = 0; l < P.nlev; l++)
+			if (!fused[l] || (l + 1 < P.nlev && !fused[l + 1]))
+				launch_blocks_level(P, l, !fused[l], l + 1 < P.nlev && !fused[l + 1], ar, b->st);
+	}
+	BCHK(hipGetLastError());
+	auto sp = b->prof.begin(B_D2H, n, b->st);
+	BCHK(hipMemcpy2DAsync(b->harena(s0), b->hstride, b->arena(s0), b->astride, P.b_end, n, hipMemcpyDeviceToHost, b->st));
+	b->prof.end(sp);
+	return RIC_OK;
+}
+
+// The GPU half of DecompressImage for plane p of n frames of set `set`: the
+// host-decoded bands to the device (one strided copy), then every inverse
+// level with the fused TSUQi factors of each frame, as one launch per level.
+int gpu_decode_plane(ric_batch* b, int set, int n, int p, const int* qs, int trans)
+{
+	Pyramid& P = b->P;
+	const int s0 = set * b->slots;
+	auto sp = b->prof.begin(B_H2D, n, b->st);
+	BCHK(hipMemcpy2DAsync(b->arena(s0), b->astride, b->harena(s0), b->hstride, P.a_end, n, hipMemcpyHostToDevice, b->st));
+	b->prof.end(sp);
+	P.set_weight(trans);
+	std::vector<int> qf(4 * n);
+	for (int l = P.nlev - 1; l >= 0; l--) {
+		const Level& L = P.L[l];
+		ZFrames fr;
+		fr.arena = b->arena(s0); fr.astride = b->astride; fr.nz = n;
+		int out_int;
+		if (l == 0) {
+			fr.out = b->plane(s0, p); fr.ostride = b->pstride; fr.po = b->pitch; out_int = 0;
+		} else {
+			const Band& LL = P.L[l - 1].b[BL];
+			fr.out = b->arena(s0) + LL.off; fr.ostride = b->astride; fr.po = LL.pitch; out_int = LL.is_int;
+		}
+		for (int i = 0; i < n; i++) {
+			const int quant = quant_of(qs[i], p);
+			int* f = &qf[4 * i];
+			if (quant) {
+				f[0] = tsuqi_factor(L.b[BD], quant); f[1] = tsuqi_factor(L.b[BH], quant); f[2] = tsuqi_factor(L.b[BV], quant);
+				f[3] = l + 1 == P.nlev ? tsuqi_factor(L.b[BL], quant) : 1;
+			} else {
+				f[0] = f[1] = f[2] = f[3] = 1;    // lossless: no TSUQi (ric.cpp:213)
+			}
+		}
+		auto si = b->prof.begin(B_INV + std::min(l, 7), n, b->st);
+		if (launch_inv_level_z(L, L.b[BL], fr, out_int, trans, qf.data(), b->zi[set][l], b->st)) return RIC_E_HIP;
+		b->prof.end(si);
+	}
+	BCHK(hipGetLastError());
+	return RIC_OK;
+}
+
+// pixel output of n frames of set `set` (after every plane's inverse)
+int gpu_pix_out(ric_batch* b, int set, int n, const int* qs, uint8_t* const* pix_out, int on_device)
+{
+	const int s0 = set * b->slots;
+	auto sp = b->prof.begin(B_PIXOUT, n, b->st);
+	for (int i = 0; i < n; i++) {
+		if (!pix_out[i]) continue;
+		uint8_t* dst = on_device ? pix_out[i] : b->stage(s0 + i);
+		launch_pix_out(b->plane(s0 + i, 0), b->pitch, b->w, b->h, b->channels, qs[i], dst, nullptr, b->st);
+	}
+	b->prof.end(sp);
+	BCHK(hipGetLastError());
+	if (!on_device)
+		for (int i = 0; i < n; i++)
+			if (pix_out[i])
+				BCHK(hipMemcpyAsync(pix_out[i], b->stage(s0 + i), (size_t)b->w * b->h * b->channels, hipMemcpyDeviceToHost, b->st));
+	return RIC_OK;
+}
+
+// Host coder of plane p of the frame in slot s.  Encode: the .ric file is
+// written in place into out (the coder buffer starts at out + 7, so the
+// payload lands at out + 9 and the two dropped leading coder bytes are
+// overwritten by the header at the end).
+int host_encode_plane(ric_batch* b, int s, int p, int q, int trans, uint8_t* out, size_t cap, size_t* len)
+{
+	Pyramid& P = b->P;
+	Mux& m = b->enc[s];
+	if (p == 0) {
+		if (cap < 16) return RIC_E_CAPACITY;
+		m.init_encoder(out + 7, cap - 7, 0);
+	}
+	int32_t* status = (int32_t*)(b->harena(s) + P.status_off);
+	if (*status) {
+		*status = 0;
+		set_last_error("fused level kernel: LDS ring hand-off timed out (device status word set; output discarded)");
+		return RIC_E_HIP;
+	}
+	const double t0 = now_ms();
+	pred_encode(m, b->view(s, P.coarsest_ll()));
+	for (int l = P.nlev - 1; l >= 0; l--) {
+		const int order[3] = {BV, BH, BD};
+		for (int k = 0; k < 3; k++) {
+			const Band& B = P.L[l].b[order[k]];
+			const uint64_t* rec = (const uint64_t*)(b->harena(s) + P.rec_off[l][order[k]]);
+			const uint8_t* pin = l + 1 < P.nlev ? (const uint8_t*)(b->harena(s) + P.pin_off[l][order[k]]) : nullptr;
+			tree_encode_records_fast(m, rec, pin, b->view(s, B), l == 0);
+		}
+	}
+	if (p + 1 == b->channels) {
+		uint8_t* e = m.end_coding();
+		if (m.overflow()) return RIC_E_CAPACITY;
+		const size_t n = (size_t)(e - (out + 7));
+		*len = 9 + n - 2;
+		memcpy(out, "RUD2", 4);
+		out[4] = b->w & 255; out[5] = (b->w >> 8) & 255; out[6] = b->h & 255; out[7] = (b->h >> 8) & 255;
+		out[8] = (uint8_t)((q & 31) | ((b->channels == 3) << 5) | ((trans & 3) << 6));
+	}
+	b->prof.host(B_HENC, now_ms() - t0);
+	return RIC_OK;
+}
+
+// Host decoder of plane p of one .ric file into the host mirror of slot s
+// (CWavelet2D::DecodeBand, src/lib/wavelet2d.cpp:179-222).
+int host_decode_plane(ric_batch* b, int s, int p, const uint8_t* ric, size_t len)
+{
+	Pyramid& P = b->P;
+	Mux& m = b->dec[s];
+	if (p == 0) {
+		// the reference reads W*H*C payload bytes (ric.cpp:203-205)
+		const size_t pay = std::min(len - 9, (size_t)b->w * b->h * b->channels);
+		m.init_decoder_payload(ric + 9, pay);
+	}
+	const double t0 = now_ms();
+	pred_decode(m, b->view(s, P.coarsest_ll()));
+	for (int l = P.nlev - 1; l >= 0; l--) {
+		const int order[3] = {BV, BH, BD};
+		for (int k = 0; k < 3; k++) {
+			BandView par;
+			if (l + 1 < P.nlev) par = b->view(s, P.L[l + 1].b[order[k]]);
+			tree_decode_fast(m, b->view(s, P.L[l].b[order[k]]), par, l == 0, l > 0);
+		}
+	}
+	b->prof.host(B_HDEC, now_ms() - t0);
+	return m.overflow() ? RIC_E_STREAM : RIC_OK;
+}
+
+// keeps the first error of a group's tasks (RIC_E_STREAM only if nothing worse)
+struct FirstErr {
+	std::atomic<int> rc{RIC_OK};
+	std::mutex mu;
+	std::string msg;
+	void put(int r)
+	{
+		if (r == RIC_OK) return;
+		std::lock_guard<std::mutex> g(mu);
+		const int cur = rc.load();
+		if (cur == RIC_OK || (cur == RIC_E_STREAM && r != RIC_E_STREAM)) {
+			rc.store(r);
+			msg = ric_last_error();    // the worker thread's message
+		}
+	}
+	int get()
+	{
+		const int r = rc.load();
+		if (r != RIC_OK && r != RIC_E_STREAM) set_last_error(msg);
+		return r;
+	}
+};
+
+int check_header(ric_batch* b, const uint8_t* ric, size_t len, int* q, int* trans)
+{
+	int w, h, ch;
+	int rc = ric_read_header(ric, len, &w, &h, &ch, q, trans);
+	if (rc) return rc;
+	if (w != b->w || h != b->h || ch != b->channels || *trans > 2) return RIC_E_ARG;
+	return RIC_OK;
+}
+
+// after a failed call: clear every slot's device status word (a fused
+// kernel's ring timeout, see host_encode_plane) so the next call starts clean
+void clear_status(ric_batch* b)
+{
+	for (int s = 0; s < b->nslot(); s++)
+		(void)hipMemsetAsync(b->arena(s) + b->P.status_off, 0, sizeof(int32_t), b->st);
+	(void)hipStreamSynchronize(b->st);
+}
+
+// device pixel pointers of n frames, staging host pixels through the slots
+int stage_pixels(ric_batch* b, int set, int n, const uint8_t* const* pix, int on_device, std::vector<const uint8_t*>& dpix)
+{
+	dpix.resize(n);
+	for (int i = 0; i < n; i++) {
+		if (on_device) { dpix[i] = pix[i]; continue; }
+		uint8_t* d = b->stage(set * b->slots + i);
+		BCHK(hipMemcpyAsync(d, pix[i], (size_t)b->w * b->h * b->channels, hipMemcpyHostToDevice, b->st));
+		dpix[i] = d;
+	}
+	return RIC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ric_batch_create(ric_batch** out, int w, int h, int channels, int slots, int threads, int device)
+{
+	if (!out || w < 8 || h < 8 || w > 65535 || h > 65535 || (channels != 1 && channels != 3) || slots < 1 || slots > 1024 ||
+	    threads < 1 || threads > 1024)
+		return RIC_E_ARG;
+	*out = nullptr;
+	if (set_dev(device)) return RIC_E_HIP;
+	ric_batch* b = new ric_batch;
+	b->device = device; b->w = w; b->h = h; b->channels = channels; b->slots = slots;
+	b->P.build(w, h, 5, 1);     // WAV_LEVELS 5, level_chg 1 (ric.cpp:159)
+	b->P.set_weight(CDF97);
+	auto up = [](size_t v, size_t a) { return (v + a - 1) / a * a; };
+	b->astride = up(b->P.arena_bytes, 1 << 16);
+	b->hstride = up(b->P.b_end, 4096);
+	b->pitch = ((long)w + 63) / 64 * 64;
+	b->pstride = up((size_t)b->pitch * h * channels * 2, 1 << 16);
+	const size_t ns = (size_t)b->nslot();
+	if (bfail(hipMalloc(&b->d_arena, ns * b->astride), "hipMalloc batch arena") ||
+	    bfail(hipHostMalloc(&b->h_arena, ns * b->hstride, 0), "hipHostMalloc batch mirror") ||
+	    bfail(hipMalloc(&b->d_planes, ns * b->pstride), "hipMalloc batch planes") ||
+	    bfail(hipMalloc(&b->d_stage, ns * (size_t)w * h * channels), "hipMalloc batch staging") ||
+	    bfail(hipStreamCreateWithFlags(&b->st, hipStreamNonBlocking), "hipStreamCreate") ||
+	    bfail(hipMemsetAsync(b->d_arena, 0, ns * b->astride, b->st), "hipMemset batch arena") ||
+	    bfail(hipStreamSynchronize(b->st), "hipStreamSynchronize")) {
+		ric_batch_destroy(b);
+		return RIC_E_HIP;
+	}
+	memset(b->h_arena, 0, ns * b->hstride);
+	b->enc = std::vector<Mux>(ns);
+	b->dec = std::vector<Mux>(ns);
+	b->pool = new Pool(threads);
+	*out = b;
+	return RIC_OK;
+}
+
+void ric_batch_destroy(ric_batch* b)
+{
+	if (!b) return;
+	delete b->pool;
+	(void)hipSetDevice(b->device);
+	if (b->st) (void)hipStreamSynchronize(b->st);
+	for (int s = 0; s < 2; s++)
+		for (int l = 0; l < kMaxLevels; l++) { zargs_free(b->zf[s][l]); zargs_free(b->zi[s][l]); }
+	b->prof.destroy();
+	if (b->d_arena) (void)hipFree(b->d_arena);
+	if (b->h_arena) (void)hipHostFree(b->h_arena);
+	if (b->d_planes) (void)hipFree(b->d_planes);
+	if (b->d_stage) (void)hipFree(b->d_stage);
+	if (b->st) (void)hipStreamDestroy(b->st);
+	delete b;
+}
+
+int ric_batch_encode(ric_batch* b, const uint8_t* const* pix, int n, int pix_on_device, int q, int trans,
+                     uint8_t* const* out, const size_t* cap, size_t* len)
+{
+	if (!b || !pix || !out || !cap || !len || n < 0 || n > b->slots || q < 0 || q > 31 || trans < 0 || trans > 2)
+		return RIC_E_ARG;
+	if (n == 0) return RIC_OK;
+	if (set_dev(b->device)) return RIC_E_HIP;
+	std::vector<const uint8_t*> dpix;
+	int rc = stage_pixels(b, 0, n, pix, pix_on_device, dpix);
+	if (rc) return rc;
+	for (int p = 0; p < b->channels; p++) {
+		rc = gpu_encode_plane(b, 0, n, p, dpix.data(), q, trans);
+		if (rc) return rc;
+		BCHK(hipStreamSynchronize(b->st));
+		FirstErr err;
+		Latch done;
+		done.reset(n);
+		for (int i = 0; i < n; i++)
+			b->pool->submit([=, &err, &done] {
+				err.put(host_encode_plane(b, i, p, q, trans, out[i], cap[i], &len[i]));
+				done.done();
+			});
+		done.wait();
+		rc = err.get();
+		if (rc == RIC_E_HIP) clear_status(b);
+		if (rc) return rc;
+	}
+	b->prof.harvest();
+	return RIC_OK;
+}
+
+int ric_batch_decode(ric_batch* b, const uint8_t* const* ric, const size_t* len, int n, uint8_t* const* pix_out,
+                     int pix_on_device)
+{
+	if (!b || !ric || !len || !pix_out || n < 0 || n > b->slots) return RIC_E_ARG;
+	if (n == 0) return RIC_OK;
+	if (set_dev(b->device)) return RIC_E_HIP;
+	std::vector<int> qs(n), ts(n);
+	for (int i = 0; i < n; i++) {
+		int rc = check_header(b, ric[i], len[i], &qs[i], &ts[i]);
+		if (rc) return rc;
+		if (ts[i] != ts[0]) return RIC_E_ARG;    // one transform per call (one kernel per level)
+	}
+	int result = RIC_OK;
+	for (int p = 0; p < b->channels; p++) {
+		FirstErr err;
+		Latch done;
+		done.reset(n);
+		for (int i = 0; i < n; i++)
+			b->pool->submit([=, &err, &done] {
+				err.put(host_decode_plane(b, i, p, ric[i], len[i]));
+				done.done();
+			});
+		done.wait();
+		const int rc = err.get();
+		if (rc && rc != RIC_E_STREAM) return rc;
+		if (rc) result = rc;
+		int r2 = gpu_decode_plane(b, 0, n, p, qs.data(), ts[0]);
+		if (r2) return r2;
+		// the next plane's host decode rewrites the mirrors the copy reads
+		BCHK(hipStreamSynchronize(b->st));
+	}
+	int rc = gpu_pix_out(b, 0, n, qs.data(), pix_out, pix_on_device);
+	if (rc) return rc;
+	BCHK(hipStreamSynchronize(b->st));
+	b->prof.harvest();
+	return result;
+}
+
+int ric_batch_roundtrip(ric_batch* b, const uint8_t* const* pix, int n, int q, int trans, uint8_t* const* out,
+                        const size_t* cap, size_t* len, uint8_t* const* pix_out)
+{
+	if (!b || !pix || !out || !cap || !len || !pix_out || n < 0 || q < 0 || q > 31 || trans < 0 || trans > 2)
+		return RIC_E_ARG;
+	if (n == 0) return RIC_OK;
+	if (set_dev(b->device)) return RIC_E_HIP;
+	const int S = b->slots;
+	const int G = (n + S - 1) / S;
+	if (b->channels != 1) {
+		// colour: plane-sequential groups (each plane's host coding needs the
+		// previous plane's bands out of the mirror first)
+		std::vector<size_t> l2(S);
+		for (int g = 0; g < G; g++) {
+			const int f0 = g * S, m = std::min(S, n - f0);
+			int rc = ric_batch_encode(b, pix + f0, m, 1, q, trans, out + f0, cap + f0, len + f0);
+			if (rc) return rc;
+			std::vector<const uint8_t*> rics(out + f0, out + f0 + m);
+			rc = ric_batch_decode(b, rics.data(), len + f0, m, pix_out + f0, 1);
+			if (rc && rc != RIC_E_STREAM) return rc;
+		}
+		return RIC_OK;
+	}
+	// gray: group g uses slot set g % 2.  The stream runs enc(0), enc(1),
+	// then for each g: dec(g), enc(g + 2) -- enc(g + 2) reuses dec(g)'s set
+	// and follows it in stream order.  Host tasks of group g wait for enc(g)'s
+	// event, encode their frame, then decode the stream just written into the
+	// same slot's mirror; dec(g) starts once all of group g's tasks are done.
+	std::vector<hipEvent_t> ev(G, nullptr);
+	for (auto& e : ev) BCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+	std::vector<Latch> done(G);
+	std::vector<FirstErr> err(G);
+	std::vector<int> qs(S, q);
+	int rc = RIC_OK;
+	auto launch_enc = [&](int g) -> int {
+		const int f0 = g * S, m = std::min(S, n - f0), set = g & 1;
+		int r = gpu_encode_plane(b, set, m, 0, pix + f0, q, trans);
+		if (r) return r;
+		BCHK(hipEventRecord(ev[g], b->st));
+		done[g].reset(m);
+		for (int i = 0; i < m; i++) {
+			const int slot = set * S + i, f = f0 + i;
+			b->pool->submit([=, &ev, &err, &done] {
+				int r1 = bfail(hipEventSynchronize(ev[g]), "hipEventSynchronize") ? RIC_E_HIP : RIC_OK;
+				if (!r1) r1 = host_encode_plane(b, slot, 0, q, trans, out[f], cap[f], &len[f]);
+				if (!r1) r1 = host_decode_plane(b, slot, 0, out[f], len[f]);
+				err[g].put(r1);
+				done[g].done();
+			});
+		}
+		return RIC_OK;
+	};
+	int launched = 0;
+	std::vector<char> waited(G, 0);
+	bool stream_err = false;
+	for (; launched < std::min(G, 2); launched++) {
+		rc = launch_enc(launched);
+		if (rc) break;
+	}
+	for (int g = 0; g < launched && rc == RIC_OK; g++) {
+		done[g].wait();
+		waited[g] = 1;
+		const int r = err[g].get();
+		if (r && r != RIC_E_STREAM) { rc = r; break; }
+		stream_err |= r == RIC_E_STREAM;
+		const int f0 = g * S, m = std::min(S, n - f0), set = g & 1;
+		rc = gpu_decode_plane(b, set, m, 0, qs.data(), trans);
+		if (!rc) rc = gpu_pix_out(b, set, m, qs.data(), pix_out + f0, 1);
+		if (!rc && launched < G) rc = launch_enc(launched++);
+	}
+	// on an error, the tasks already queued still run: wait for them
+	for (int k = 0; k < launched; k++)
+		if (!waited[k]) done[k].wait();
+	const bool ok = !bfail(hipStreamSynchronize(b->st), "hipStreamSynchronize");
+	for (auto& e : ev) (void)hipEventDestroy(e);
+	if (rc == RIC_E_HIP) clear_status(b);
+	if (rc) return rc;
+	if (!ok) return RIC_E_HIP;
+	b->prof.harvest();
+	return stream_err ? RIC_E_STREAM : RIC_OK;
+}
+
+int ric_batch_prof_enable(ric_batch* b, int on)
+{
+	if (!b) return RIC_E_ARG;
+	if (set_dev(b->device)) return RIC_E_HIP;
+	BCHK(hipStreamSynchronize(b->st));
+	b->prof.harvest();
+	b->prof.on = on != 0;
+	b->prof.reset();
+	return RIC_OK;
+}
+
+int ric_batch_prof_read(ric_batch* b, double* ms, long* frames, long* launches, int n)
+{
+	if (!b || !ms || !frames || !launches) return RIC_E_ARG;
+	for (int i = 0; i < n && i < B_COUNT; i++) { ms[i] = b->prof.ms[i]; frames[i] = b->prof.frames[i]; launches[i] = b->prof.launches[i]; }
+	return B_COUNT;
+}
+
+}  // extern "C"

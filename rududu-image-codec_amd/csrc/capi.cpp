@@ -15,6 +15,7 @@
 #include "ric_kernels.h"
 #include "ric_image.h"
 #include "entropy.h"
+#include "codec_params.h"
 
 using namespace ric;
 
@@ -30,23 +31,6 @@ bool hip_fail(hipError_t e, const char* what)
 }
 
 #define HIPCHK(x) do { if (hip_fail((x), #x)) return RIC_E_HIP; } while (0)
-
-int tr_any(bool sh, int v) { return sh ? (int)(int16_t)v : v; }
-
-// CBandCodec::makeThres + clen (src/lib/bandcodec.cpp:129-157)
-void make_thres(bool sh, int* thres, int quant, int lambda)
-{
-	static const int blen[17] = {20, 40, 55, 66, 75, 81, 85, 88, 89, 88, 85, 81, 75, 66, 55, 40, 20};
-	static const uint8_t kk[] = {0,0,0,0,0,0,0,0,0,0,0,1,1,1,1,2};
-	static const uint8_t mps[] = {1,1,2,2,2,5,5,5,5,5,5,5,5,5,5,5};
-	for (int i = 0; i < 16; i++) {
-		int clen1 = (kk[i] + 1) * 5 + mps[i];
-		int t = tr_any(sh, (quant + ((lambda * (blen[i + 1] - blen[i] + clen1) + 8) >> 4)) & 0xFFFE);
-		if (t > quant * 2) t = tr_any(sh, quant * 2);
-		if (t < (quant & 0xFFFE)) t = tr_any(sh, quant & 0xFFFE);
-		thres[i] = t;
-	}
-}
 
 // Stage timers (ric_prof_*): GPU stages by hipEvents on the object's stream,
 // host stages by a steady clock.  Harvested at the sync points that already
@@ -133,6 +117,25 @@ namespace {
 
 int set_dev(int device) { return hip_fail(hipSetDevice(device), "hipSetDevice") ? RIC_E_HIP : RIC_OK; }
 
+// The device status word (Pyramid::status_off): a fused level kernel whose
+// LDS ring hand-off timed out raised it (dwt.hip ring_wait_ge); its bands and
+// records are not trusted.  in_copy: the word already came with a region-B
+// copy, else it is read here (the caller has synchronised the stream).
+int take_status(ric_wavelet* w, bool in_copy)
+{
+	int32_t* hs = (int32_t*)(w->h_arena + w->P.status_off);
+	if (!in_copy) {
+		HIPCHK(hipMemcpyAsync(hs, w->d_arena + w->P.status_off, sizeof(int32_t), hipMemcpyDeviceToHost, w->st));
+		HIPCHK(hipStreamSynchronize(w->st));
+	}
+	if (*hs == 0) return RIC_OK;
+	*hs = 0;
+	HIPCHK(hipMemsetAsync(w->d_arena + w->P.status_off, 0, sizeof(int32_t), w->st));
+	HIPCHK(hipStreamSynchronize(w->st));
+	g_err = "fused level kernel: LDS ring hand-off timed out (device status word set; output discarded)";
+	return RIC_E_HIP;
+}
+
 // region A (+ B with records): see Pyramid in ric_types.h
 int to_host(ric_wavelet* w, bool records = false)
 {
@@ -142,7 +145,7 @@ int to_host(ric_wavelet* w, bool records = false)
 	w->prof.end(S_D2H, w->st);
 	HIPCHK(hipStreamSynchronize(w->st));
 	w->prof.harvest();
-	return RIC_OK;
+	return records ? take_status(w, true) : RIC_OK;
 }
 
 int to_device(ric_wavelet* w)
@@ -211,18 +214,6 @@ int inverse(ric_wavelet* w, int16_t* dimg, long stride, int trans)
 	return RIC_OK;
 }
 
-// CWavelet2D::TSUQi fused into TransformI (the codec's decode path): the
-// bands stay quantised in HBM and every inverse level multiplies the band
-// values it loads by their TSUQi factor (src/lib/band.h:94-107,
-// src/lib/wavelet2d.cpp:248-268); the coarsest level also its LL.
-int tsuqi_factor(const Band& B, int quant)
-{
-	const bool sh = !B.is_int;
-	int q = tr_any(sh, quant);
-	q = tr_any(sh, (int)((float)q / B.weight));
-	return q == 0 ? 1 : q;
-}
-
 int inverse_deq(ric_wavelet* w, int16_t* dimg, long stride, int trans, int quant)
 {
 	Pyramid& P = w->P;
@@ -245,34 +236,7 @@ int inverse_deq(ric_wavelet* w, int16_t* dimg, long stride, int trans, int quant
 	return RIC_OK;
 }
 
-// buildTree parameters of level l (src/lib/bandcodec.cpp:243-247, float32 as
-// the reference); qin carries CodeBand's per-level C-typed Quant.
-QuantParams level_qp(const Pyramid& P, int l, int& qin, int lambda)
-{
-	const bool sh = !P.L[l].is_int;
-	qin = tr_any(sh, qin);
-	QuantParams qp;
-	for (int b = 0; b < 3; b++) {
-		const Band& B = P.L[l].b[b];
-		int lbda = (int)((float)lambda / B.weight);
-		int Q = tr_any(sh, (int16_t)(int)((float)qin / B.weight));
-		if (Q == 0) Q = 1;
-		qp.Q[b] = Q;
-		qp.iQ[b] = (1 << 16) / Q;
-		make_thres(sh, qp.thres[b], Q, lbda);
-	}
-	return qp;
-}
-
-// CBand::TSUQ on the coarsest LL with Thres 0.5 (band.h:65-92): parameters
-void ll_params(ric_wavelet* w, int quant, int& Q, int& iQ, int& T0)
-{
-	Band& B = w->P.coarsest_ll();
-	Q = (int)((float)quant / B.weight);
-	if (Q == 0) Q = 1;
-	iQ = (1 << 16) / Q;
-	T0 = tr_any(!B.is_int, (int)(0.5f * (float)Q));
-}
+void ll_params(ric_wavelet* w, int quant, int& Q, int& iQ, int& T0) { ll_params(w->P, quant, Q, iQ, T0); }
 void quant_ll(ric_wavelet* w, int quant)
 {
 	int Q, iQ, T0;
@@ -361,8 +325,12 @@ int flush_pending(ric_wavelet* w)
 }
 
 // The host half: bands + records to the pinned mirror (unless the caller
-// copied them already), then the serial coder.
-int code_band_host(ric_wavelet* w, Mux& m, bool copy = true)
+// copied them already), then the serial coder.  state: also leave the bands
+// in the state the reference's CodeBand leaves them in (sign-magnitude, the
+// INSIGNIF markers the scan consumes cleared: src/lib/bandcodec.cpp:510-588),
+// for API callers that read the bands or run TSUQi next
+// (src/lib/rududucodec.cpp:70-73); the codec's .ric path does not need it.
+int code_band_host(ric_wavelet* w, Mux& m, bool copy = true, bool state = false)
 {
 	Pyramid& P = w->P;
 	if (copy) {
@@ -382,7 +350,19 @@ int code_band_host(ric_wavelet* w, Mux& m, bool copy = true)
 		}
 	}
 	w->prof.host(S_HENC, now_ms() - t0);
-	w->host_valid = true;   // the bands now hold the encoder's final state
+	if (state) {
+		for (int l = P.nlev - 1; l >= 0; l--) {
+			const int order[3] = {BV, BH, BD};
+			for (int k = 0; k < 3; k++) {
+				BandView par;
+				if (l + 1 < P.nlev) par = view(w, P.L[l + 1].b[order[k]]);
+				tree_encode_state(view(w, P.L[l].b[order[k]]), par, l > 0);
+			}
+		}
+	}
+	// the host mirror is now the reference: CodeBand's final state with
+	// `state`, else buildTree's (the codec path never reads it back)
+	w->host_valid = true;
 	return RIC_OK;
 }
 
@@ -432,7 +412,7 @@ int code_band(ric_wavelet* w, Mux& m, int quant, int lambda)
 {
 	int rc = w->pend ? encode_gpu(w, w->d_img, (long)w->img_pitch, w->pend_trans, quant, lambda)
 	                 : quantize_gpu(w, quant, lambda);
-	return rc ? rc : code_band_host(w, m);
+	return rc ? rc : code_band_host(w, m, true, true);
 }
 
 // Exclusive GPU sections: the codec's device stages (pixel conversion, DWT,
@@ -473,6 +453,12 @@ int ric_device_count(void)
 }
 
 const char* ric_last_error(void) { return g_err.c_str(); }
+
+}  // extern "C"
+
+void ric::set_last_error(const std::string& msg) { g_err = msg; }
+
+extern "C" {
 
 int ric_wavelet_create(ric_wavelet** out, int x, int y, int level, int level_chg, int device)
 {
@@ -594,7 +580,7 @@ int ric_quantize(ric_wavelet* w, int quant, int lambda)
 	                 : quantize_gpu(w, quant, lambda);
 	if (rc) return rc;
 	HIPCHK(hipStreamSynchronize(w->st));
-	return RIC_OK;
+	return take_status(w, false);
 }
 
 int ric_transform_quantize(ric_wavelet* w, const int16_t* image, int stride, int trans, int on_device,
@@ -616,7 +602,7 @@ int ric_transform_quantize(ric_wavelet* w, const int16_t* image, int stride, int
 	if (rc) return rc;
 	HIPCHK(hipStreamSynchronize(w->st));
 	w->prof.harvest();
-	return RIC_OK;
+	return take_status(w, false);
 }
 
 int ric_decode_band(ric_wavelet* w, ric_mux* m)
@@ -974,6 +960,12 @@ int ric_diag_wgtrace(int device, uint64_t* out, int n)
 	if (!out || n < 0) return RIC_E_ARG;
 	const int r = diag_wgtrace(device, out, n);
 	return r < 0 ? RIC_E_HIP : r;
+}
+
+int ric_diag_fault(int on)
+{
+	diag_set_fault(on);
+	return RIC_OK;
 }
 
 // SURVEY.md §8(d) synthetic generator (integer-only, bit-reproducible)

@@ -16,7 +16,10 @@
 // (tr<SH>), the int level does not.  The boundary formulas are the reference's
 // start/tail cases (symmetric extension).
 #include <hip/hip_runtime.h>
+#include <atomic>
 #include <cstdlib>
+#include <cstring>
+#include <vector>
 #include <mutex>
 #include <type_traits>
 #include "ric_types.h"
@@ -828,6 +831,8 @@ struct FqArgs {
 	uint64_t* wgt;                     // diagnostics: per-workgroup timestamps (dbg 128), or null
 	int pk;                            // k_fwdq_gen: short bands whose thresholds pass pk_ok
 	int level;
+	int* err;                          // device error word (ring hand-off timeout), or null
+	int fault;                         // fault injection (ric_diag_fault): force a ring timeout
 };
 
 struct PRow8 { v2s q[4]; };            // (c0,c2) (c4,c6) | (c1,c3) (c5,c7)
@@ -1047,10 +1052,17 @@ __device__ __forceinline__ void ring_put(int* p, int v)
 	asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 	__hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-// bounded spin (~30 ms): a protocol error ends in wrong output, never a hang
-__device__ __forceinline__ void ring_wait_ge(int* p, int need)
+// Bounded spin (~30 ms): a protocol error must never hang the GPU.  A wait
+// that gives up raises the launch's device error word (FqArgs::err, the
+// arena's status word), which the host reads at its next sync point and turns
+// into RIC_E_HIP: the slot it would have taken is not trusted.  limit: polls
+// (the fault-injection knob, ric_diag_fault, shortens it).
+constexpr int kRingPolls = 1 << 20;
+__device__ __forceinline__ void ring_wait_ge(int* p, int need, int* err, int limit = kRingPolls)
 {
-	for (int n = 0; ring_get(p) < need && n < (1 << 20); n++) __builtin_amdgcn_s_sleep(1);
+	int n = 0;
+	for (; ring_get(p) < need && n < limit; n++) __builtin_amdgcn_s_sleep(1);
+	if (n >= limit && err) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 	asm volatile("" ::: "memory");
 }
 
@@ -1144,9 +1156,9 @@ __device__ __forceinline__ void fq_seg(const FqArgs& a, const int (*thr)[16], co
 			cur = (it - 1) & (kRing - 1);
 			const int need = it - kRing;
 			if (need > 0) {
-				ring_wait_ge(hring + 1, need);
-				ring_wait_ge(hring + 2, need);
-				ring_wait_ge(hring + 3, need);
+				ring_wait_ge(hring + 1, need, a.err);
+				ring_wait_ge(hring + 2, need, a.err);
+				ring_wait_ge(hring + 3, need, a.err);
 			}
 		} else {
 			cur = it & 1;
@@ -1292,11 +1304,14 @@ __device__ __forceinline__ void fq_consume(const FqArgs& a, int (*s_thres)[16], 
 	FqCrd c0 = fq_crd_load(a, b, kx, ky0);
 	fq_stage_tables<192>(a, s_thres, s_F, s_tpk, t);
 	ring_put(ring + st + b, 1);
-	ring_wait_ge(ring + st, 1); ring_wait_ge(ring + st + 1, 1); ring_wait_ge(ring + st + 2, 1);
+	ring_wait_ge(ring + st, 1, a.err); ring_wait_ge(ring + st + 1, 1, a.err); ring_wait_ge(ring + st + 2, 1, a.err);
 	if (lt && lane == 0) lt[3 + b] = __builtin_amdgcn_s_memrealtime();
 	auto row = [&](int j, const FqCrd& cr) {
-		ring_wait_ge(ring, j + 1);
-		if (npub > 1) ring_wait_ge(ring + 1, j + 1);
+		// fault injection (a.fault): the first block row waits for a count
+		// that never comes, with a short limit
+		const bool inject = a.fault && j == 0;
+		ring_wait_ge(ring, inject ? (1 << 30) : j + 1, a.err, inject ? 64 : kRingPolls);
+		if (npub > 1) ring_wait_ge(ring + 1, j + 1, a.err);
 		uint2 v[4];
 #pragma unroll
 		for (int r = 0; r < 4; r++) v[r] = buf[j & (kRing - 1)][b][r][lane];
@@ -1364,7 +1379,7 @@ constexpr int kWgTraceMax = 8192;
 // role known before the first barrier lets the producer issue its prologue
 // row loads before the workgroup stages the format tables.
 template <bool ASYNC>
-__global__ void __launch_bounds__(256, 4) k_fwdq_pc(FqArgs a, int S, int dbg)
+__device__ __forceinline__ void fwdq_pc_body(const FqArgs& a, int S, int dbg)
 {
 	__shared__ int s_thres[3][16];
 	__shared__ FqTables s_F __attribute__((aligned(16)));
@@ -1448,6 +1463,17 @@ __global__ void __launch_bounds__(256, 4) k_fwdq_pc(FqArgs a, int S, int dbg)
 	}
 }
 
+// One frame (arguments by value), or a batch of frames: blockIdx.z = frame,
+// per-frame arguments from a device array (their pointers differ), so the
+// levels of many frames run as one grid.
+template <bool ASYNC>
+__global__ void __launch_bounds__(256, 4) k_fwdq_pc(FqArgs a, int S, int dbg) { fwdq_pc_body<ASYNC>(a, S, dbg); }
+template <bool ASYNC>
+__global__ void __launch_bounds__(256, 4) k_fwdq_pc_z(const FqArgs* __restrict__ az, int S, int dbg)
+{
+	fwdq_pc_body<ASYNC>(az[blockIdx.z], S, dbg);
+}
+
 // ------------------------------------ two-producer fused level (k_fwdq_pc2)
 // The producer of k_fwdq_pc is the segment's critical path: one wave lifts
 // 8 columns per lane, and a wave alone on its SIMD issues one VALU op per
@@ -1507,9 +1533,9 @@ __device__ __forceinline__ void fq2_producer(const FqArgs& a, int x, int lane, i
 			cur = (it - 1) & (kRing - 1);
 			const int need = it - kRing;
 			if (need > 0) {
-				ring_wait_ge(hring + 2, need);
-				ring_wait_ge(hring + 3, need);
-				ring_wait_ge(hring + 4, need);
+				ring_wait_ge(hring + 2, need, a.err);
+				ring_wait_ge(hring + 3, need, a.err);
+				ring_wait_ge(hring + 4, need, a.err);
 			}
 		} else {
 			cur = it & 1;
@@ -1573,7 +1599,7 @@ __device__ __forceinline__ void fq2_producer(const FqArgs& a, int x, int lane, i
 // grid (strips, segments), 5 waves: 0, 1 = producers of the two halves,
 // 2..4 = the D, H, V consumers
 template <bool ASYNC>
-__global__ void __launch_bounds__(320) k_fwdq_pc2(FqArgs a, int S, int dbg)
+__device__ __forceinline__ void fwdq_pc2_body(const FqArgs& a, int S, int dbg)
 {
 	__shared__ int s_thres[3][16];
 	__shared__ FqTables s_F __attribute__((aligned(16)));
@@ -1647,6 +1673,14 @@ __global__ void __launch_bounds__(320) k_fwdq_pc2(FqArgs a, int S, int dbg)
 		                     (uint32_t)__builtin_amdgcn_s_memtime();
 		if (w == 0) wgt[7] = (uint64_t)wgi | ((uint64_t)__builtin_amdgcn_s_getreg(kHwRegXcc) << 32);
 	}
+}
+
+template <bool ASYNC>
+__global__ void __launch_bounds__(320) k_fwdq_pc2(FqArgs a, int S, int dbg) { fwdq_pc2_body<ASYNC>(a, S, dbg); }
+template <bool ASYNC>
+__global__ void __launch_bounds__(320) k_fwdq_pc2_z(const FqArgs* __restrict__ az, int S, int dbg)
+{
+	fwdq_pc2_body<ASYNC>(az[blockIdx.z], S, dbg);
 }
 
 int fq_seg_rows(int H)
@@ -1839,7 +1873,7 @@ __device__ __forceinline__ void gen_block(const FqArgs& a, const int* thr, const
 // that take this kernel are small and latency-bound: the wide block phase
 // replaces the two dependent rounds of a wave-per-segment form.
 template <typename TI, typename TO>
-__global__ void __launch_bounds__(256) k_fwdq_gen(FqArgs a, GenLL ll, int nseg)
+__device__ __forceinline__ void fwdq_gen_body(const FqArgs& a, const GenLL& ll, int nseg)
 {
 	__shared__ int s_thres[3][16];
 	__shared__ FqTables s_F __attribute__((aligned(16)));
@@ -1909,6 +1943,14 @@ __global__ void __launch_bounds__(256) k_fwdq_gen(FqArgs a, GenLL ll, int nseg)
 		}
 		if (wgt && threadIdx.x == 0) wgt[8] = __builtin_amdgcn_s_memrealtime();
 	}
+}
+
+template <typename TI, typename TO>
+__global__ void __launch_bounds__(256) k_fwdq_gen(FqArgs a, GenLL ll, int nseg) { fwdq_gen_body<TI, TO>(a, ll, nseg); }
+template <typename TI, typename TO>
+__global__ void __launch_bounds__(256) k_fwdq_gen_z(const FqArgs* __restrict__ az, GenLL ll, int nseg)
+{
+	fwdq_gen_body<TI, TO>(az[blockIdx.z], ll, nseg);
 }
 
 // ---------------------------------------------------------- inverse level
@@ -2314,7 +2356,7 @@ __device__ __forceinline__ void inv97p_seg(const InvArgs<int16_t, int16_t, int16
 }
 
 template <int TRANS, typename TB, typename TL, typename TO, int S>
-__global__ void __launch_bounds__(256) k_inv(InvArgs<TB, TL, TO> a)
+__device__ __forceinline__ void inv_body(const InvArgs<TB, TL, TO>& a)
 {
 	const int lane = threadIdx.x & 63;
 	const int seg = blockIdx.y * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: row math stays scalar
@@ -2331,6 +2373,14 @@ __global__ void __launch_bounds__(256) k_inv(InvArgs<TB, TL, TO> a)
 		if (fast) inv_seg<TRANS, TB, TL, TO, S, true>(a, x, lane, y0);
 		else inv_seg<TRANS, TB, TL, TO, S, false>(a, x, lane, y0);
 	}
+}
+
+template <int TRANS, typename TB, typename TL, typename TO, int S>
+__global__ void __launch_bounds__(256) k_inv(InvArgs<TB, TL, TO> a) { inv_body<TRANS, TB, TL, TO, S>(a); }
+template <int TRANS, typename TB, typename TL, typename TO, int S>
+__global__ void __launch_bounds__(256) k_inv_z(const InvArgs<TB, TL, TO>* __restrict__ az)
+{
+	inv_body<TRANS, TB, TL, TO, S>(az[blockIdx.z]);
 }
 
 // S rows per wave: enough waves to fill the chip on every level, short
@@ -2381,6 +2431,23 @@ void fwd_launch(const Level& L, const void* src, long sp, char* arena, int vec, 
 	else fwd_launch_s<TRANS, TI, TO, 8>(L, src, sp, arena, vec, st);
 }
 
+template <typename TB, typename TO>
+InvArgs<TB, TB, TO> inv_args(const Level& L, const Band& lls, char* arena, void* out, long po, const int* q, int S)
+{
+	InvArgs<TB, TB, TO> a;
+	memset(&a, 0, sizeof a);
+	for (int b = 0; b < 4; b++) a.q[b] = q ? q[b] : 1;
+	a.ovec = (po % 4 == 0) && ((uintptr_t)out % 16 == 0);
+	a.nofast = dbg_nofast();
+	for (int b = 0; b < 3; b++) { a.d[b] = (const TB*)(arena + L.b[b].off); a.p[b] = L.b[b].pitch; }
+	a.ll = (const TB*)(arena + lls.off); a.pl = lls.pitch;
+	a.out = (TO*)out; a.po = po;
+	a.W = L.w; a.H = L.h;
+	a.nseg = (L.h + S - 1) / S;
+	a.quirk_dalign = L.b[BD].ref_align; a.quirk_halign = L.b[BH].ref_align;
+	return a;
+}
+
 template <int TRANS, typename TB, typename TO, int S>
 void inv_launch_s(const Level& L, const Band& lls, char* arena, void* out, long po, const int* q, hipStream_t st)
 {
@@ -2429,6 +2496,11 @@ void inv_dispatch(const Level& L, const Band& lls, char* arena, void* out, long 
 
 }  // namespace
 
+// fault injection (include/ric_gpu.h ric_diag_fault): the consumer waves of
+// the next ring-form launches wait for a block row that never comes
+std::atomic<int> g_ring_fault{0};
+void diag_set_fault(int on) { g_ring_fault.store(on, std::memory_order_relaxed); }
+
 void launch_fwd_level(const Level& L, const void* src, long sp, char* arena, int trans, int vec, hipStream_t st)
 {
 	if (trans == CDF97) fwd_dispatch<CDF97>(L, src, sp, arena, vec, st);
@@ -2447,14 +2519,24 @@ int fwdq_mode(const Level& L, int trans, const QuantParams& qp, int vec16)
 	return packed ? FQ_PACKED : FQ_GENERIC;
 }
 
-void launch_fwdq_level(const Pyramid& P, int l, const void* src, long sp, int vec8, int vec16, const QuantParams& qp,
-                       char* arena, hipStream_t st)
+namespace {
+// The arguments of a fused level launch over one frame's arena.  gen: the
+// generic kernel (k_fwdq_gen), else the packed ring forms.
+FqArgs fq_args(const Pyramid& P, int l, const void* src, long sp, int vec8, int vec16, const QuantParams& qp,
+               char* arena, bool gen)
 {
 	const Level& L = P.L[l];
 	FqArgs a;
+	memset(&a, 0, sizeof a);   // (padding too: batched launches compare argument images)
 	a.wgt = nullptr;
-	a.src = (const int16_t*)src; a.sp = sp; a.W = L.w; a.H = L.h;
-	a.vec8 = vec8; a.vec16 = vec16; a.nofast = dbg_nofast(); a.high = l == 0; a.level = l; a.pk = 1;
+	a.src = (const int16_t*)src; a.sp = sp; a.W = L.w; a.H = L.h; a.nseg = 0;
+	a.vec8 = vec8; a.high = l == 0; a.level = l;
+	if (gen) {
+		a.vec16 = 0; a.nofast = 1;
+		a.pk = !L.is_int && pk_ok(qp.thres[0]) && pk_ok(qp.thres[1]) && pk_ok(qp.thres[2]);
+	} else {
+		a.vec16 = vec16; a.nofast = dbg_nofast(); a.pk = 1;
+	}
 	for (int b = 0; b < 4; b++) { a.d[b] = (int16_t*)(arena + L.b[b].off); a.p[b] = L.b[b].pitch; }
 	for (int b = 0; b < 3; b++) {
 		const Band& B = L.b[b];
@@ -2472,6 +2554,17 @@ void launch_fwdq_level(const Pyramid& P, int l, const void* src, long sp, int ve
 		a.Q[b] = qp.Q[b]; a.iQ[b] = qp.iQ[b];
 		for (int i = 0; i < 16; i++) a.thres[b][i] = qp.thres[b][i];
 	}
+	a.err = (int*)(arena + P.status_off);
+	a.fault = gen ? 0 : g_ring_fault.load(std::memory_order_relaxed);
+	return a;
+}
+}  // namespace
+
+void launch_fwdq_level(const Pyramid& P, int l, const void* src, long sp, int vec8, int vec16, const QuantParams& qp,
+                       char* arena, hipStream_t st)
+{
+	const Level& L = P.L[l];
+	FqArgs a = fq_args(P, l, src, sp, vec8, vec16, qp, arena, false);
 	if (fq_pc()) { fq_launch_pc(a, st); return; }
 	const int S = fq_seg_rows(L.h);
 	if (S == 32) fq_launch_s<32>(a, st);
@@ -2483,29 +2576,9 @@ void launch_fwdq_gen_level(const Pyramid& P, int l, const void* src, long sp, in
                            int ll_on, int ll_iQ, int ll_T0, char* arena, hipStream_t st)
 {
 	const Level& L = P.L[l];
-	FqArgs a;
+	FqArgs a = fq_args(P, l, src, sp, vec8, 0, qp, arena, true);
 	static const int gtrace = [] { const char* e = getenv("RIC_LVL_TRACE"); return e ? atoi(e) : -1; }();
 	a.wgt = gtrace == l ? fq_wgtrace() : nullptr;
-	a.src = (const int16_t*)src; a.sp = sp; a.W = L.w; a.H = L.h;
-	a.vec8 = vec8; a.vec16 = 0; a.nofast = 1; a.high = l == 0; a.level = l;
-	a.pk = !L.is_int && pk_ok(qp.thres[0]) && pk_ok(qp.thres[1]) && pk_ok(qp.thres[2]);
-	for (int b = 0; b < 4; b++) { a.d[b] = (int16_t*)(arena + L.b[b].off); a.p[b] = L.b[b].pitch; }
-	for (int b = 0; b < 3; b++) {
-		const Band& B = L.b[b];
-		a.dx[b] = B.dx; a.dy[b] = B.dy; a.bw[b] = B.bw(); a.bh[b] = B.bh();
-		a.rd[b] = (uint32_t*)(arena + B.rd_off);
-		a.rec[b] = (uint64_t*)(arena + P.rec_off[l][b]);
-		if (l > 0) {
-			const Band& C = P.L[l - 1].b[b];
-			a.crd[b] = (const uint32_t*)(arena + C.rd_off); a.cbw[b] = C.bw();
-			a.cpin[b] = (uint8_t*)(arena + P.pin_off[l - 1][b]); a.cpw[b] = C.bw(); a.cph[b] = C.bh();
-		} else {
-			a.crd[b] = nullptr; a.cbw[b] = 0;
-			a.cpin[b] = nullptr; a.cpw[b] = 0; a.cph[b] = 0;
-		}
-		a.Q[b] = qp.Q[b]; a.iQ[b] = qp.iQ[b];
-		for (int i = 0; i < 16; i++) a.thres[b][i] = qp.thres[b][i];
-	}
 	GenLL ll = {ll_on, ll_iQ, ll_T0};
 	const int nseg = (L.h + kGenRows - 1) / kGenRows;
 	a.nseg = nseg;
@@ -2521,6 +2594,143 @@ void launch_inv_level(const Level& L, const Band& lls, char* arena, void* out, l
 	if (trans == CDF97) inv_dispatch<CDF97>(L, lls, arena, out, po, out_is_int, q, st);
 	else if (trans == CDF53) inv_dispatch<CDF53>(L, lls, arena, out, po, out_is_int, q, st);
 	else inv_dispatch<HAAR>(L, lls, arena, out, po, out_is_int, q, st);
+}
+
+// ------------------------------------------------- batched (blockIdx.z) forms
+// The frames of a batch sit at fixed strides (arena, level input, output),
+// so every launch below is one grid over nz frames, its per-frame arguments
+// in a device array (ZArgs) that is only re-uploaded when it changes.
+int zargs_put(ZArgs& z, const void* data, size_t bytes, hipStream_t st)
+{
+	if (z.img.size() == bytes && memcmp(z.img.data(), data, bytes) == 0) return 0;
+	// the previous image may still be read by queued launches or copied from
+	if (hipStreamSynchronize(st) != hipSuccess) return -1;
+	if (z.cap < bytes) {
+		if (z.dev && hipFree(z.dev) != hipSuccess) return -1;
+		z.dev = nullptr;
+		z.cap = 0;
+		if (hipMalloc(&z.dev, bytes) != hipSuccess) return -1;
+		z.cap = bytes;
+	}
+	z.img.assign((const char*)data, (const char*)data + bytes);
+	return hipMemcpyAsync(z.dev, z.img.data(), bytes, hipMemcpyHostToDevice, st) == hipSuccess ? 0 : -1;
+}
+
+void zargs_free(ZArgs& z)
+{
+	if (z.dev) (void)hipFree(z.dev);
+	z.dev = nullptr;
+	z.cap = 0;
+	z.img.clear();
+}
+
+namespace {
+// segment rows of the ring forms over nz frames: about one round of resident
+// workgroups over the whole batch (tuning knobs RIC_FQZ_SL0..2)
+int pc_seg_rows_z(int W, int H, int nz, int level)
+{
+	static const int sl[3] = {[] { const char* e = getenv("RIC_FQZ_SL0"); return e ? atoi(e) : 0; }(),
+	                          [] { const char* e = getenv("RIC_FQZ_SL1"); return e ? atoi(e) : 0; }(),
+	                          [] { const char* e = getenv("RIC_FQZ_SL2"); return e ? atoi(e) : 0; }()};
+	if (level < 3 && sl[level] >= 8 && sl[level] % 8 == 0) return sl[level];
+	const int nstrip = (W + kFqStrip - 1) / kFqStrip;
+	const int want = std::max(1, kPcResident / (nstrip * nz));          // segments per strip per frame
+	const int s = ((H + want - 1) / want + 7) / 8 * 8;
+	return s < 8 ? 8 : s;
+}
+}  // namespace
+
+int launch_fwdq_level_z(const Pyramid& P, int l, const ZFrames& fr, int vec8, int vec16, const QuantParams& qp,
+                        ZArgs& z, hipStream_t st)
+{
+	const Level& L = P.L[l];
+	const int S = pc_seg_rows_z(L.w, L.h, fr.nz, l);
+	std::vector<FqArgs> v(fr.nz);
+	for (int f = 0; f < fr.nz; f++) {
+		v[f] = fq_args(P, l, (const char*)fr.src + f * fr.sstride, fr.sp, vec8, vec16, qp, fr.arena + f * fr.astride, false);
+		v[f].nseg = (L.h + S - 1) / S;
+	}
+	if (zargs_put(z, v.data(), v.size() * sizeof(FqArgs), st)) return -1;
+	const FqArgs* d = (const FqArgs*)z.dev;
+	const dim3 grid((L.w + kFqStrip - 1) / kFqStrip, v[0].nseg, fr.nz);
+	// the one-producer form on level 0 (VALU-bound), two producers above (see fq_launch_pc)
+	if (l == 0) hipLaunchKernelGGL(k_fwdq_pc_z<true>, grid, dim3(256), 0, st, d, S, 0);
+	else hipLaunchKernelGGL(k_fwdq_pc2_z<true>, grid, dim3(320), 0, st, d, S, 0);
+	return 0;
+}
+
+int launch_fwdq_gen_level_z(const Pyramid& P, int l, const ZFrames& fr, int vec8, const QuantParams& qp, int ll_on,
+                            int ll_iQ, int ll_T0, ZArgs& z, hipStream_t st)
+{
+	const Level& L = P.L[l];
+	const int nseg = (L.h + kGenRows - 1) / kGenRows;
+	std::vector<FqArgs> v(fr.nz);
+	for (int f = 0; f < fr.nz; f++) {
+		v[f] = fq_args(P, l, (const char*)fr.src + f * fr.sstride, fr.sp, vec8, 0, qp, fr.arena + f * fr.astride, true);
+		v[f].nseg = nseg;
+	}
+	if (zargs_put(z, v.data(), v.size() * sizeof(FqArgs), st)) return -1;
+	const FqArgs* d = (const FqArgs*)z.dev;
+	const GenLL ll = {ll_on, ll_iQ, ll_T0};
+	const dim3 grid((L.w + kStripValid - 1) / kStripValid, nseg, fr.nz);
+	if (!L.in_is_int && !L.is_int) hipLaunchKernelGGL((k_fwdq_gen_z<int16_t, int16_t>), grid, dim3(256), 0, st, d, ll, nseg);
+	else if (!L.in_is_int) hipLaunchKernelGGL((k_fwdq_gen_z<int16_t, int32_t>), grid, dim3(256), 0, st, d, ll, nseg);
+	else hipLaunchKernelGGL((k_fwdq_gen_z<int32_t, int32_t>), grid, dim3(256), 0, st, d, ll, nseg);
+	return 0;
+}
+
+namespace {
+// rows per inverse wave in a batch (tuning knob RIC_INVZ_S: forced value)
+template <typename T>
+int inv_seg_rows_z(int H, int nz)
+{
+	static const int forced = [] { const char* e = getenv("RIC_INVZ_S"); return e ? atoi(e) : 0; }();
+	if (forced == 2 || forced == 8 || forced == 16 || ((forced == 32 || forced == 64) && sizeof(T) == 2)) return forced;
+	(void)nz;
+	return seg_rows<T>(H);
+}
+
+template <int TRANS, typename TB, typename TO, int S>
+int inv_launch_z(const Level& L, const Band& lls, const ZFrames& fr, int nz, const int* q, ZArgs& z, hipStream_t st)
+{
+	std::vector<InvArgs<TB, TB, TO>> v(nz);
+	for (int f = 0; f < nz; f++)
+		v[f] = inv_args<TB, TO>(L, lls, fr.arena + f * fr.astride, (char*)fr.out + f * fr.ostride, fr.po, q, S);
+	if (zargs_put(z, v.data(), v.size() * sizeof(v[0]), st)) return -1;
+	const dim3 grid((L.w + kStripValid - 1) / kStripValid, (v[0].nseg + kWavesPerBlock - 1) / kWavesPerBlock, nz);
+	hipLaunchKernelGGL((k_inv_z<TRANS, TB, TB, TO, S>), grid, dim3(256), 0, st, (const InvArgs<TB, TB, TO>*)z.dev);
+	return 0;
+}
+
+template <int TRANS, typename TB, typename TO>
+int inv_launch_zs(const Level& L, const Band& lls, const ZFrames& fr, const int* q, ZArgs& z, hipStream_t st)
+{
+	const int S = inv_seg_rows_z<TB>(L.h, fr.nz);
+	if constexpr (sizeof(TB) == 2) {
+		if (S == 64) return inv_launch_z<TRANS, TB, TO, 64>(L, lls, fr, fr.nz, q, z, st);
+		if (S == 32) return inv_launch_z<TRANS, TB, TO, 32>(L, lls, fr, fr.nz, q, z, st);
+	}
+	if (S == 16) return inv_launch_z<TRANS, TB, TO, 16>(L, lls, fr, fr.nz, q, z, st);
+	if (S == 2) return inv_launch_z<TRANS, TB, TO, 2>(L, lls, fr, fr.nz, q, z, st);
+	return inv_launch_z<TRANS, TB, TO, 8>(L, lls, fr, fr.nz, q, z, st);
+}
+
+template <int TRANS>
+int inv_dispatch_z(const Level& L, const Band& lls, const ZFrames& fr, int out_is_int, const int* q, ZArgs& z,
+                   hipStream_t st)
+{
+	if (!L.is_int) return inv_launch_zs<TRANS, int16_t, int16_t>(L, lls, fr, q, z, st);
+	if (out_is_int) return inv_launch_zs<TRANS, int32_t, int32_t>(L, lls, fr, q, z, st);
+	return inv_launch_zs<TRANS, int32_t, int16_t>(L, lls, fr, q, z, st);
+}
+}  // namespace
+
+int launch_inv_level_z(const Level& L, const Band& lls, const ZFrames& fr, int out_is_int, int trans, const int* q,
+                       ZArgs& z, hipStream_t st)
+{
+	if (trans == CDF97) return inv_dispatch_z<CDF97>(L, lls, fr, out_is_int, q, z, st);
+	if (trans == CDF53) return inv_dispatch_z<CDF53>(L, lls, fr, out_is_int, q, z, st);
+	return inv_dispatch_z<HAAR>(L, lls, fr, out_is_int, q, z, st);
 }
 
 }  // namespace ric

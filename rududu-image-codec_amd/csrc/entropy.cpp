@@ -107,10 +107,35 @@ void Mux::init_encoder(uint8_t* buf, size_t cap, uint16_t first_word)
 
 void Mux::init_decoder(const uint8_t* buf, size_t len)
 {
+	free(owned_);
+	owned_cap_ = 0;
 	owned_ = (uint8_t*)calloc(len + kDecPad, 1);
 	memcpy(owned_, buf, len);
 	base_ = owned_;
 	limit_ = owned_ + len + kDecPad - 16;
+	range_ = 1u << 16;
+	nbits_ = 0; buffer_ = 0; overflow_ = false;
+	init_ = owned_ + 2; p_ = owned_ + 2;
+	code_ = low_ = ((uint32_t)p_[0] << 8) | p_[1];
+	p_ += 2;
+}
+
+void Mux::init_decoder_payload(const uint8_t* payload, size_t n)
+{
+	// the reference reads the payload at buf + 2 (src/ric/ric.cpp:203-205):
+	// two zero bytes, then the .ric payload, then zero padding.  The buffer
+	// is kept across frames (no fresh zeroed pages per frame).
+	const size_t need = n + 2 + kDecPad;
+	if (owned_cap_ < need) {
+		free(owned_);
+		owned_ = (uint8_t*)malloc(need);
+		owned_cap_ = need;
+	}
+	owned_[0] = owned_[1] = 0;
+	memcpy(owned_ + 2, payload, n);
+	memset(owned_ + 2 + n, 0, kDecPad);
+	base_ = owned_;
+	limit_ = owned_ + n + 2 + kDecPad - 16;
 	range_ = 1u << 16;
 	nbits_ = 0; buffer_ = 0; overflow_ = false;
 	init_ = owned_ + 2; p_ = owned_ + 2;
@@ -635,6 +660,68 @@ void tree_t(Mux& m, const BandView& b, const BandView& par, bool has_child)
 	}
 }
 
+// The band writes of tree<encode> alone (src/lib/bandcodec.cpp:510-588): the
+// parent's INSIGNIF markers this band consumes are cleared, a skipped or
+// insignificant full block gets the marker (or 0 without children) at its
+// four child anchors, an insignificant edge block's marker becomes 0.  Run on
+// every band in coding order it leaves the pyramid in the state CodeBand
+// leaves it in (what a caller of TSUQi after CodeBand dequantises).
+template <typename C, typename P>
+void tree_state_t(const BandView& b, const BandView& par, bool has_child)
+{
+	constexpr bool SH = is_short<C>();
+	const long st = b.pitch;
+	const int dx = b.dx, dy = b.dy;
+	P* pbase = (P*)par.p;
+	const long pst = par.pitch;
+	const int pdx = par.dx, pdy = par.dy;
+	const C mark = (C)tr<SH>(has_child ? kInsignif : 0);
+	C* band = (C*)b.p;
+	auto edge_block = [&](C* c1, int i, P* pp, bool chk_row, int j) {
+		if (pp && (i >> 1) < pdx && (!chk_row || (j >> 1) < pdy) && pp[i >> 1] == kInsignif) pp[i >> 1] = 0;
+		if (c1[i] == (C)kInsignif) c1[i] = 0;
+	};
+	int j = 0;
+	for (; j + 4 <= dy; j += 4) {
+		C* c1 = band + j * st;
+		C* c2 = c1 + 2 * st;
+		P* pp = pbase ? pbase + (long)(j >> 1) * pst : nullptr;
+		int i = 0, bs = 4;
+		if (j & 4) {
+			bs = -4;
+			i = dx & ~3;
+			if (dx > i) edge_block(c1, i, pp, false, j);
+			i += bs;
+		}
+		for (; i >= 0 && i + 4 <= dx; i += bs) {
+			const int k = i >> 1;
+			if (pp && pp[k] == kInsignif) {
+				pp[k] = 0;
+				c1[i] = c1[i + 2] = c2[i] = c2[i + 2] = mark;
+			} else if (c1[i] == (C)kInsignif) {
+				c1[i] = c1[i + 2] = c2[i] = c2[i + 2] = mark;
+			}
+		}
+		if (i > 0 && i < dx) edge_block(c1, i, pp, false, j);
+	}
+	if (j < dy) {
+		C* c1 = band + j * st;
+		P* pp = pbase ? pbase + (long)(j >> 1) * pst : nullptr;
+		int i = 0, bs = 4;
+		if (j & 4) {
+			bs = -4;
+			i = dx & ~3;
+			if (dx > i) edge_block(c1, i, pp, true, j);
+			i += bs;
+		}
+		for (; i >= 0 && i + 4 <= dx; i += bs) {
+			if (pp && (j >> 1) < pdy && pp[i >> 1] == kInsignif) pp[i >> 1] = 0;
+			if (c1[i] == (C)kInsignif) c1[i] = 0;
+		}
+		if (i > 0 && i < dx) edge_block(c1, i, pp, true, j);
+	}
+}
+
 template <bool DEC>
 void tree_dispatch(Mux& m, const BandView& b, const BandView& par, bool high, bool has_child)
 {
@@ -668,6 +755,13 @@ void tree_encode(Mux& m, const BandView& b, const BandView& par, bool high, bool
 void tree_decode(Mux& m, const BandView& b, const BandView& par, bool high, bool has_child)
 {
 	tree_dispatch<true>(m, b, par, high, has_child);
+}
+void tree_encode_state(const BandView& b, const BandView& par, bool has_child)
+{
+	const bool pint = par.p ? par.is_int : b.is_int;
+	if (!b.is_int && !pint) tree_state_t<int16_t, int16_t>(b, par, has_child);
+	else if (!b.is_int) tree_state_t<int16_t, int32_t>(b, par, has_child);
+	else tree_state_t<int32_t, int32_t>(b, par, has_child);
 }
 
 }  // namespace ric

@@ -23,6 +23,12 @@ public:
 	void init_encoder(uint8_t* buf, size_t cap, uint16_t first_word = 0);
 	// decoder over a copy of [buf, buf + len) padded with zeros
 	void init_decoder(const uint8_t* buf, size_t len);
+	// decoder over a .ric payload (the bytes after the 9-byte header): the
+	// same as init_decoder on two zero bytes followed by the payload
+	void init_decoder_payload(const uint8_t* payload, size_t n);
+	Mux() = default;
+	Mux(const Mux&) = delete;
+	Mux& operator=(const Mux&) = delete;
 	~Mux();
 
 	uint8_t* end_coding();                  // endCoding, muxcodec.cpp:87-106
@@ -115,6 +121,7 @@ private:
 	uint8_t *base_ = nullptr, *p_ = nullptr, *init_ = nullptr, *limit_ = nullptr;
 	uint8_t *last_[4] = {nullptr, nullptr, nullptr, nullptr}, *reserved_ = nullptr;
 	uint8_t* owned_ = nullptr;              // decoder copy
+	size_t owned_cap_ = 0;                  // its size when reused (init_decoder_payload)
 	uint32_t range_ = 0, low_ = 0, code_ = 0, outcount_ = 0, nbits_ = 0, buffer_ = 0;
 	uint64_t ebuf_ = 0;                     // encoder raw-bit FIFO
 	uint32_t ebits_ = 0;
@@ -155,6 +162,9 @@ void pred_decode(Mux& m, const BandView& b);
 // CBandCodec::tree, src/lib/bandcodec.cpp:484-589.  par.p == nullptr: no parent.
 void tree_encode(Mux& m, const BandView& b, const BandView& par, bool high, bool has_child);
 void tree_decode(Mux& m, const BandView& b, const BandView& par, bool high, bool has_child);
+// The band writes of tree<encode> without the coding (entropy.cpp): applied
+// coarse -> fine after the record encoder, the pyramid ends in CodeBand's state.
+void tree_encode_state(const BandView& b, const BandView& par, bool has_child);
 // Register-resident decoder of one band (decoder.cpp), same semantics as
 // tree_decode.
 void tree_decode_fast(Mux& m, const BandView& b, const BandView& par, bool high, bool has_child);

@@ -1,6 +1,7 @@
 // ric_kernels.h -- host-side launchers of the HIP kernels (dwt.hip, quant.hip).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <vector>
 #include "ric_types.h"
 
 namespace ric {
@@ -51,7 +52,38 @@ void launch_blocks_level(const Pyramid& P, int l, bool do_rec, bool do_pin, char
 void launch_tsuq_band(const Band& B, int iQ, int T0, char* arena, unsigned int* count, hipStream_t st);
 // CBand::TSUQi on one band (src/lib/band.h:94-107).
 void launch_dequant_band(const Band& B, int q, char* arena, hipStream_t st);
+// ------------------------------------------------------- batched launches
+// nz frames at fixed strides: frame f's arena is arena + f * astride, its
+// level input src + f * sstride (bytes, row pitch sp elements), its inverse
+// output out + f * ostride (bytes, row pitch po elements).  One grid over all
+// frames (blockIdx.z = frame).
+struct ZFrames {
+	char* arena = nullptr; size_t astride = 0;
+	const void* src = nullptr; size_t sstride = 0; long sp = 0;
+	void* out = nullptr; size_t ostride = 0; long po = 0;
+	int nz = 0;
+};
+// Per-frame argument array of one batched launch, on the device; re-uploaded
+// (after a stream sync) only when it changes.
+struct ZArgs {
+	void* dev = nullptr;
+	size_t cap = 0;
+	std::vector<char> img;
+};
+int zargs_put(ZArgs& z, const void* data, size_t bytes, hipStream_t st);
+void zargs_free(ZArgs& z);
+// The batched forms of launch_fwdq_level / launch_fwdq_gen_level /
+// launch_inv_level; 0 or -1 (HIP error).
+int launch_fwdq_level_z(const Pyramid& P, int l, const ZFrames& fr, int vec8, int vec16, const QuantParams& qp,
+                        ZArgs& z, hipStream_t st);
+int launch_fwdq_gen_level_z(const Pyramid& P, int l, const ZFrames& fr, int vec8, const QuantParams& qp, int ll_on,
+                            int ll_iQ, int ll_T0, ZArgs& z, hipStream_t st);
+int launch_inv_level_z(const Level& L, const Band& lls, const ZFrames& fr, int out_is_int, int trans, const int* q,
+                       ZArgs& z, hipStream_t st);
+
 // diagnostics: the level-0 workgroup trace of the fused level kernel (dwt.hip)
 int diag_wgtrace(int device, uint64_t* host, int n);
+// fault injection: force a ring hand-off timeout in the next fused launches
+void diag_set_fault(int on);
 
 }  // namespace ric

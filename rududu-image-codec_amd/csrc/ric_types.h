@@ -71,8 +71,8 @@ struct Level {
 // CWavelet2D::Init geometry (src/lib/wavelet2d.cpp:69-81, src/lib/band.cpp:51-65).
 // Arena layout (one allocation on the device, a pinned mirror on the host):
 //   region A [0, a_end):     the coded bands (D/H/V of every level + coarsest LL)
-//   region B [a_end, b_end): per-block zerotree records + parent info of the
-//                            3*nlev high bands
+//   region B [a_end, b_end): the device status word, per-block zerotree
+//                            records + parent info of the 3*nlev high bands
 //   region C [b_end, end):   device-only scratch: intermediate LL planes, pRD
 // Encode copies A+B to the host, decode copies A back to the device.
 struct Pyramid {
@@ -80,6 +80,7 @@ struct Pyramid {
 	int w = 0, h = 0, levels = 0, lc = 0;
 	Level L[kMaxLevels];
 	size_t arena_bytes = 0, a_end = 0, b_end = 0;
+	size_t status_off = 0;                // int: device error word (ring timeout), start of region B
 	size_t rec_off[kMaxLevels][3] = {};   // u64 block records (symbols.h), raster order
 	size_t pin_off[kMaxLevels][3] = {};   // u8 parent info per block (symbols.h), raster order
 
@@ -116,6 +117,7 @@ struct Pyramid {
 			for (int b = 0; b < 3; b++) L[l].b[b].off = take(L[l].b[b].bytes());
 		L[nlev - 1].b[BL].off = take(L[nlev - 1].b[BL].bytes());
 		a_end = off;
+		status_off = take(256);
 		for (int l = 0; l < nlev; l++)
 			for (int b = 0; b < 3; b++) rec_off[l][b] = take((size_t)L[l].b[b].bw() * L[l].b[b].bh() * 8);
 		for (int l = 0; l < nlev; l++)

@@ -80,6 +80,14 @@ def lib():
         "ric_codec_wavelet": (_P, [_P]),
         "ric_synth_image": (None, [_I, _I, _I, _I, _P]),
         "ric_diag_wgtrace": (_I, [_I, _P, _I]),
+        "ric_diag_fault": (_I, [_I]),
+        "ric_batch_create": (_I, [ctypes.POINTER(_P), _I, _I, _I, _I, _I, _I]),
+        "ric_batch_destroy": (None, [_P]),
+        "ric_batch_encode": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _P]),
+        "ric_batch_decode": (_I, [_P, _P, _P, _I, _P, _I]),
+        "ric_batch_roundtrip": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _P]),
+        "ric_batch_prof_enable": (_I, [_P, _I]),
+        "ric_batch_prof_read": (_I, [_P, _P, _P, _P, _I]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -256,6 +264,103 @@ class Wavelet2D:
     def write_band(self, i, arr):
         a = np.ascontiguousarray(arr, np.int32)
         _chk(lib().ric_band_write(self.h, i, a.ctypes.data), "band_write")
+
+
+BATCH_STAGES = (["pix_in"] + ["fwd_l%d" % l for l in range(8)] + ["d2h", "host_enc", "host_dec", "h2d"] +
+                ["inv_l%d" % l for l in range(8)] + ["pix_out"])
+
+
+def _ptrs(xs):
+    a = (ctypes.c_void_p * len(xs))()
+    for i, x in enumerate(xs):
+        a[i] = _ptr(x)
+    return a
+
+
+class Batch:
+    """ric_batch: CompressImage / DecompressImage over groups of up to `slots`
+    frames (one GPU launch per level per group, a native pool of `threads`
+    host coder threads).  Frames are (channels, h, w) uint8 numpy arrays or
+    device tensors / pointers."""
+
+    def __init__(self, w, h, channels=1, slots=16, threads=16, device=0):
+        hd = _P()
+        _chk(lib().ric_batch_create(ctypes.byref(hd), w, h, channels, slots, threads, device), "ric_batch_create")
+        self.h = hd
+        self.w, self.hgt, self.channels, self.slots = w, h, channels, slots
+        self.cap = w * h * channels * 2 + 65536
+        self._outs = []
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.ric_batch_destroy(self.h)
+            self.h = None
+
+    def _out_bufs(self, n):
+        while len(self._outs) < n:
+            self._outs.append(np.empty(self.cap, np.uint8))
+        return self._outs[:n]
+
+    def compress(self, frames, q=9, trans=None, on_device=None):
+        """Returns the list of .ric files (bytes)."""
+        if trans is None:
+            trans = CDF53 if q == 0 else CDF97
+        n = len(frames)
+        dev = on_device if on_device is not None else not isinstance(frames[0], np.ndarray)
+        if not dev:
+            frames = [np.ascontiguousarray(f, np.uint8) for f in frames]
+        outs = self._out_bufs(n)
+        caps = (ctypes.c_size_t * n)(*([self.cap] * n))
+        lens = (ctypes.c_size_t * n)()
+        _chk(lib().ric_batch_encode(self.h, _ptrs(frames), n, int(dev), q, trans, _ptrs(outs), caps, lens),
+             "ric_batch_encode")
+        return [outs[i][:lens[i]].tobytes() for i in range(n)]
+
+    def decompress(self, rics, pix_out=None):
+        """Host mode: returns a list of (channels, h, w) uint8 arrays.  Device
+        mode: pass device tensors / pointers in pix_out.  Returns the status
+        (RIC_OK or RIC_E_STREAM) in device mode."""
+        n = len(rics)
+        bufs = [np.frombuffer(r, np.uint8) for r in rics]
+        lens = (ctypes.c_size_t * n)(*[len(r) for r in rics])
+        if pix_out is None:
+            outs = [np.zeros((self.channels, self.hgt, self.w), np.uint8) for _ in range(n)]
+            rc = lib().ric_batch_decode(self.h, _ptrs(bufs), lens, n, _ptrs(outs), 0)
+            if rc not in (RIC_OK, RIC_E_STREAM):
+                _chk(rc, "ric_batch_decode")
+            return outs
+        rc = lib().ric_batch_decode(self.h, _ptrs(bufs), lens, n, _ptrs(pix_out), 1)
+        if rc not in (RIC_OK, RIC_E_STREAM):
+            _chk(rc, "ric_batch_decode")
+        return rc
+
+    def roundtrip(self, frames, pix_out, q=9, trans=0):
+        """Encode then decode every frame (device pixels in and out), groups
+        pipelined; returns the .ric files' sizes and keeps the files in
+        self.streams(n)."""
+        n = len(frames)
+        outs = self._out_bufs(n)
+        caps = (ctypes.c_size_t * n)(*([self.cap] * n))
+        lens = (ctypes.c_size_t * n)()
+        rc = lib().ric_batch_roundtrip(self.h, _ptrs(frames), n, q, trans, _ptrs(outs), caps, lens, _ptrs(pix_out))
+        if rc not in (RIC_OK, RIC_E_STREAM):
+            _chk(rc, "ric_batch_roundtrip")
+        self._lens = [lens[i] for i in range(n)]
+        return self._lens
+
+    def stream(self, i):
+        return self._outs[i][:self._lens[i]].tobytes()
+
+    def prof_enable(self, on=True):
+        _chk(lib().ric_batch_prof_enable(self.h, int(on)), "ric_batch_prof_enable")
+
+    def prof_read(self):
+        k = len(BATCH_STAGES)
+        ms = np.zeros(k, np.float64)
+        fr = np.zeros(k, np.int64)
+        ln = np.zeros(k, np.int64)
+        lib().ric_batch_prof_read(self.h, ms.ctypes.data, fr.ctypes.data, ln.ctypes.data, k)
+        return {s: (float(ms[i]), int(fr[i]), int(ln[i])) for i, s in enumerate(BATCH_STAGES)}
 
 
 def read_header(ric):

@@ -74,9 +74,15 @@ def main():
         pl = O.gray_plane(O.synth(w, h, 1, 0)[0], q)
         Q = O.quants(q + 20) if q else 0
         lam = O.quants(q + 13) if q else 0
-        for stage in (0, 1):
-            b = ref.bands(pl, L, lc, t, stage, Q, lam)
-            flat = np.concatenate([x.ravel() for x in b]).astype(np.int32)
+        # stage 0: after Transform, 1: after buildTree + LL TSUQ, 2: after the
+        # whole CodeBand; 3: the closed loop CodeBand -> TSUQi -> TransformI
+        # (src/lib/rududucodec.cpp:67-74), the reconstructed plane
+        for stage in (0, 1, 2, 3):
+            if stage == 3:
+                flat = ref.closed_loop(pl, L, lc, t, Q, lam, Q or 1)[0].ravel().astype(np.int32)
+            else:
+                b = ref.bands(pl, L, lc, t, stage, Q, lam)
+                flat = np.concatenate([x.ravel() for x in b]).astype(np.int32)
             nm = "bands_%dx%d_L%d_lc%d_t%d_q%d_s%d" % (w, h, L, lc, t, q, stage)
             np.save(os.path.join(HERE, nm + ".npy"), flat)
             out["bands"].append({"name": nm, "w": w, "h": h, "levels": L, "lc": lc, "trans": t, "q": q,

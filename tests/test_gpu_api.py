@@ -97,3 +97,26 @@ def test_tsuq(ric, port, t, thres):
         total += int((~zero).sum())
         assert np.array_equal(got[i], exp), i
     assert cnt.value == total
+
+
+def test_ring_timeout_is_an_error(ric, port):
+    """A fused level kernel whose LDS ring hand-off times out raises the
+    device status word, and the encode returns RIC_E_HIP instead of a corrupt
+    stream (fault injection: ric_diag_fault); the next encode is clean."""
+    w, h = 1024, 768
+    pix = ric.synth(w, h, 1, 1)
+    c = ric.Codec(w, h, 1)
+    lib = ric.lib()
+    lib.ric_diag_fault(1)
+    try:
+        with pytest.raises(ric.RicError) as ei:
+            c.compress(pix, 9, 0)
+        assert ei.value.rc == ric.RIC_E_HIP and "ring" in str(ei.value)
+        W = ric.Wavelet2D(w, h, 5, 1)
+        W.SetWeight(0)
+        pl = O.gray_plane(pix[0], 9)
+        with pytest.raises(ric.RicError):
+            W.TransformQuantize(pl, w, 0, 96, 36)
+    finally:
+        lib.ric_diag_fault(0)
+    assert c.compress(pix, 9, 0) == port.encode_ric(pix, 9, 0)

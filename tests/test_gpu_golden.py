@@ -38,17 +38,86 @@ def test_small_golden(ric, e):
 
 
 @pytest.mark.parametrize("e", G["bands"], ids=[e["name"] for e in G["bands"]])
-def test_band_dumps_golden(ric, e):
-    """Transform (stage 0) on the GPU equals the reference's band dump.  Stage 1
-    (buildTree) is checked through the encoded stream elsewhere."""
-    if e["stage"] != 0:
-        pytest.skip("stage-1 state checked via streams")
-    pl = O.gray_plane(ric.synth(e["w"], e["h"], 1, 0)[0], e["q"])
-    W = ric.Wavelet2D(e["w"], e["h"], e["levels"], e["lc"])
-    W.SetWeight(e["trans"])
-    W.Transform(pl, e["w"], e["trans"])
-    flat = np.concatenate([b.ravel() for b in W.bands()])
+@pytest.mark.parametrize("fused", [False, True], ids=["api", "fused"])
+def test_band_dumps_golden(ric, e, fused):
+    """The reference's band dumps through the CWavelet2D mirror on the GPU:
+    stage 0 Transform; stage 1 buildTree + LL TSUQ (Quantize, or the fused
+    TransformQuantize); stage 2 the whole CodeBand (the bands the zerotree scan
+    leaves, src/lib/bandcodec.cpp:510-588); stage 3 the closed loop CodeBand ->
+    TSUQi -> TransformI (src/lib/rududucodec.cpp:67-74)."""
+    w, h, t, st = e["w"], e["h"], e["trans"], e["stage"]
+    if fused and st != 1:
+        pytest.skip("the fused entry only exists for stage 1")
+    pl = O.gray_plane(ric.synth(w, h, 1, 0)[0], e["q"])
+    W = ric.Wavelet2D(w, h, e["levels"], e["lc"])
+    W.SetWeight(t)
+    if fused:
+        W.TransformQuantize(pl, w, t, e["quant"], e["lambda"])
+    else:
+        W.Transform(pl, w, t)
+    if st == 1 and not fused:
+        W.Quantize(e["quant"], e["lambda"])
+    if st >= 2:
+        buf = np.zeros(w * h * 4 + 4096, np.uint8)
+        m = ric.MuxCodec(buf, first_word=0)
+        W.CodeBand(m, e["quant"], e["lambda"])
+        m.endCoding()
+    if st == 3:
+        W.TSUQi(e["quant"] or 1)
+        out = np.zeros((h, w), np.int16)
+        W.TransformI(out, w, t)
+        flat = out.ravel().astype(np.int32)
+    else:
+        flat = np.concatenate([b.ravel() for b in W.bands()])
     assert np.array_equal(flat, np.load(os.path.join(GOLD, e["name"] + ".npy")))
+
+
+@pytest.mark.parametrize("w,h", [(300, 220), (129, 77), (640, 480)])
+@pytest.mark.parametrize("t", [0, 1])
+@pytest.mark.parametrize("L,lc", [(5, 1), (3, 0)])
+def test_closed_loop(ric, port, w, h, t, L, lc):
+    """CodeBand -> TSUQi -> TransformI through the C-ABI equals the oracle
+    (bands after TSUQi and the reconstructed plane)."""
+    pl = O.gray_plane(ric.synth(w, h, 1, 6)[0], 9)
+    exp_plane, exp_bands = port.closed_loop(pl, L, lc, t, 96, 36, 96)
+    W = ric.Wavelet2D(w, h, L, lc)
+    W.SetWeight(t)
+    W.Transform(pl, w, t)
+    buf = np.zeros(w * h * 4 + 4096, np.uint8)
+    m = ric.MuxCodec(buf, first_word=0)
+    W.CodeBand(m, 96, 36)
+    m.endCoding()
+    W.TSUQi(96)
+    for a, b in zip(W.bands(), exp_bands):
+        assert np.array_equal(a, b)
+    out = np.zeros((h, w), np.int16)
+    W.TransformI(out, w, t)
+    assert np.array_equal(out, exp_plane)
+
+
+@pytest.mark.parametrize("t", [0, 1])
+@pytest.mark.parametrize("quant", [96, 7, 1])
+def test_tsuqi(ric, port, t, quant):
+    """CWavelet2D::TSUQi (src/lib/wavelet2d.cpp:248-268, CBand::TSUQi
+    src/lib/band.h:94-107: v *= (C)(Quant / Weight), float32, at least 1) on
+    the raw transform (the k_dequant kernel), restated in numpy."""
+    w, h = 257, 130
+    pl = O.gray_plane(ric.synth(w, h, 1, 2)[0], 9)
+    W = ric.Wavelet2D(w, h, 5, 1)
+    W.SetWeight(t)
+    W.Transform(pl, w, t)
+    raw = W.bands()
+    W.TSUQi(quant)
+    got = W.bands()
+    for i in range(W.band_count()):
+        _, _, isint, wt = W.band_info(i)
+        q = quant if isint else int(np.int16(quant))
+        q = int(np.float32(q) / np.float32(wt))
+        q = q if isint else int(np.int16(q))
+        q = q or 1
+        v = raw[i].astype(np.int64) * q
+        exp = v.astype(np.int32) if isint else v.astype(np.int16).astype(np.int32)
+        assert np.array_equal(got[i], exp), i
 
 
 def test_c1_api_planes(ric):

@@ -13,7 +13,7 @@ SIZES = [(8, 8), (16, 16), (17, 23), (33, 47), (64, 48), (100, 101), (129, 77), 
 
 @pytest.mark.parametrize("w,h", SIZES)
 @pytest.mark.parametrize("t", [0, 1])
-@pytest.mark.parametrize("stage", [0, 1])
+@pytest.mark.parametrize("stage", [0, 1, 2])
 def test_bands(w, h, t, stage):
     pl = O.gray_plane(O.synth(w, h, 1, 3)[0], 9)
     # the top level is always `short` in the reference callers (Transform<short> only);
@@ -23,6 +23,20 @@ def test_bands(w, h, t, stage):
         b = REF.bands(pl, L, lc, t, stage, 96, 36)
         for x, y in zip(a, b):
             assert np.array_equal(x, y)
+
+
+@pytest.mark.parametrize("w,h", [(64, 48), (129, 77), (300, 220)])
+@pytest.mark.parametrize("t", [0, 1])
+@pytest.mark.parametrize("L,lc", [(5, 1), (3, 0)])
+def test_closed_loop(w, h, t, L, lc):
+    """CodeBand -> TSUQi -> TransformI on the bands CodeBand leaves behind
+    (the video driver's loop, src/lib/rududucodec.cpp:67-74)."""
+    pl = O.gray_plane(O.synth(w, h, 1, 6)[0], 9)
+    a, ab = O.port().closed_loop(pl, L, lc, t, 96, 36, 96)
+    b, bb = REF.closed_loop(pl, L, lc, t, 96, 36, 96)
+    assert np.array_equal(a, b)
+    for x, y in zip(ab, bb):
+        assert np.array_equal(x, y)
 
 
 @pytest.mark.parametrize("q", [0, 1, 5, 9, 20, 31])
