@@ -162,6 +162,11 @@ int ric_batch_roundtrip(ric_batch* b, const uint8_t* const* pix, int n, int q, i
  * 13..20 inverse level 0..7 (fused TSUQi), 21 pixel conversion out.  ms are
  * sums; frames = frames covered; launches = GPU launches (host: frames). */
 #define RIC_BATCH_STAGES 22
+/* Diagnostics: the batch's GPU stages alone, iters times over n <= slots
+ * device frames (forward levels + D2H, H2D + inverse levels of the bands just
+ * quantised, pixel output to pix_out if given); no host coding. */
+int ric_batch_diag_gpu(ric_batch* b, const uint8_t* const* pix, int n, int q, int trans, int iters,
+                       uint8_t* const* pix_out);
 int ric_batch_prof_enable(ric_batch* b, int on);
 int ric_batch_prof_read(ric_batch* b, double* ms, long* frames, long* launches, int n);
 

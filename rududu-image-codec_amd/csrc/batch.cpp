@@ -681,6 +681,27 @@ int ric_batch_roundtrip(ric_batch* b, const uint8_t* const* pix, int n, int q, i
 	return stream_err ? RIC_E_STREAM : RIC_OK;
 }
 
+// Diagnostics: the GPU stages alone, `iters` times over n frames (slot set
+// 0): pixel conversion + fused forward levels + D2H, then H2D + inverse
+// levels of the quantised bands just copied + pixel output (no host coding;
+// the decode's values are not a real decode).  For kernel timing
+// (ric_batch_prof_*, rocprofv3).
+int ric_batch_diag_gpu(ric_batch* b, const uint8_t* const* pix, int n, int q, int trans, int iters, uint8_t* const* pix_out)
+{
+	if (!b || !pix || n < 1 || n > b->slots || iters < 0) return RIC_E_ARG;
+	if (set_dev(b->device)) return RIC_E_HIP;
+	std::vector<int> qs(n, q);
+	for (int it = 0; it < iters; it++) {
+		int rc = gpu_encode_plane(b, 0, n, 0, pix, q, trans);
+		if (!rc) rc = gpu_decode_plane(b, 0, n, 0, qs.data(), trans);
+		if (!rc && pix_out) rc = gpu_pix_out(b, 0, n, qs.data(), pix_out, 1);
+		if (rc) return rc;
+	}
+	BCHK(hipStreamSynchronize(b->st));
+	b->prof.harvest();
+	return RIC_OK;
+}
+
 int ric_batch_prof_enable(ric_batch* b, int on)
 {
 	if (!b) return RIC_E_ARG;

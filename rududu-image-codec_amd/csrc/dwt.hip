@@ -2695,7 +2695,8 @@ int inv_launch_z(const Level& L, const Band& lls, const ZFrames& fr, int nz, con
 {
 	std::vector<InvArgs<TB, TB, TO>> v(nz);
 	for (int f = 0; f < nz; f++)
-		v[f] = inv_args<TB, TO>(L, lls, fr.arena + f * fr.astride, (char*)fr.out + f * fr.ostride, fr.po, q, S);
+		v[f] = inv_args<TB, TO>(L, lls, fr.arena + f * fr.astride, (char*)fr.out + f * fr.ostride, fr.po,
+		                        q ? q + 4 * f : nullptr, S);
 	if (zargs_put(z, v.data(), v.size() * sizeof(v[0]), st)) return -1;
 	const dim3 grid((L.w + kStripValid - 1) / kStripValid, (v[0].nseg + kWavesPerBlock - 1) / kWavesPerBlock, nz);
 	hipLaunchKernelGGL((k_inv_z<TRANS, TB, TB, TO, S>), grid, dim3(256), 0, st, (const InvArgs<TB, TB, TO>*)z.dev);

@@ -73,7 +73,8 @@ struct ZArgs {
 int zargs_put(ZArgs& z, const void* data, size_t bytes, hipStream_t st);
 void zargs_free(ZArgs& z);
 // The batched forms of launch_fwdq_level / launch_fwdq_gen_level /
-// launch_inv_level; 0 or -1 (HIP error).
+// launch_inv_level; 0 or -1 (HIP error).  The inverse takes 4 TSUQi factors
+// per frame (q + 4 f), or none.
 int launch_fwdq_level_z(const Pyramid& P, int l, const ZFrames& fr, int vec8, int vec16, const QuantParams& qp,
                         ZArgs& z, hipStream_t st);
 int launch_fwdq_gen_level_z(const Pyramid& P, int l, const ZFrames& fr, int vec8, const QuantParams& qp, int ll_on,

@@ -87,6 +87,7 @@ def lib():
         "ric_batch_decode": (_I, [_P, _P, _P, _I, _P, _I]),
         "ric_batch_roundtrip": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _P]),
         "ric_batch_prof_enable": (_I, [_P, _I]),
+        "ric_batch_diag_gpu": (_I, [_P, _P, _I, _I, _I, _I, _P]),
         "ric_batch_prof_read": (_I, [_P, _P, _P, _P, _I]),
     }
     for name, (res, args) in sig.items():
@@ -350,6 +351,11 @@ class Batch:
 
     def stream(self, i):
         return self._outs[i][:self._lens[i]].tobytes()
+
+    def diag_gpu(self, frames, q=9, trans=0, iters=1, pix_out=None):
+        """GPU stages only (kernel timing), see ric_batch_diag_gpu."""
+        po = _ptrs(pix_out) if pix_out is not None else None
+        _chk(lib().ric_batch_diag_gpu(self.h, _ptrs(frames), len(frames), q, trans, iters, po), "ric_batch_diag_gpu")
 
     def prof_enable(self, on=True):
         _chk(lib().ric_batch_prof_enable(self.h, int(on)), "ric_batch_prof_enable")
