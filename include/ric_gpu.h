@@ -98,6 +98,11 @@ int ric_band_count(ric_wavelet* w);
 int ric_band_info(ric_wavelet* w, int index, int* dimx, int* dimy, int* is_int, float* weight);
 int ric_band_read(ric_wavelet* w, int index, int32_t* host_out);
 int ric_band_write(ric_wavelet* w, int index, const int32_t* host_in);
+/* CBand::pBand (src/lib/band.h:58): a pointer to band `index` in this
+ * object's host mirror (row pitch *pitch samples, the band's C type), synced
+ * from the device; the mirror stays authoritative -- what the caller writes
+ * there is what the next GPU stage reads -- until a stage rewrites the bands. */
+int ric_band_host(ric_wavelet* w, int index, void** ptr, int* pitch);
 
 /* ------------------------------------------------------------- ric_mux */
 /* CMuxCodec(unsigned char* pStream, unsigned short firstWord)
@@ -106,6 +111,10 @@ int ric_mux_create_encoder(ric_mux** out, uint8_t* buf, size_t cap, uint16_t fir
 /* CMuxCodec(unsigned char* pStream) (src/lib/muxcodec.h:103): decoder over
  * len bytes of buf (the reference reads its payload from buf + 2). */
 int ric_mux_create_decoder(ric_mux** out, const uint8_t* buf, size_t len);
+/* CMuxCodec(unsigned char* pStream) exactly (src/lib/muxcodec.h:103,
+ * muxcodec.cpp:31-34): reads buf + 2 in place with no end, like the
+ * reference (the caller's buffer must hold the stream). */
+int ric_mux_create_decoder_inplace(ric_mux** out, const uint8_t* buf);
 /* CMuxCodec::endCoding() (src/lib/muxcodec.h:106): *len_out = end - buf. */
 int ric_mux_end(ric_mux* m, size_t* len_out);
 /* CMuxCodec::getSize() (src/lib/muxcodec.h:107) */

@@ -3,25 +3,41 @@
 //
 // Callers written against the reference (src/ric/ric.cpp:123-251,
 // src/lib/rududucodec.cpp:67-85) keep their code: same namespace, class and
-// method names, argument meaning and defaults:
+// member names, constructor forms, argument meaning and defaults:
 //
 //   rududu::CMuxCodec   (src/lib/muxcodec.h:66-130)
-//   rududu::CWavelet2D  (src/lib/wavelet2d.h:27-51)
+//   rududu::CWavelet2D  (src/lib/wavelet2d.h:27-51): DBand/HBand/VBand/LBand,
+//                       pLow/pHigh, Transform/TransformI/CodeBand/DecodeBand/
+//                       TSUQ/TSUQi/SetWeight/Stats
+//   rududu::CBand / CBandCodec (src/lib/band.h:37-161): the public fields
+//                       DimX..type, pParent/pChild, pBand, Mean/TSUQ/TSUQi/
+//                       Add/Clear/GetBand
 //   rududu::trans / cmode / band_t  (src/lib/utils.h:27-28, band.h:35)
 //
-// Differences, all explicit:
-//   * the band pyramid lives in GPU memory; DBand/HBand/VBand/LBand expose
-//     DimX/DimY/DimXAlign/type/Weight and read() instead of a raw pBand;
-//   * CMuxCodec takes an explicit capacity (the reference has none) and throws
-//     rududu::RicError on overflow or on any HIP failure -- there is no CPU
-//     fallback;
+// What differs, and why:
+//   * the pyramid lives in GPU memory.  CBand::pBand converts (C-style cast,
+//     `(short*) band.pBand`) to a pointer into a host mirror of the band, with
+//     row stride DimXAlign, synced from the device on that conversion; writes
+//     through it are what the next GPU operation on the pyramid reads.  The
+//     pointer is valid until the next CWavelet2D call.
+//   * DimXAlign is this pyramid's row pitch (64 samples), not the reference's
+//     32-byte rounding: it is the stride of pBand, as in the reference.
+//   * every failure (HIP error, no GPU, stream capacity) throws
+//     rududu::RicError: there is no CPU fallback.
+//   * the sub-level CWavelet2D objects of the pLow chain are views of the one
+//     pyramid: their bands and Stats are theirs, the transform / coding
+//     methods act on the whole pyramid and are called on the top object, as
+//     every reference caller does.
 //   * after CodeBand the bands hold the reference's post-CodeBand state
 //     (quantised sign-magnitude, the markers the zerotree scan consumes
 //     cleared), so TSUQi / TransformI after CodeBand match the reference.
 #pragma once
 
 #include <cstdint>
-#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <iostream>
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -34,6 +50,10 @@ typedef enum { encode, decode } cmode;
 typedef enum { cdf97 = 0, cdf53 = 1, haar = 2 } trans;
 typedef enum { sshort, sint } band_t;
 
+#ifndef ALIGN
+#define ALIGN 32
+#endif
+
 struct RicError : std::runtime_error {
 	int status;
 	RicError(int rc, const std::string& what)
@@ -45,15 +65,36 @@ inline void ric_check(int rc, const char* what)
 	if (rc != RIC_OK) throw RicError(rc, what);
 }
 
+// tag of the bounded decoder constructor
+struct bounded_t {};
+constexpr bounded_t bounded{};
+
 class CMuxCodec {
 public:
-	// encoder: CMuxCodec(unsigned char* pStream, unsigned short firstWord)
+	// CMuxCodec(unsigned char* pStream, unsigned short firstWord): encoder
+	// (src/lib/muxcodec.h:102).  Like the reference it takes no capacity: it
+	// codes into its own buffer (address space reserved, touched as it fills)
+	// and endCoding() copies the stream to pStream -- the caller's buffer must
+	// hold it, as with the reference.
+	CMuxCodec(unsigned char* pStream, unsigned short firstWord) : buf_(pStream)
+	{
+		own_.reset((unsigned char*)std::malloc(kOwnCap));
+		if (!own_) throw std::bad_alloc();
+		ric_check(ric_mux_create_encoder(&m_, own_.get(), kOwnCap, firstWord), "CMuxCodec(encoder)");
+	}
+	// the bounded encoder: writes pStream directly, at most capacity bytes
 	CMuxCodec(unsigned char* pStream, unsigned short firstWord, size_t capacity) : buf_(pStream)
 	{
 		ric_check(ric_mux_create_encoder(&m_, pStream, capacity, firstWord), "CMuxCodec(encoder)");
 	}
-	// decoder: CMuxCodec(unsigned char* pStream) -- reads from pStream + 2
-	CMuxCodec(const unsigned char* pStream, size_t length) : buf_(const_cast<unsigned char*>(pStream))
+	// CMuxCodec(unsigned char* pStream): decoder reading from pStream + 2 in
+	// place, with no end, like the reference (src/lib/muxcodec.h:103)
+	explicit CMuxCodec(const unsigned char* pStream) : buf_(const_cast<unsigned char*>(pStream))
+	{
+		ric_check(ric_mux_create_decoder_inplace(&m_, pStream), "CMuxCodec(decoder)");
+	}
+	// the bounded decoder: `length` bytes of pStream (payload at pStream + 2)
+	CMuxCodec(const unsigned char* pStream, size_t length, bounded_t) : buf_(const_cast<unsigned char*>(pStream))
 	{
 		ric_check(ric_mux_create_decoder(&m_, pStream, length), "CMuxCodec(decoder)");
 	}
@@ -65,135 +106,293 @@ public:
 	{
 		size_t n = 0;
 		ric_check(ric_mux_end(m_, &n), "endCoding");
+		if (own_) std::memcpy(buf_, own_.get(), n);
 		return buf_ + n;
 	}
 	unsigned int getSize() { return (unsigned int)ric_mux_size(m_); }
 	ric_mux* handle() { return m_; }
 
 private:
+	static constexpr size_t kOwnCap = (size_t)1 << 30;
+	struct Free { void operator()(unsigned char* p) const { std::free(p); } };
 	ric_mux* m_ = nullptr;
 	unsigned char* buf_;
+	std::unique_ptr<unsigned char, Free> own_;
 };
 
-class CWavelet2D;
-
-// Read-only view of one band of the GPU-resident pyramid (CBand's public
-// geometry fields, src/lib/band.h:43-59).
-class CBandView {
+// CBand::pBand: converts to a typed pointer into the band's host mirror
+// (synced from the device on conversion; see the header comment)
+class BandData {
 public:
-	unsigned int DimX = 0, DimY = 0, DimXAlign = 0;
-	band_t type = sshort;
-	float Weight = 1.f;
-	// the band's values as int32, row-major DimX * DimY (copied from HBM)
-	std::vector<int32_t> read() const
+	template <class T> operator T*() const
 	{
-		std::vector<int32_t> v((size_t)DimX * DimY);
-		ric_check(ric_band_read(w_, index_, v.data()), "band read");
-		return v;
+		if (!w_) return nullptr;
+		void* p = nullptr;
+		int pitch = 0;
+		ric_check(ric_band_host(w_, index_, &p, &pitch), "CBand::pBand");
+		return (T*)p;
 	}
-	void write(const std::vector<int32_t>& v)
-	{
-		ric_check(ric_band_write(w_, index_, v.data()), "band write");
-	}
+	explicit operator bool() const { return w_ != nullptr; }
 
 private:
 	friend class CWavelet2D;
+	friend class CBand;
 	ric_wavelet* w_ = nullptr;
 	int index_ = 0;
 };
 
+// CBand, src/lib/band.h:37-161: one band of the GPU-resident pyramid
+class CBand {
+public:
+	unsigned int DimX = 0;       // width of the band
+	unsigned int DimY = 0;       // height
+	unsigned int DimXAlign = 0;  // row stride of pBand (samples)
+	unsigned int BandSize = 0;   // DimXAlign * DimY
+	int Max = 0, Min = 0;        // set by TSUQ (band level)
+	unsigned int Dist = 0;
+	unsigned int Count = 0;      // set by TSUQ (band level)
+	float Weight = 1.f;
+	CBand* pParent = nullptr;    // the same band one level coarser
+	CBand* pChild = nullptr;     // the same band one level finer
+	CBand* pNeighbor[3] = {nullptr, nullptr, nullptr};
+	BandData pBand;
+	band_t type = sshort;
+
+	// src/lib/band.h:65-92, on the host mirror
+	template <class C> unsigned int TSUQ(int Quant, float Thres)
+	{
+		Quant = (int)(Quant / Weight);
+		if (Quant == 0) Quant = 1;
+		const int iQuant = (int)(1 << 16) / Quant;
+		const C T = (C)(Thres * Quant);
+		int mn = 0, mx = 0;
+		Count = 0;
+		C* p = (C*)pBand;
+		for (unsigned int j = 0; j < DimY; j++, p += DimXAlign)
+			for (unsigned int i = 0; i < DimX; i++) {
+				if ((unsigned int)(p[i] + T) <= (unsigned int)(2 * T)) {
+					p[i] = 0;
+				} else {
+					Count++;
+					p[i] = (C)((int)((unsigned int)p[i] * (unsigned int)iQuant + (1u << 15)) >> 16);
+					if (p[i] > mx) mx = p[i];
+					if (p[i] < mn) mn = p[i];
+				}
+			}
+		Min = mn;
+		Max = mx;
+		return Count;
+	}
+	// src/lib/band.h:94-107
+	template <class C> void TSUQi(C Quant)
+	{
+		Quant = (C)(Quant / Weight);
+		if (Quant == 0) Quant = 1;
+		C* p = (C*)pBand;
+		for (unsigned int j = 0; j < DimY; j++, p += DimXAlign)
+			for (unsigned int i = 0; i < DimX; i++) p[i] = (C)(p[i] * Quant);
+	}
+	// src/lib/band.h:116-132, the reference's arithmetic: the products in
+	// int, the sample-count square in unsigned (both wrap on big bands)
+	template <class C> void Mean(float& Mean, float& Var)
+	{
+		int64_t Sum = 0, SSum = 0;
+		const C* p = (const C*)pBand;
+		for (unsigned int j = 0; j < DimY; j++)
+			for (unsigned int i = 0; i < DimX; i++) {
+				const int v = p[i + j * DimXAlign];
+				Sum += v;
+				SSum += (int)((unsigned int)v * (unsigned int)v);
+			}
+		const unsigned int n = DimX * DimY;
+		Mean = (float)Sum * Weight / n;
+		Var = ((float)(SSum - Sum * Sum)) * Weight * Weight / (n * n);
+	}
+	// src/lib/band.h:135-141
+	template <class C> void Add(C val)
+	{
+		C* p = (C*)pBand;
+		for (unsigned int i = 0; i < BandSize; i++) p[i] += val;
+	}
+	// src/lib/band.cpp:162-167 (recurse: the finer bands too)
+	void Clear(bool recurse = false)
+	{
+		if (!pBand) return;
+		std::memset((void*)pBand, 0, (size_t)BandSize * (type == sint ? 4 : 2));
+		if (recurse && pChild) pChild->Clear(true);
+	}
+	// src/lib/band.h:145-155
+	template <class C, class T> void GetBand(T* pOut)
+	{
+		const C* pIn = (const C*)pBand;
+		const int add = 1 << (sizeof(T) * 8 - 1);
+		for (unsigned int j = 0; j < DimY; j++, pOut += DimX, pIn += DimXAlign)
+			for (unsigned int i = 0; i < DimX; i++) pOut[i] = (T)(pIn[i] + add);
+	}
+
+	// the band's values as int32, row-major DimX * DimY
+	std::vector<int32_t> read() const
+	{
+		std::vector<int32_t> v((size_t)DimX * DimY);
+		ric_check(ric_band_read(pBand.w_, pBand.index_, v.data()), "band read");
+		return v;
+	}
+	void write(const std::vector<int32_t>& v)
+	{
+		ric_check(ric_band_write(pBand.w_, pBand.index_, v.data()), "band write");
+	}
+};
+
+// the reference's CBandCodec adds the band coder to CBand; here the coder
+// runs inside CodeBand / DecodeBand and the band's public face is CBand's
+typedef CBand CBandCodec;
+
 class CWavelet2D {
 public:
 	// CWavelet2D(int x, int y, int level, int level_chg = 0, int Align = ALIGN)
-	CWavelet2D(int x, int y, int level, int level_chg = 0, int /*Align*/ = 32, int device = 0)
-		: DimX(x), DimY(y), levels_(level)
+	CWavelet2D(int x, int y, int level, int level_chg = 0, int /*Align*/ = ALIGN, int device = 0)
+		: DimX(x), DimY(y)
 	{
 		ric_check(ric_wavelet_create(&w_, x, y, level, level_chg, device), "CWavelet2D");
-		nbands_ = ric_band_count(w_);
-		nlev_ = (nbands_ - 1) / 3;
+		const int nb = ric_band_count(w_);
+		const int nlev = (nb - 1) / 3;
+		// the pLow chain: one view per level (src/lib/wavelet2d.cpp:47-81)
+		CWavelet2D* cur = this;
+		for (int l = 0; l < nlev; l++) {
+			cur->w_ = w_;
+			cur->level_ = l;
+			cur->bind(cur->DBand, 3 * l + 0);
+			cur->bind(cur->HBand, 3 * l + 1);
+			cur->bind(cur->VBand, 3 * l + 2);
+			if (l + 1 < nlev) {
+				CWavelet2D* low = new CWavelet2D(cur);
+				cur->pLow = low;
+				cur = low;
+			}
+		}
+		cur->bind(cur->LBand, nb - 1);
+		// parents: the same band one level coarser (src/lib/wavelet2d.cpp:53-59)
+		for (CWavelet2D* c = this; c->pLow; c = c->pLow) {
+			c->DBand.pParent = &c->pLow->DBand; c->pLow->DBand.pChild = &c->DBand;
+			c->HBand.pParent = &c->pLow->HBand; c->pLow->HBand.pChild = &c->HBand;
+			c->VBand.pParent = &c->pLow->VBand; c->pLow->VBand.pChild = &c->VBand;
+		}
 	}
-	~CWavelet2D() { ric_wavelet_destroy(w_); }
+	~CWavelet2D()
+	{
+		delete pLow;
+		if (!pHigh) ric_wavelet_destroy(w_);
+	}
 	CWavelet2D(const CWavelet2D&) = delete;
 	CWavelet2D& operator=(const CWavelet2D&) = delete;
 
 	// Transform<short>(short* pImage, int Stride, trans t): pImage on the host
 	void Transform(short* pImage, int Stride, trans t)
 	{
-		ric_check(ric_transform(w_, pImage, Stride, (int)t, 0), "Transform");
+		ric_check(ric_transform(top(), pImage, Stride, (int)t, 0), "Transform");
 	}
 	// TransformI<short>(short* pImageEnd, int Stride, trans t): like the
 	// reference, the END pointer (image + DimY * Stride) of the host image
 	void TransformI(short* pImageEnd, int Stride, trans t)
 	{
-		ric_check(ric_transform_inv(w_, pImageEnd - (long)DimY * Stride, Stride, (int)t, 0), "TransformI");
+		ric_check(ric_transform_inv(top(), pImageEnd - (long)DimY * Stride, Stride, (int)t, 0), "TransformI");
 	}
 	// device-pointer variants (images already resident in HBM)
 	void TransformDevice(const short* dImage, int Stride, trans t)
 	{
-		ric_check(ric_transform(w_, dImage, Stride, (int)t, 1), "Transform");
+		ric_check(ric_transform(top(), dImage, Stride, (int)t, 1), "Transform");
 	}
 	void TransformIDevice(short* dImage, int Stride, trans t)
 	{
-		ric_check(ric_transform_inv(w_, dImage, Stride, (int)t, 1), "TransformI");
+		ric_check(ric_transform_inv(top(), dImage, Stride, (int)t, 1), "TransformI");
 	}
-	void SetWeight(trans t, float baseWeight = 1.f) { ric_check(ric_set_weight(w_, (int)t, baseWeight), "SetWeight"); }
+	void SetWeight(trans t, float baseWeight = 1.f)
+	{
+		ric_check(ric_set_weight(top(), (int)t, baseWeight), "SetWeight");
+		refresh_weights();
+	}
 	void CodeBand(CMuxCodec* pCodec, int Quant, int lambda)
 	{
-		ric_check(ric_code_band(w_, pCodec->handle(), Quant, lambda), "CodeBand");
+		ric_check(ric_code_band(top(), pCodec->handle(), Quant, lambda), "CodeBand");
 	}
 	void DecodeBand(CMuxCodec* pCodec)
 	{
-		const int rc = ric_decode_band(w_, pCodec->handle());
+		const int rc = ric_decode_band(top(), pCodec->handle());
 		if (rc != RIC_OK && rc != RIC_E_STREAM) ric_check(rc, "DecodeBand");
 	}
 	unsigned int TSUQ(int Quant, float Thres)
 	{
 		unsigned int n = 0;
-		ric_check(ric_tsuq(w_, Quant, Thres, &n), "TSUQ");
+		ric_check(ric_tsuq(top(), Quant, Thres, &n), "TSUQ");
 		return n;
 	}
-	void TSUQi(int Quant) { ric_check(ric_tsuqi(w_, Quant), "TSUQi"); }
+	void TSUQi(int Quant) { ric_check(ric_tsuqi(top(), Quant), "TSUQi"); }
 
-	// CWavelet2D::Stats (src/lib/wavelet2d.cpp:270-303): weighted band variances
+	// CWavelet2D::Stats (src/lib/wavelet2d.cpp:270-303): band variances, D H V
+	// per level from this one down, then the coarsest L (CBand::Mean arithmetic)
 	void Stats()
 	{
-		static const char* nm[3] = {"D", "H", "V"};
-		for (int i = 0; i < nbands_; i++) {
-			CBandView b = band(i);
-			std::vector<int32_t> v = b.read();
-			int64_t sum = 0, ssum = 0;
-			for (int32_t x : v) { sum += x; ssum += (int64_t)x * x; }
-			const float n = (float)b.DimX * b.DimY;
-			const float var = ((float)(ssum - sum * sum)) * b.Weight * b.Weight / (n * n);
-			std::printf("%s :\t%g\n", i == nbands_ - 1 ? "L" : nm[i % 3], var);
+		float Mean = 0, Var = 0;
+		const char* nm[3] = {"D", "H", "V"};
+		CBand* b[3] = {&DBand, &HBand, &VBand};
+		for (int k = 0; k < 3; k++) {
+			if (b[k]->type == sshort) b[k]->Mean<short>(Mean, Var); else b[k]->Mean<int>(Mean, Var);
+			std::cout << nm[k] << " :\t" << Var << std::endl;
+		}
+		if (pLow) {
+			pLow->Stats();
+		} else {
+			if (LBand.type == sshort) LBand.Mean<short>(Mean, Var); else LBand.Mean<int>(Mean, Var);
+			std::cout << "L" << " :\t" << Var << std::endl;
 		}
 	}
 
-	// band i in canonical order: levels finest->coarsest D, H, V, then the LL
-	CBandView band(int i) const
-	{
-		CBandView v;
-		int dx, dy, isint;
-		float wt;
-		ric_check(ric_band_info(w_, i, &dx, &dy, &isint, &wt), "band_info");
-		v.DimX = dx; v.DimY = dy; v.type = isint ? sint : sshort; v.Weight = wt;
-		v.DimXAlign = ((dx * (isint ? 4 : 2) + 31) & -32) / (isint ? 4 : 2);
-		v.w_ = w_; v.index_ = i;
-		return v;
-	}
-	// the finest level's bands (DBand/HBand/VBand) and the coarsest LBand
-	CBandView DBand() const { return band(0); }
-	CBandView HBand() const { return band(1); }
-	CBandView VBand() const { return band(2); }
-	CBandView LBand() const { return band(nbands_ - 1); }
-	int levels() const { return nlev_; }
+	CBandCodec DBand;
+	CBandCodec HBand;
+	CBandCodec VBand;
+	CBandCodec LBand;
+	CWavelet2D* pLow = nullptr;
+	CWavelet2D* pHigh = nullptr;
+
+	int levels() const { int n = 1; for (const CWavelet2D* c = this; c->pLow; c = c->pLow) n++; return n; }
 	ric_wavelet* handle() { return w_; }
 
 	const int DimX, DimY;
 
 private:
+	explicit CWavelet2D(CWavelet2D* high) : pHigh(high), DimX(0), DimY(0) {}
+	ric_wavelet* top()
+	{
+		if (pHigh) throw RicError(RIC_E_ARG, "CWavelet2D: call on the top of the pLow chain");
+		return w_;
+	}
+	void bind(CBand& b, int index)
+	{
+		int dx, dy, isint;
+		float wt;
+		ric_check(ric_band_info(w_, index, &dx, &dy, &isint, &wt), "band_info");
+		b.DimX = dx; b.DimY = dy; b.type = isint ? sint : sshort; b.Weight = wt;
+		b.DimXAlign = (dx + 63) / 64 * 64;
+		if (b.DimXAlign == 0) b.DimXAlign = 64;
+		b.BandSize = b.DimXAlign * dy;
+		b.pBand.w_ = w_;
+		b.pBand.index_ = index;
+	}
+	void refresh_weights()
+	{
+		for (CWavelet2D* c = this; c; c = c->pLow) {
+			CBand* bs[4] = {&c->DBand, &c->HBand, &c->VBand, &c->LBand};
+			for (CBand* b : bs) {
+				if (!b->pBand) continue;
+				int dx, dy, isint;
+				float wt;
+				ric_check(ric_band_info(w_, b->pBand.index_, &dx, &dy, &isint, &wt), "band_info");
+				b->Weight = wt;
+			}
+		}
+	}
 	ric_wavelet* w_ = nullptr;
-	int levels_ = 0, nbands_ = 0, nlev_ = 0;
+	int level_ = 0;
 };
 
 }  // namespace rududu

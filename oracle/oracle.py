@@ -173,6 +173,34 @@ def quants(idx):
     return int(port().lib.ricor_quants(idx))
 
 
+def set_weight(n_bands, trans, base=1.0):
+    """CWavelet2D::SetWeight (src/lib/wavelet2d.cpp:1009-1032) in float32:
+    the weights of the canonical band order (per level D, H, V; then L)."""
+    f = np.float32
+    scale = f(1.149604398) * f(1.149604398) if trans == 0 else f(2.0)
+    out, nlev = [], (n_bands - 1) // 3
+    D, V, H, L = f(base) / scale, f(base), f(base), f(base) * scale
+    for l in range(nlev):
+        if l > 0:
+            D, V = V, L
+            H, L = V, V * scale
+        out += [D, H, V]
+    return out + [L]
+
+
+def band_variance(band, weight):
+    """CBand::Mean's variance (src/lib/band.h:116-132) with the reference's
+    C arithmetic: int products, int64 sums (wrapping), the sample count
+    squared in unsigned, float32 arithmetic."""
+    v = band.astype(np.int64)
+    s = int(v.sum())
+    ss = int(((v * v) & 0xFFFFFFFF).astype(np.uint32).view(np.int32).astype(np.int64).sum())
+    d = ((ss - s * s) + (1 << 63)) % (1 << 64) - (1 << 63)
+    n = (band.shape[0] * band.shape[1]) & 0xFFFFFFFF
+    w = np.float32(weight)
+    return np.float32(np.float32(d) * w * w / np.float32((n * n) & 0xFFFFFFFF))
+
+
 def gray_plane(pix, q):
     """Level shift of src/ric/ric.cpp:144-148 for one gray plane."""
     p = pix.astype(np.int32) - 128

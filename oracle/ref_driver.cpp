@@ -149,6 +149,31 @@ long ricref_closed_loop(const int16_t* img, int w, int h, int levels, int lc, in
 	return nb;
 }
 
+// CWavelet2D::Stats' numbers (src/lib/wavelet2d.cpp:270-303): CBand::Mean's
+// variance of every band after Transform (SetWeight(trans) weights),
+// canonical order.  Returns the number of bands.
+long ricref_stats(const int16_t* img, int w, int h, int levels, int lc, int trans, float* var_out)
+{
+	std::vector<short> buf(img, img + (size_t)w * h);
+	CWavelet2D wav(w, h, levels, lc);
+	wav.SetWeight((rududu::trans)trans);
+	wav.Transform(buf.data(), w, (rududu::trans)trans);
+	long n = 0;
+	auto one = [&](CBand& b) {
+		float mean = 0, var = 0;
+		if (b.type == sshort) b.Mean<short>(mean, var); else b.Mean<int>(mean, var);
+		var_out[n++] = var;
+	};
+	CWavelet2D* c = &wav;
+	while (true) {
+		one(c->DBand); one(c->HBand); one(c->VBand);
+		if (!c->pLow) break;
+		c = c->pLow;
+	}
+	one(c->LBand);
+	return n;
+}
+
 // Encodes nplanes int16 planes (coded in the given order) into one stream.
 // Returns the full coder buffer length (endCoding() - buf, including the two
 // leading bytes that the .ric file drops), or -needed if cap is too small.

@@ -214,28 +214,6 @@ int inverse(ric_wavelet* w, int16_t* dimg, long stride, int trans)
 	return RIC_OK;
 }
 
-int inverse_deq(ric_wavelet* w, int16_t* dimg, long stride, int trans, int quant)
-{
-	Pyramid& P = w->P;
-	int rc = to_device(w);
-	if (rc) return rc;
-	w->prof.begin(S_INV, w->st);
-	for (int l = P.nlev - 1; l >= 0; l--) {
-		const Level& L = P.L[l];
-		void* out;
-		long po;
-		int out_int;
-		if (l == 0) { out = dimg; po = stride; out_int = 0; }
-		else { const Band& LL = P.L[l - 1].b[BL]; out = w->d_arena + LL.off; po = LL.pitch; out_int = LL.is_int; }
-		const int q[4] = {tsuqi_factor(L.b[BD], quant), tsuqi_factor(L.b[BH], quant), tsuqi_factor(L.b[BV], quant),
-		                  l + 1 == P.nlev ? tsuqi_factor(L.b[BL], quant) : 1};
-		launch_inv_level(L, L.b[BL], w->d_arena, out, po, out_int, trans, w->st, q);
-	}
-	w->prof.end(S_INV, w->st);
-	HIPCHK(hipGetLastError());
-	return RIC_OK;
-}
-
 void ll_params(ric_wavelet* w, int quant, int& Q, int& iQ, int& T0) { ll_params(w->P, quant, Q, iQ, T0); }
 void quant_ll(ric_wavelet* w, int quant)
 {
@@ -250,6 +228,8 @@ void quant_ll(ric_wavelet* w, int quant)
 int quantize_gpu(ric_wavelet* w, int quant, int lambda)
 {
 	Pyramid& P = w->P;
+	int rc = to_device(w);   // bands a caller wrote through CBand::pBand
+	if (rc) return rc;
 	// buildTree on every level, finest first (bandcodec.cpp:239-319)
 	int qin = quant;
 	w->prof.begin(S_QUANT, w->st);
@@ -384,6 +364,51 @@ int decode_band(ric_wavelet* w, Mux& m)
 	}
 	w->prof.host(S_HDEC, now_ms() - t0);
 	w->host_valid = true;
+	return m.overflow() ? RIC_E_STREAM : RIC_OK;
+}
+
+// DecodeBand + TSUQi + TransformI of one plane, pipelined by level (the
+// codec's decode path).  The reference decodes coarse -> fine
+// (src/lib/wavelet2d.cpp:179-222) and inverts coarsest level first (:960-990),
+// so as soon as the host has decoded a level's V, H, D bands they go to the
+// device and that level's inverse (TSUQi fused, quant != 0) is queued, while
+// the host decodes the next finer level.  The stream is synchronised once,
+// at the end.
+int decode_inverse_pipelined(ric_wavelet* w, Mux& m, int16_t* dimg, long stride, int trans, int quant)
+{
+	Pyramid& P = w->P;
+	const double t0 = now_ms();
+	pred_decode(m, view(w, P.coarsest_ll()));
+	for (int l = P.nlev - 1; l >= 0; l--) {
+		const int order[3] = {BV, BH, BD};
+		for (int k = 0; k < 3; k++) {
+			BandView par;
+			if (l + 1 < P.nlev) par = view(w, P.L[l + 1].b[order[k]]);
+			tree_decode_fast(m, view(w, P.L[l].b[order[k]]), par, l == 0, l > 0);
+		}
+		// level l's D, H, V are contiguous in region A; the coarsest LL ends it
+		const Level& L = P.L[l];
+		const size_t lo = L.b[BD].off;
+		const size_t hi = l + 1 == P.nlev ? P.a_end : L.b[BV].off + L.b[BV].bytes();
+		HIPCHK(hipMemcpyAsync(w->d_arena + lo, w->h_arena + lo, hi - lo, hipMemcpyHostToDevice, w->st));
+		void* out;
+		long po;
+		int out_int;
+		if (l == 0) { out = dimg; po = stride; out_int = 0; }
+		else { const Band& LL = P.L[l - 1].b[BL]; out = w->d_arena + LL.off; po = LL.pitch; out_int = LL.is_int; }
+		if (quant) {
+			const int q[4] = {tsuqi_factor(L.b[BD], quant), tsuqi_factor(L.b[BH], quant), tsuqi_factor(L.b[BV], quant),
+			                  l + 1 == P.nlev ? tsuqi_factor(L.b[BL], quant) : 1};
+			launch_inv_level(L, L.b[BL], w->d_arena, out, po, out_int, trans, w->st, q);
+		} else {
+			launch_inv_level(L, L.b[BL], w->d_arena, out, po, out_int, trans, w->st);
+		}
+	}
+	HIPCHK(hipGetLastError());
+	w->prof.host(S_HDEC, now_ms() - t0);
+	// the host mirror is rewritten by the next DecodeBand: wait for the copies
+	HIPCHK(hipStreamSynchronize(w->st));
+	w->host_valid = false;    // the device now holds these bands
 	return m.overflow() ? RIC_E_STREAM : RIC_OK;
 }
 
@@ -682,6 +707,22 @@ int ric_band_read(ric_wavelet* w, int index, int32_t* out)
 	return RIC_OK;
 }
 
+int ric_band_host(ric_wavelet* w, int index, void** ptr, int* pitch)
+{
+	if (!w || !ptr || index < 0 || index >= w->P.nbands()) return RIC_E_ARG;
+	if (set_dev(w->device)) return RIC_E_HIP;
+	if (flush_pending(w)) return RIC_E_HIP;
+	if (!w->host_valid) {
+		int rc = to_host(w, false);
+		if (rc) return rc;
+		w->host_valid = true;   // the mirror is authoritative until the next GPU stage
+	}
+	const Band& B = w->P.band(index);
+	*ptr = w->h_arena + B.off;
+	if (pitch) *pitch = B.pitch;
+	return RIC_OK;
+}
+
 int ric_band_write(ric_wavelet* w, int index, const int32_t* in)
 {
 	if (!w || !in || index < 0 || index >= w->P.nbands()) return RIC_E_ARG;
@@ -720,6 +761,16 @@ int ric_mux_create_decoder(ric_mux** out, const uint8_t* buf, size_t len)
 	ric_mux* m = new ric_mux;
 	m->encoder = false;
 	m->m.init_decoder(buf, len);
+	*out = m;
+	return RIC_OK;
+}
+
+int ric_mux_create_decoder_inplace(ric_mux** out, const uint8_t* buf)
+{
+	if (!out || !buf) return RIC_E_ARG;
+	ric_mux* m = new ric_mux;
+	m->encoder = false;
+	m->m.init_decoder_inplace(buf);
 	*out = m;
 	return RIC_OK;
 }
@@ -866,18 +917,14 @@ int ric_codec_decode(ric_codec* c, const uint8_t* ric, size_t len, int dither,
 	m.init_decoder(buf, pay + 2);
 	w->P.set_weight(trans);
 	const long plane = c->pitch * c->h;
+	int stream_rc = RIC_OK;
 	for (int p = 0; p < c->channels; p++) {
 		const int boost = p ? 8 : 0;
-		rc = decode_band(w, m);
+		rc = decode_inverse_pipelined(w, m, c->d_planes + p * plane, c->pitch, trans, q ? ric_quants(q + 20 + boost) : 0);
 		if (rc && rc != RIC_E_STREAM) return rc;
-		GpuSection gs(c->device);
-		rc = to_device(w);
-		if (rc) return rc;
-		rc = q ? inverse_deq(w, c->d_planes + p * plane, c->pitch, trans, ric_quants(q + 20 + boost))
-		       : inverse(w, c->d_planes + p * plane, c->pitch, trans);
-		if (rc) return rc;
-		HIPCHK(hipStreamSynchronize(w->st));
+		if (rc) stream_rc = rc;
 	}
+	(void)stream_rc;
 	if (dither && q && c->channels == 1) {
 		// dither() is a serial error diffusion (src/ric/ric.cpp:51-74): host side
 		std::vector<int16_t> img((size_t)c->w * c->h);

@@ -13,6 +13,7 @@
 // the sign bit that follows it are read as one (k + 1)-bit chunk (no range
 // decoding happens between them, so the same bytes are read).
 #include "entropy.h"
+#include "coder_tables.h"
 
 #include <cstring>
 #include <vector>
@@ -23,26 +24,14 @@ namespace ric {
 
 namespace {
 
-const uint16_t kBitThresD[11] = {2584, 1512, 745, 371, 185, 92, 46, 23, 12, 6, 3};
-const uint16_t kGeoThresD[11] = {1512, 2584, 3351, 3725, 3911, 4004, 4050, 4073, 4084, 4090, 4093};
-const uint8_t kGeoKD[25] = {0,0,0,0,0,0,0,0,0,0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,14};
-const uint8_t kGeoShiftD[25] = {10,9,8,7,6,5,4,3,2,1,1,1,1,1,1,1,1,1,1,1,1,1,1,1,1};
-const uint8_t kCnkLenD[16][8] = {
-	{0,0,0,0,0,0,0,0},{1,0,0,0,0,0,0,0},{2,2,0,0,0,0,0,0},{2,3,2,0,0,0,0,0},
-	{3,4,4,3,0,0,0,0},{3,4,5,4,3,0,0,0},{3,5,6,6,5,3,0,0},{3,5,6,7,6,5,3,0},
-	{4,6,7,7,7,7,6,4},{4,6,7,8,8,8,7,6},{4,6,8,9,9,9,9,8},{4,7,8,9,10,10,10,9},
-	{4,7,9,10,11,11,11,11},{4,7,9,10,11,12,12,12},{4,7,9,11,12,13,13,13},{4,7,10,11,13,13,14,14}};
-const uint16_t kCnkLostD[16][8] = {
-	{0,0,0,0,0,0,0,0},{0,0,0,0,0,0,0,0},{1,1,0,0,0,0,0,0},{0,2,0,0,0,0,0,0},
-	{3,6,6,3,0,0,0,0},{2,1,12,1,2,0,0,0},{1,11,29,29,11,1,0,0},{0,4,8,58,8,4,0,0},
-	{7,28,44,2,2,44,28,7},{6,19,8,46,4,46,8,19},{5,9,91,182,50,50,182,91},
-	{4,62,36,17,232,100,232,17},{3,50,226,309,761,332,332,761},{2,37,148,23,46,1093,664,1093},
-	{1,23,57,683,1093,3187,1757,1757},{0,8,464,228,3824,184,4944,3514}};
-const uint8_t kKConv2D[9][16] = {
-	{15}, {7,15}, {4,10,15}, {3,7,11,15}, {2,4,7,10,12,15}, {1,3,5,7,9,11,13,15},
-	{1,3,4,6,8,10,11,13,15}, {0,2,3,4,6,7,8,10,11,12,14,15},
-	{0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,15}};
-const uint8_t kKConv1D[16] = {0,1,2,3,0,4,0,5,6,0,0,7,0,0,0,8};
+using namespace tables;
+
+// The longest unary run of a valid stream: a `short` band stores the
+// sign-magnitude 2|q| + sign in 16 bits, so |q| - 1 < 2^15; an `int` band
+// (the coarsest level) is guarded at 2^20.  Past that a stream is corrupt and
+// the run is cut: a hostile stream cannot keep the decoder spinning for long
+// (the reference has no guard), and every valid stream decodes the same.
+template <typename C> constexpr uint32_t kUnaryMax = sizeof(C) == 2 ? (1u << 15) : (1u << 20);
 
 // binomials C(n, r) for n < 17
 struct Binom {
@@ -168,8 +157,8 @@ struct DecCore {
 	}
 	RIC_AI uint32_t enum_code(uint32_t k, uint32_t nmax)       // code part of enumDecode, muxcodec.cpp:391-393
 	{
-		const uint32_t lost = kCnkLostD[nmax - 1][k - 1];
-		uint32_t c = bits(kCnkLenD[nmax - 1][k - 1] - 1);
+		const uint32_t lost = kCnkLost[nmax - 1][k - 1];
+		uint32_t c = bits(kCnkLen[nmax - 1][k - 1] - 1);
 		if (c >= lost) c = ((c << 1) | bits(1)) - lost;
 		return c;
 	}
@@ -217,8 +206,8 @@ struct BitM {                                                   // CBitCodec
 		const int sh = shift[c];
 		freq[c] = (uint16_t)(freq[c] + (sym << (9 - sh)) - (freq[c] >> (3 + sh)));
 		sym ^= mps[c];
-		if ((uint16_t)(freq[c] - kBitThresD[sh + 1]) > kBitThresD[sh] - kBitThresD[sh + 1]) {
-			if (freq[c] > kBitThresD[sh]) {
+		if ((uint16_t)(freq[c] - kBitThres[sh + 1]) > kBitThres[sh] - kBitThres[sh + 1]) {
+			if (freq[c] > kBitThres[sh]) {
 				if (sh == 0) { mps[c] ^= 1; freq[c] = (uint16_t)(4096 - freq[c]); shift[c] = 1; }
 				else shift[c]--;
 			} else if (sh < 9) shift[c]++;
@@ -234,27 +223,29 @@ struct GeoM {                                                   // CGeomCodec
 	{
 		for (int c = 0; c < 16; c++) {
 			idx[c] = kinit[c];
-			freq[c] = idx[c] >= 9 ? 2048 : (uint16_t)((kGeoThresD[idx[c] - 1] + kGeoThresD[idx[c]]) >> 1);
+			freq[c] = idx[c] >= 9 ? 2048 : (uint16_t)((kGeoThres[idx[c] - 1] + kGeoThres[idx[c]]) >> 1);
 		}
 	}
 	RIC_AI void adapt(int c, int s)
 	{
 		freq[c] += (4096 - freq[c]) >> (3 + s);
-		if ((uint16_t)(freq[c] - kGeoThresD[s - 1]) > kGeoThresD[s] - kGeoThresD[s - 1]) {
-			if (freq[c] < kGeoThresD[s - 1]) { if (idx[c] < 24) idx[c]++; }
+		if ((uint16_t)(freq[c] - kGeoThres[s - 1]) > kGeoThres[s] - kGeoThres[s - 1]) {
+			if (freq[c] < kGeoThres[s - 1]) { if (idx[c] < 24) idx[c]++; }
 			else if (idx[c] > 0) idx[c]--;
 			if (idx[c] >= 9) freq[c] = 2048;
 		}
 	}
-	// the signed coefficient: geometric magnitude - 1 then the raw sign bit
+	// the signed coefficient: geometric magnitude - 1 then the raw sign bit.
+	// LMAX: the longest unary run a valid stream can hold (see kUnaryMax)
+	template <uint32_t LMAX>
 	RIC_AI int decode_signed(DecCore& d, int c)
 	{
-		const uint32_t k = kGeoKD[idx[c]], f = freq[c];
-		const int s = kGeoShiftD[idx[c]];
+		const uint32_t k = kGeoK[idx[c]], f = freq[c];
+		const int s = kGeoShift[idx[c]];
 		uint32_t l = 0;
 		while (d.get_bit(f)) {
 			freq[c] -= freq[c] >> (3 + s);
-			if (++l > (1u << 20)) break;            // corrupt-stream guard
+			if (++l > LMAX) break;                  // corrupt-stream guard
 		}
 		const uint32_t v = d.bits(k + 1);
 		const uint32_t sym = (l << k) | (v >> 1);
@@ -264,8 +255,8 @@ struct GeoM {                                                   // CGeomCodec
 	}
 	RIC_AI uint32_t decode(DecCore& d, int c)
 	{
-		const uint32_t k = kGeoKD[idx[c]], f = freq[c];
-		const int s = kGeoShiftD[idx[c]];
+		const uint32_t k = kGeoK[idx[c]], f = freq[c];
+		const int s = kGeoShift[idx[c]];
 		uint32_t l = 0;
 		while (d.get_bit(f)) {
 			freq[c] -= freq[c] >> (3 + s);
@@ -285,20 +276,21 @@ struct GeoReg {
 	uint32_t freq, idx;
 	RIC_AI void load(const GeoM& g, int c) { freq = g.freq[c]; idx = g.idx[c]; }
 	RIC_AI void store(GeoM& g, int c) const { g.freq[c] = (uint16_t)freq; g.idx[c] = (uint8_t)idx; }
+	template <uint32_t LMAX>
 	RIC_AI int decode_signed(DecCore& d)                         // GeoM::decode_signed
 	{
-		const uint32_t k = kGeoKD[idx], f = freq;
-		const int s = kGeoShiftD[idx];
+		const uint32_t k = kGeoK[idx], f = freq;
+		const int s = kGeoShift[idx];
 		uint32_t fr = freq, l = 0;
 		while (d.get_bit(f)) {
 			fr -= fr >> (3 + s);
-			if (++l > (1u << 20)) break;            // corrupt-stream guard
+			if (++l > LMAX) break;                  // corrupt-stream guard
 		}
 		const uint32_t v = d.bits(k + 1);
 		const uint32_t sym = (l << k) | (v >> 1);
 		fr = (uint16_t)(fr + ((4096 - fr) >> (3 + s)));             // adapt
-		if ((uint16_t)(fr - kGeoThresD[s - 1]) > kGeoThresD[s] - kGeoThresD[s - 1]) {
-			if (fr < kGeoThresD[s - 1]) { if (idx < 24) idx++; }
+		if ((uint16_t)(fr - kGeoThres[s - 1]) > kGeoThres[s] - kGeoThres[s - 1]) {
+			if (fr < kGeoThres[s - 1]) { if (idx < 24) idx++; }
 			else if (idx > 0) idx--;
 			if (idx >= 9) fr = 2048;
 		}
@@ -338,7 +330,7 @@ RIC_AI int block_full_dec(DecCore& d, GeoM& g, C* blk, long st, int idx)
 			const int b = 31 - __builtin_clz(sig);      // bit 15 = raster position 0
 			sig &= ~(1u << b);
 			const int i = 15 - b;
-			blk[(i >> 2) * st + (i & 3)] = (C)tr<SH>(r.decode_signed(d));
+			blk[(i >> 2) * st + (i & 3)] = (C)tr<SH>(r.template decode_signed<kUnaryMax<C>>(d));
 		}
 		r.store(g, gc);
 	}
@@ -354,10 +346,10 @@ void block_edge_dec(DecCore& d, GeoM& g, C* blk, long st, int w, int h)
 	if (k > cnt) k = cnt;                                       // corrupt-stream guard
 	if (HIGH || k != 0) {
 		uint32_t sig = k != cnt ? d.enum_n(k, cnt) : (1u << cnt) - 1;
-		const int gc = kKConv2D[kKConv1D[cnt]][k - 1];
+		const int gc = kKConv2[kKConv1[cnt]][k - 1];
 		for (int j = 0; j < h; j++)
 			for (int i = 0; i < w; i++) {
-				if (sig & (1u << (cnt - 1))) blk[j * st + i] = (C)tr<SH>(g.decode_signed(d, gc));
+				if (sig & (1u << (cnt - 1))) blk[j * st + i] = (C)tr<SH>(g.template decode_signed<kUnaryMax<C>>(d, gc));
 				sig <<= 1;
 			}
 	}

@@ -5,6 +5,7 @@
 // codeBin / bitsCode / normalize_enc / flushBuffer (src/lib/muxcodec.h:156-231,
 // muxcodec.cpp:63-74, 536-570).  Output is byte-identical to the reference's tree<encode>.
 #include "entropy.h"
+#include "coder_tables.h"
 #include "symbols.h"
 
 namespace ric {
@@ -13,10 +14,7 @@ namespace ric {
 
 namespace {
 
-const uint16_t kBitThresE[11] = {2584, 1512, 745, 371, 185, 92, 46, 23, 12, 6, 3};
-const uint16_t kGeoThresE[11] = {1512, 2584, 3351, 3725, 3911, 4004, 4050, 4073, 4084, 4090, 4093};
-const uint8_t kGeoKE[25] = {0,0,0,0,0,0,0,0,0,0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,14};
-const uint8_t kGeoShiftE[25] = {10,9,8,7,6,5,4,3,2,1,1,1,1,1,1,1,1,1,1,1,1,1,1,1,1};
+using namespace tables;
 
 #define RIC_AI __attribute__((always_inline)) inline
 
@@ -75,8 +73,8 @@ struct BitE {                                             // CBitCodec::code
 		e.bin(freq[c], s ^ 1);
 		const int sh = shift[c];
 		freq[c] = (uint16_t)(freq[c] + (s << (9 - sh)) - (freq[c] >> (3 + sh)));
-		if ((uint16_t)(freq[c] - kBitThresE[sh + 1]) > kBitThresE[sh] - kBitThresE[sh + 1]) {
-			if (freq[c] > kBitThresE[sh]) {
+		if ((uint16_t)(freq[c] - kBitThres[sh + 1]) > kBitThres[sh] - kBitThres[sh + 1]) {
+			if (freq[c] > kBitThres[sh]) {
 				if (sh == 0) { mps[c] ^= 1; freq[c] = (uint16_t)(4096 - freq[c]); shift[c] = 1; }
 				else shift[c]--;
 			} else if (sh < 9) shift[c]++;
@@ -91,14 +89,14 @@ struct GeoE {                                             // CGeomCodec::code
 	{
 		for (int c = 0; c < 16; c++) {
 			idx[c] = kinit[c];
-			freq[c] = idx[c] >= 9 ? 2048 : (uint16_t)((kGeoThresE[idx[c] - 1] + kGeoThresE[idx[c]]) >> 1);
+			freq[c] = idx[c] >= 9 ? 2048 : (uint16_t)((kGeoThres[idx[c] - 1] + kGeoThres[idx[c]]) >> 1);
 		}
 	}
 	// magnitude - 1 then the raw sign bit (remainder and sign as one chunk)
 	RIC_AI void code_signed(EncCore& e, uint32_t sym, uint32_t sign, int c)
 	{
-		const uint32_t k = kGeoKE[idx[c]], f = freq[c];
-		const int s = kGeoShiftE[idx[c]];
+		const uint32_t k = kGeoK[idx[c]], f = freq[c];
+		const int s = kGeoShift[idx[c]];
 		for (uint32_t l = sym >> k; l > 0; l--) {
 			e.bin(f, 1);
 			freq[c] -= freq[c] >> (3 + s);
@@ -106,8 +104,8 @@ struct GeoE {                                             // CGeomCodec::code
 		e.bin(f, 0);
 		e.bits(((sym & ((1u << k) - 1)) << 1) | sign, k + 1);
 		freq[c] += (4096 - freq[c]) >> (3 + s);
-		if ((uint16_t)(freq[c] - kGeoThresE[s - 1]) > kGeoThresE[s] - kGeoThresE[s - 1]) {
-			if (freq[c] < kGeoThresE[s - 1]) { if (idx[c] < 24) idx[c]++; }
+		if ((uint16_t)(freq[c] - kGeoThres[s - 1]) > kGeoThres[s] - kGeoThres[s - 1]) {
+			if (freq[c] < kGeoThres[s - 1]) { if (idx[c] < 24) idx[c]++; }
 			else if (idx[c] > 0) idx[c]--;
 			if (idx[c] >= 9) freq[c] = 2048;
 		}
@@ -122,8 +120,8 @@ struct GeoRegE {
 	RIC_AI void store(GeoE& g, int c) const { g.freq[c] = (uint16_t)freq; g.idx[c] = (uint8_t)idx; }
 	RIC_AI void code_signed(EncCore& e, uint32_t sym, uint32_t sign)   // GeoE::code_signed
 	{
-		const uint32_t k = kGeoKE[idx], f = freq;
-		const int s = kGeoShiftE[idx];
+		const uint32_t k = kGeoK[idx], f = freq;
+		const int s = kGeoShift[idx];
 		uint32_t fr = freq;
 		for (uint32_t l = sym >> k; l > 0; l--) {
 			e.bin(f, 1);
@@ -132,8 +130,8 @@ struct GeoRegE {
 		e.bin(f, 0);
 		e.bits(((sym & ((1u << k) - 1)) << 1) | sign, k + 1);
 		fr = (uint16_t)(fr + ((4096 - fr) >> (3 + s)));
-		if ((uint16_t)(fr - kGeoThresE[s - 1]) > kGeoThresE[s] - kGeoThresE[s - 1]) {
-			if (fr < kGeoThresE[s - 1]) { if (idx < 24) idx++; }
+		if ((uint16_t)(fr - kGeoThres[s - 1]) > kGeoThres[s] - kGeoThres[s - 1]) {
+			if (fr < kGeoThres[s - 1]) { if (idx < 24) idx++; }
 			else if (idx > 0) idx--;
 			if (idx >= 9) fr = 2048;
 		}

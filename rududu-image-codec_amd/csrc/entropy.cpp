@@ -1,5 +1,6 @@
 // entropy.cpp -- host serial coder of the .ric path (see entropy.h).
 #include "entropy.h"
+#include "coder_tables.h"
 #include "symbols.h"
 
 #include <cstdlib>
@@ -10,6 +11,8 @@ namespace ric {
 #include "huff_tables.inc"
 
 namespace {
+
+using namespace tables;
 
 // Cnk[k][n] = C(n, k + 1) (src/lib/muxcodec.cpp:282-292), built once.
 struct CnkTable {
@@ -27,19 +30,6 @@ struct CnkTable {
 	}
 };
 const CnkTable kCnk;
-
-// src/lib/muxcodec.cpp:294-332 (format constants)
-const uint8_t kCnkLen[16][8] = {
-	{0,0,0,0,0,0,0,0},{1,0,0,0,0,0,0,0},{2,2,0,0,0,0,0,0},{2,3,2,0,0,0,0,0},
-	{3,4,4,3,0,0,0,0},{3,4,5,4,3,0,0,0},{3,5,6,6,5,3,0,0},{3,5,6,7,6,5,3,0},
-	{4,6,7,7,7,7,6,4},{4,6,7,8,8,8,7,6},{4,6,8,9,9,9,9,8},{4,7,8,9,10,10,10,9},
-	{4,7,9,10,11,11,11,11},{4,7,9,10,11,12,12,12},{4,7,9,11,12,13,13,13},{4,7,10,11,13,13,14,14}};
-const uint16_t kCnkLost[16][8] = {
-	{0,0,0,0,0,0,0,0},{0,0,0,0,0,0,0,0},{1,1,0,0,0,0,0,0},{0,2,0,0,0,0,0,0},
-	{3,6,6,3,0,0,0,0},{2,1,12,1,2,0,0,0},{1,11,29,29,11,1,0,0},{0,4,8,58,8,4,0,0},
-	{7,28,44,2,2,44,28,7},{6,19,8,46,4,46,8,19},{5,9,91,182,50,50,182,91},
-	{4,62,36,17,232,100,232,17},{3,50,226,309,761,332,332,761},{2,37,148,23,46,1093,664,1093},
-	{1,23,57,683,1093,3187,1757,1757},{0,8,464,228,3824,184,4944,3514}};
 
 // taboo code tables for n = 2 (initTaboo(2), src/lib/muxcodec.cpp:113-129)
 struct TabooTable {
@@ -81,12 +71,6 @@ struct HuffLut {
 };
 const HuffLut kHuffLut;
 
-const uint16_t kBitThres[11] = {2584, 1512, 745, 371, 185, 92, 46, 23, 12, 6, 3};   // bitcodec.cpp:40-42
-const uint16_t kGeoThres[11] = {1512, 2584, 3351, 3725, 3911, 4004, 4050, 4073, 4084, 4090, 4093};  // geomcodec.cpp:44-46
-// K and shift (geomcodec.cpp:48-54); entry 24 guards an index the reference
-// never reaches on valid data.
-const uint8_t kGeoK[25] = {0,0,0,0,0,0,0,0,0,0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,14};
-const uint8_t kGeoShift[25] = {10,9,8,7,6,5,4,3,2,1,1,1,1,1,1,1,1,1,1,1,1,1,1,1,1};
 
 constexpr size_t kDecPad = 1 << 16;
 
@@ -139,6 +123,18 @@ void Mux::init_decoder_payload(const uint8_t* payload, size_t n)
 	range_ = 1u << 16;
 	nbits_ = 0; buffer_ = 0; overflow_ = false;
 	init_ = owned_ + 2; p_ = owned_ + 2;
+	code_ = low_ = ((uint32_t)p_[0] << 8) | p_[1];
+	p_ += 2;
+}
+
+void Mux::init_decoder_inplace(const uint8_t* buf)
+{
+	// no copy and no end: the reference's CMuxCodec(pStream) contract
+	base_ = const_cast<uint8_t*>(buf);
+	limit_ = reinterpret_cast<uint8_t*>(UINTPTR_MAX);
+	range_ = 1u << 16;
+	nbits_ = 0; buffer_ = 0; overflow_ = false;
+	init_ = base_ + 2; p_ = base_ + 2;
 	code_ = low_ = ((uint32_t)p_[0] << 8) | p_[1];
 	p_ += 2;
 }
@@ -275,7 +271,10 @@ uint32_t Mux::taboo_decode()
 		l++;
 		if (l > (int)nbits_) { fill_buffer(l); t <<= 8; }
 		t >>= 1;
-		if (l > 40) { overflow_ = true; return 0; }
+		// the 32-bit raw-bit buffer holds a code of at most 25 bits (fill
+		// adds up to 7 bits past the request); the reference's own buffer
+		// overflows on a longer, i.e. corrupt, code
+		if (l > 25) { overflow_ = true; return 0; }
 	}
 	nbits_ -= l;
 	uint32_t cd = buffer_ >> (nbits_ + nt + 1);
@@ -283,7 +282,7 @@ uint32_t Mux::taboo_decode()
 	if (i > 0) { i--; nb += kTaboo.sum[i]; }
 	while (i > (int)nt) {
 		uint32_t j = 1;
-		while (((cd >> (i - j)) & 1) == 0) j++;
+		while (j < (uint32_t)i && ((cd >> (i - j)) & 1) == 0) j++;   // (a valid code has the 1 bit)
 		nb += kTaboo.sum[i - j] - kTaboo.sum[i - nt];
 		i -= j;
 	}
@@ -460,17 +459,16 @@ void pred_t(Mux& m, const BandView& b, bool dec)
 		for (int i = 1; i < b.dx; i++) {
 			int a = c[i - 1] - c[i - 1 - st], bb = c[i - st] - c[i - 1 - st];
 			int var = bitlen((uint32_t)((a < 0 ? -a : a) + (bb < 0 ? -bb : bb)));
+			// the reference indexes its 16 geometric contexts with var
+			// unchecked (out of bounds, i.e. undefined, past 15): only a
+			// corrupt stream or an out-of-range LL gets there; clamp
+			if (var > 15) var = 15;
 			if (!dec) g.code(m, s2u(c[i] - c[i - 1] - c[i - st] + c[i - 1 - st]), var);
 			else c[i] = (C)tr<SH>(c[i - 1] + c[i - st] - c[i - 1 - st] + u2s((int)g.decode(m, var)));
 		}
 	}
 }
 
-const uint8_t kKConv2[9][16] = {                 // bandcodec.cpp:409-420
-	{15}, {7,15}, {4,10,15}, {3,7,11,15}, {2,4,7,10,12,15}, {1,3,5,7,9,11,13,15},
-	{1,3,4,6,8,10,11,13,15}, {0,2,3,4,6,7,8,10,11,12,14,15},
-	{0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,15}};
-const uint8_t kKConv1[16] = {0,1,2,3,0,4,0,5,6,0,0,7,0,0,0,8};   // bandcodec.cpp:422-423
 
 // block_enum (full 4x4), src/lib/bandcodec.cpp:346-403
 template <typename C, bool HIGH, bool DEC>

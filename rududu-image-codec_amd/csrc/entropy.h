@@ -26,6 +26,10 @@ public:
 	// decoder over a .ric payload (the bytes after the 9-byte header): the
 	// same as init_decoder on two zero bytes followed by the payload
 	void init_decoder_payload(const uint8_t* payload, size_t n);
+	// decoder reading buf + 2 in place with no end (the reference's
+	// CMuxCodec(pStream), src/lib/muxcodec.cpp:31-34, 51-61): the caller's
+	// buffer must outlive it and hold the stream
+	void init_decoder_inplace(const uint8_t* buf);
 	Mux() = default;
 	Mux(const Mux&) = delete;
 	Mux& operator=(const Mux&) = delete;

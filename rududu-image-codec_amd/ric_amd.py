@@ -62,6 +62,8 @@ def lib():
         "ric_band_info": (_I, [_P, _I, ctypes.POINTER(_I), ctypes.POINTER(_I), ctypes.POINTER(_I), ctypes.POINTER(_F)]),
         "ric_band_read": (_I, [_P, _I, _P]),
         "ric_band_write": (_I, [_P, _I, _P]),
+        "ric_band_host": (_I, [_P, _I, ctypes.POINTER(_P), ctypes.POINTER(_I)]),
+        "ric_mux_create_decoder_inplace": (_I, [ctypes.POINTER(_P), _P]),
         "ric_mux_create_encoder": (_I, [ctypes.POINTER(_P), _P, _S, ctypes.c_uint16]),
         "ric_mux_create_decoder": (_I, [ctypes.POINTER(_P), _P, _S]),
         "ric_mux_end": (_I, [_P, ctypes.POINTER(_S)]),

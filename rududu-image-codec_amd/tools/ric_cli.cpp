@@ -111,7 +111,8 @@ void CompressImage(const std::string& infile, const std::string& outfile, int Qu
 		for (size_t i = 0; i < n; i++) img.px[i] = Quant ? (short)((img.px[i] - 128) << kShift) : (short)(img.px[i] - 128);
 	}
 	std::vector<unsigned char> stream(n * img.c * 2 + 65536);
-	CMuxCodec Codec(stream.data(), 0, stream.size());
+	unsigned char* pStream = stream.data();
+	CMuxCodec Codec(pStream, 0);                                // the reference's form (ric.cpp:157)
 	CWavelet2D Wavelet(img.w, img.h, kLevels, kLevels - 4);
 	Wavelet.SetWeight(Trans);
 	const int planes[3] = {2, 1, 0};
@@ -140,9 +141,10 @@ void DecompressImage(const std::string& infile, const std::string& outfile, bool
 	if (rc == RIC_E_FORMAT) throw 2;                            // BAD_MAGIC
 	ric_check(rc, "read header");
 	const size_t n = (size_t)w * h;
-	std::vector<unsigned char> stream(n * c + 2, 0);            // payload at buf + 2 (:203-205)
+	std::vector<unsigned char> stream(n * c + 2 + 16, 0);       // payload at buf + 2 (:203-205), look-ahead pad
 	memcpy(stream.data() + 2, file.data() + 9, std::min(file.size() - 9, n * c));
-	CMuxCodec Codec(stream.data(), stream.size());
+	unsigned char* pStream = stream.data();
+	CMuxCodec Codec(pStream);                                   // the reference's form (ric.cpp:207)
 	CWavelet2D Wavelet(w, h, kLevels, kLevels - 4);
 	Wavelet.SetWeight((trans)t);
 	Image img;

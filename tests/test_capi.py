@@ -64,3 +64,13 @@ def test_mux_capacity_is_explicit():
     m = ric_amd.MuxCodec(buf, first_word=0)
     assert m.getSize() == 2
     assert m.endCoding() <= 8
+
+
+def test_shim_compat_builds():
+    """A caller in the reference's own call forms (CMuxCodec(pStream, 0),
+    CMuxCodec(pStream), DBand/pLow members, (C*) pBand) compiles and links
+    against include/rududu_gpu.hpp + librududu_amd.so (tests/native/shim_compat.cpp)."""
+    import subprocess
+    nat = os.path.join(os.path.dirname(os.path.abspath(__file__)), "native")
+    subprocess.run(["make", "-s", "-C", nat, "all"], check=True, capture_output=True, timeout=300)
+    assert os.path.exists(os.path.join(nat, "shim_compat"))

@@ -120,3 +120,36 @@ def test_ring_timeout_is_an_error(ric, port):
     finally:
         lib.ric_diag_fault(0)
     assert c.compress(pix, 9, 0) == port.encode_ric(pix, 9, 0)
+
+
+SHIM = os.path.join(REPO, "tests", "native", "shim_compat")
+
+
+@pytest.mark.parametrize("w,h,q,t", [(200, 150, 9, 0), (129, 77, 0, 1), (64, 48, 9, 0)])
+def test_shim_reference_call_forms(ric, port, tmp_path, w, h, q, t):
+    """tests/native/shim_compat.cpp -- the reference's call forms over
+    include/rududu_gpu.hpp: CMuxCodec(pStream, 0) / CMuxCodec(pStream),
+    TransformI on the plane end, DBand/pLow members, (C*) pBand, Stats()."""
+    pix = ric.synth(w, h, 1, 3)
+    raw = str(tmp_path / "in.raw")
+    pix.tofile(raw)
+    out = str(tmp_path / "o.ric")
+    subprocess.run([SHIM, "enc", str(w), str(h), str(q), str(t), raw, out], check=True, timeout=120)
+    r = open(out, "rb").read()
+    assert r == port.encode_ric(pix, q, t)
+    dec = str(tmp_path / "o.raw")
+    subprocess.run([SHIM, "dec", out, dec], check=True, timeout=120)
+    assert np.array_equal(np.fromfile(dec, np.uint8).reshape(1, h, w), port.decode_ric(r)[0])
+    bd = str(tmp_path / "b.i32")
+    subprocess.run([SHIM, "bands", str(w), str(h), str(q), str(t), raw, bd], check=True, timeout=120)
+    exp = np.concatenate([b.ravel() for b in port.bands(O.gray_plane(pix[0], q), 5, 1, t, 0)])
+    assert np.array_equal(np.fromfile(bd, np.int32), exp)
+    # Stats(): the reference's order and arithmetic on the same bands
+    st = subprocess.run([SHIM, "stats", str(w), str(h), str(t), raw], check=True, capture_output=True,
+                        text=True, timeout=120).stdout.split("\n")
+    bands = port.bands(O.gray_plane(pix[0], 9), 5, 1, t, 0)
+    names = ["D", "H", "V"] * ((len(bands) - 1) // 3) + ["L"]
+    wts = O.set_weight(len(bands), t)
+    want = ["%s :\t%s" % (nm, format(float(O.band_variance(b, wts[i])), ".6g"))
+            for i, (nm, b) in enumerate(zip(names, bands))]
+    assert st[:len(want)] == want

@@ -68,3 +68,22 @@ def test_haar_even_sizes():
     a = O.port().encode_ric(pix, 9, 2)
     assert a == REF.encode_ric(pix, 9, 2)
     assert np.array_equal(O.port().decode_ric(a)[1], REF.decode_ric(a)[1])
+
+
+@pytest.mark.parametrize("w,h", [(64, 48), (300, 220), (1001, 603)])
+@pytest.mark.parametrize("t", [0, 1])
+def test_stats_restatement(w, h, t):
+    """oracle.band_variance / set_weight (the numbers CWavelet2D::Stats
+    prints) against the reference's CBand::Mean on its own bands."""
+    import ctypes
+    pl = O.gray_plane(O.synth(w, h, 1, 5)[0], 9)
+    f = REF.lib.ricref_stats
+    f.restype = ctypes.c_long
+    f.argtypes = [ctypes.c_void_p] + [ctypes.c_int] * 5 + [ctypes.c_void_p]
+    out = np.zeros(64, np.float32)
+    n = f(pl.ctypes.data, w, h, 5, 1, t, out.ctypes.data)
+    bands = REF.bands(pl, 5, 1, t, 0)
+    assert n == len(bands)
+    wts = O.set_weight(n, t)
+    for i, b in enumerate(bands):
+        assert O.band_variance(b, wts[i]) == out[i], i
