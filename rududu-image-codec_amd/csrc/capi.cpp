@@ -369,23 +369,16 @@ int decode_band(ric_wavelet* w, Mux& m)
 
 // DecodeBand + TSUQi + TransformI of one plane, pipelined by level (the
 // codec's decode path).  The reference decodes coarse -> fine
-// (src/lib/wavelet2d.cpp:179-222) and inverts coarsest level first (:960-990),
-// so as soon as the host has decoded a level's V, H, D bands they go to the
-// device and that level's inverse (TSUQi fused, quant != 0) is queued, while
-// the host decodes the next finer level.  The stream is synchronised once,
-// at the end.
+// (src/lib/wavelet2d.cpp:179-222) and inverts coarsest level first (:960-990).
+// Decoding level l also rewrites level l + 1: the zerotree scan clears the
+// parent markers it consumes (src/lib/bandcodec.cpp:528-531).  So once the
+// host has decoded level l, level l + 1 is final: its bands go to the device
+// and its inverse (TSUQi fused, quant != 0) is queued while the host decodes
+// level l - 1; level 0 follows the last host step.  One stream sync, at the end.
 int decode_inverse_pipelined(ric_wavelet* w, Mux& m, int16_t* dimg, long stride, int trans, int quant)
 {
 	Pyramid& P = w->P;
-	const double t0 = now_ms();
-	pred_decode(m, view(w, P.coarsest_ll()));
-	for (int l = P.nlev - 1; l >= 0; l--) {
-		const int order[3] = {BV, BH, BD};
-		for (int k = 0; k < 3; k++) {
-			BandView par;
-			if (l + 1 < P.nlev) par = view(w, P.L[l + 1].b[order[k]]);
-			tree_decode_fast(m, view(w, P.L[l].b[order[k]]), par, l == 0, l > 0);
-		}
+	auto issue = [&](int l) -> int {
 		// level l's D, H, V are contiguous in region A; the coarsest LL ends it
 		const Level& L = P.L[l];
 		const size_t lo = L.b[BD].off;
@@ -403,9 +396,26 @@ int decode_inverse_pipelined(ric_wavelet* w, Mux& m, int16_t* dimg, long stride,
 		} else {
 			launch_inv_level(L, L.b[BL], w->d_arena, out, po, out_int, trans, w->st);
 		}
+		return RIC_OK;
+	};
+	const double t0 = now_ms();
+	pred_decode(m, view(w, P.coarsest_ll()));
+	for (int l = P.nlev - 1; l >= 0; l--) {
+		const int order[3] = {BV, BH, BD};
+		for (int k = 0; k < 3; k++) {
+			BandView par;
+			if (l + 1 < P.nlev) par = view(w, P.L[l + 1].b[order[k]]);
+			tree_decode_fast(m, view(w, P.L[l].b[order[k]]), par, l == 0, l > 0);
+		}
+		if (l + 1 < P.nlev) {
+			int rc = issue(l + 1);
+			if (rc) return rc;
+		}
 	}
-	HIPCHK(hipGetLastError());
 	w->prof.host(S_HDEC, now_ms() - t0);
+	int rc = issue(0);
+	if (rc) return rc;
+	HIPCHK(hipGetLastError());
 	// the host mirror is rewritten by the next DecodeBand: wait for the copies
 	HIPCHK(hipStreamSynchronize(w->st));
 	w->host_valid = false;    // the device now holds these bands
