@@ -188,10 +188,11 @@ def workload_frames(a, rank, world, threads):
     if a.workload == "C5":
         W, H = 4096, 4096
         total = a.frames or a.batch or 64
-        return W, H, 1, [(f, f, None) for f in range(rank, total, world)], "strong"
+        import shard
+        return W, H, 1, [(f, f, None) for f in shard.frames_of_rank(total, world, rank)], "strong"
     import shard
     rects = shard.tile_rects(7680, 4320)
-    mine = [(i, 0, r) for i, r in enumerate(rects) if i % world == rank]
+    mine = [(i, 0, rects[i]) for i in shard.tiles_of_rank(world, rank)]
     return 3840, 2160, 3, mine, "strong"
 
 
@@ -244,11 +245,31 @@ def main():
     b = ric_amd.Batch(W, H, CH, slots=slots, threads=threads, device=local) if nfr else None
     gather = world > 1 and not a.no_gather
     gathered = [0]
+    container = [None]
 
     def step():
         if b is not None:
             b.roundtrip(frames, outs, q=a.q, trans=a.trans)
-        if gather:
+        if gather and a.workload == "C4":
+            # C4: the tile streams to rank 0 into one RTL1 container, and the
+            # decode side of the exchange: the container's tiles scattered
+            # back to the ranks that decode them (shard.scatter_streams)
+            streams = [b.stream(i) for i in range(nfr)] if b is not None else []
+            got = shard.gather_streams(streams, dist, device=cdev)
+            per_rank = None
+            if rank == 0:
+                tiles = [None] * 4
+                for r, lst in enumerate(got):
+                    for i, s in zip(shard.tiles_of_rank(world, r), lst):
+                        tiles[i] = s
+                container[0] = shard.pack_tiles(7680, 4320, 2, 2, tiles)
+                gathered[0] = len(container[0])
+                _, _, _, _, back = shard.unpack_tiles(container[0])
+                per_rank = [[back[i] for i in shard.tiles_of_rank(world, r)] for r in range(world)]
+            mine_back = shard.scatter_streams(per_rank, dist, device=cdev)
+            if mine_back != streams:
+                raise RuntimeError("rank %d: scattered tile streams differ from the encoded ones" % rank)
+        elif gather:
             # the path's one exchange: every rank's .ric streams to rank 0
             # (SURVEY.md §8(e)); rank 0 keeps them on the device
             streams = [b.stream(i) for i in range(nfr)] if b is not None else []
@@ -413,6 +434,8 @@ def main():
         out["gpu_path_split"] = split
     if gather:
         out["gather"] = {"backend": backend, "bytes_to_rank0_per_step": gathered[0]}
+        if a.workload == "C4":
+            out["gather"]["container"] = "RTL1, 4 tiles, %d bytes; tiles scattered back per step" % gathered[0]
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(W, H, a.q, a.trans, threads)   # gray frames of the workload's size

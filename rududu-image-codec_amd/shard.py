@@ -41,6 +41,13 @@ def tile_of_rank(rank, nx=2, ny=2):
     return rank % nx, rank // nx
 
 
+def tiles_of_rank(world, rank, nx=2, ny=2):
+    """Tile indices (2*ty + tx for 2x2) coded by `rank`: tile i on rank i mod
+    world -- one tile per rank at world == nx*ny, round robin
+    below that."""
+    return list(range(rank, nx * ny, world))
+
+
 def pack_tiles(W, H, nx, ny, streams):
     assert len(streams) == nx * ny
     head = TILE_MAGIC + struct.pack("<HHBB", W, H, nx, ny) + struct.pack("<%dI" % len(streams),
@@ -104,4 +111,46 @@ def gather_streams(local, dist, device=None, to_host=True):
             lst.append(data[off:off + L])
             off += L
         out.append(lst)
+    return out
+
+
+def scatter_streams(per_rank, dist, device=None):
+    """The decode side of gather_streams: rank 0 holds one list of byte
+    streams per rank (`per_rank`, ignored elsewhere); every rank gets its own
+    list.  A broadcast of the padded sizes, then two scatters (sizes,
+    payloads) -- RCCL over xGMI with "nccl", gloo on CPU."""
+    import torch
+    world = dist.get_world_size()
+    rank = dist.get_rank()
+    dev = device if device is not None else torch.device("cpu")
+    head = torch.zeros(2, dtype=torch.int64, device=dev)
+    if rank == 0:
+        head[0] = max(len(x) for x in per_rank)
+        head[1] = max(max(sum(len(s) for s in x) for x in per_rank), 1)
+    dist.broadcast(head, src=0)
+    maxn, maxb = int(head[0]), int(head[1])
+    sz = torch.zeros(maxn + 1, dtype=torch.int64, device=dev)
+    buf = torch.zeros(maxb, dtype=torch.uint8, device=dev)
+    sz_list = buf_list = None
+    if rank == 0:
+        sz_list, buf_list = [], []
+        for lst in per_rank:
+            t = torch.zeros(maxn + 1, dtype=torch.int64)
+            t[0] = len(lst)
+            if lst:
+                t[1:len(lst) + 1] = torch.tensor([len(x) for x in lst], dtype=torch.int64)
+            b = torch.zeros(maxb, dtype=torch.uint8)
+            if lst:
+                payload = np.frombuffer(b"".join(lst), np.uint8)
+                b[:payload.size] = torch.from_numpy(payload.copy())
+            sz_list.append(t.to(dev))
+            buf_list.append(b.to(dev))
+    dist.scatter(sz, scatter_list=sz_list, src=0)
+    dist.scatter(buf, scatter_list=buf_list, src=0)
+    n = int(sz[0])
+    data = buf.cpu().numpy().tobytes()
+    out, off = [], 0
+    for L in (int(x) for x in sz[1:n + 1]):
+        out.append(data[off:off + L])
+        off += L
     return out

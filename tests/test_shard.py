@@ -17,6 +17,36 @@ def test_frames_partition():
         assert all(len(shard.frames_of_rank(64, world, r)) == 64 // world for r in range(world))
 
 
+def test_tiles_partition():
+    for world in (1, 2, 3, 4):
+        got = sorted(sum((shard.tiles_of_rank(world, r) for r in range(world)), []))
+        assert got == [0, 1, 2, 3]
+    assert [shard.tiles_of_rank(4, r) for r in range(4)] == [[0], [1], [2], [3]]
+    assert [shard.tile_of_rank(r) for r in range(4)] == [shard.tile_rects(8, 8)[r][:2] for r in range(4)]
+
+
+def test_bench_workload_partition():
+    """bench.py's C3 / C4 / C5 frame sets: every frame or tile exactly once
+    over the ranks."""
+    import argparse
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    for wl in ("C4", "C5"):
+        for world in (1, 2, 4, 8):
+            a = argparse.Namespace(workload=wl, frames=0, batch=0)
+            seen = []
+            for r in range(world):
+                W, H, C, mine, scaling = bench.workload_frames(a, r, world, 16)
+                seen += [m[0] for m in mine]
+                assert scaling == "strong"
+            assert sorted(seen) == list(range(4 if wl == "C4" else 64))
+    a = argparse.Namespace(workload="C3", frames=0, batch=0)
+    f0 = bench.workload_frames(a, 0, 2, 16)[3]
+    f1 = bench.workload_frames(a, 1, 2, 16)[3]
+    assert len(f0) == len(f1) == 128 and not set(m[1] for m in f0) & set(m[1] for m in f1)
+
+
 def test_tiles_cover_image():
     rects = shard.tile_rects(7680, 4320)
     assert [(r[0], r[1]) for r in rects] == [(0, 0), (1, 0), (0, 1), (1, 1)]
@@ -86,3 +116,50 @@ def test_gather_streams_gloo_world2():
         for f, s in zip(shard.frames_of_rank(7, 2, r), lst):
             flat[f] = s
     assert all(flat[f] == (b"frame%d:" % f) * (f + 1) for f in range(7))
+
+
+def _worker_tiles(rank, world, port, q):
+    """C4's exchange: each rank's tile streams to rank 0 (gather), the RTL1
+    container there, and the decode side: unpack + scatter back."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "rududu-image-codec_amd"))
+    import torch.distributed as dist
+    import shard as S
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    mine = S.tiles_of_rank(world, rank)
+    local = [(b"tile%d|" % i) * (50 + 7 * i) for i in mine]
+    got = S.gather_streams(local, dist)
+    blob = None
+    per_rank = None
+    if rank == 0:
+        streams = [None] * 4
+        for r, lst in enumerate(got):
+            for i, s in zip(S.tiles_of_rank(world, r), lst):
+                streams[i] = s
+        blob = S.pack_tiles(7680, 4320, 2, 2, streams)
+        _, _, _, _, back = S.unpack_tiles(blob)
+        per_rank = [[back[i] for i in S.tiles_of_rank(world, r)] for r in range(world)]
+    mine_back = S.scatter_streams(per_rank, dist)
+    q.put((rank, (local, mine_back, blob)))
+    dist.destroy_process_group()
+
+
+def test_tiles_gather_container_scatter_gloo_world2():
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker_tiles, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    out = dict(q.get(timeout=120) for _ in range(2))
+    for p in ps:
+        p.join(timeout=60)
+    for r in range(2):
+        local, back, _ = out[r]
+        assert back == local and len(local) == 2
+    W, H, nx, ny, streams = shard.unpack_tiles(out[0][2])
+    assert (W, H, nx, ny) == (7680, 4320, 2, 2)
+    assert streams == [(b"tile%d|" % i) * (50 + 7 * i) for i in range(4)]
