@@ -18,6 +18,18 @@ using namespace tables;
 
 #define RIC_AI __attribute__((always_inline)) inline
 
+// Measurement builds only (tests/native ENC_STATS): event counts of the
+// serial pass by kind, and RIC_ENC_NO_RAW, which drops every raw-bit write
+// (wrong output; the time of the pass without its raw-bit half).
+#ifdef RIC_ENC_STATS
+}  // namespace
+uint64_t g_enc_stats[8];   // bins, sign bits, remainder bits, huffman bits, enum/edge raw bits, raw calls
+namespace {
+#define RIC_STAT(i, n) (g_enc_stats[i] += (n))
+#else
+#define RIC_STAT(i, n) ((void)0)
+#endif
+
 struct EncCore {
 	Mux::EncState s;
 	explicit EncCore(const Mux::EncState& st) : s(st) {}
@@ -50,6 +62,7 @@ struct EncCore {
 	}
 	RIC_AI void bin(uint32_t freq, uint32_t bit)           // codeBin, muxcodec.h:156-163
 	{
+		RIC_STAT(0, 1);
 		if (__builtin_expect(s.range <= 4096u, 0)) norm();
 		const uint32_t t = (s.range * freq) >> 12;
 		s.low += t & (0u - bit);
@@ -57,6 +70,10 @@ struct EncCore {
 	}
 	RIC_AI void bits(uint32_t v, uint32_t len)             // bitsCode (64-bit FIFO, see entropy.h)
 	{
+		RIC_STAT(5, 1);
+#ifdef RIC_ENC_NO_RAW
+		return;
+#endif
 		if (__builtin_expect(s.ebits + len > 64, 0)) drain();
 		s.ebuf = (s.ebuf << len) | v;
 		s.ebits += len;
@@ -102,6 +119,7 @@ struct GeoE {                                             // CGeomCodec::code
 			freq[c] -= freq[c] >> (3 + s);
 		}
 		e.bin(f, 0);
+		RIC_STAT(1, 1); RIC_STAT(2, k);
 		e.bits(((sym & ((1u << k) - 1)) << 1) | sign, k + 1);
 		freq[c] += (4096 - freq[c]) >> (3 + s);
 		if ((uint16_t)(freq[c] - kGeoThres[s - 1]) > kGeoThres[s] - kGeoThres[s - 1]) {
@@ -128,6 +146,7 @@ struct GeoRegE {
 			fr -= fr >> (3 + s);
 		}
 		e.bin(f, 0);
+		RIC_STAT(1, 1); RIC_STAT(2, k);
 		e.bits(((sym & ((1u << k) - 1)) << 1) | sign, k + 1);
 		fr = (uint16_t)(fr + ((4096 - fr) >> (3 + s)));
 		if ((uint16_t)(fr - kGeoThres[s - 1]) > kGeoThres[s] - kGeoThres[s - 1]) {
@@ -165,6 +184,7 @@ void tree_rec_fast(Mux& m, const uint64_t* rec, const uint8_t* pin, const BandVi
 			if (__builtin_expect(BlockRec::edge(r), 0)) {
 				bord.code(e, ins, 0);
 				if (ins) continue;
+				RIC_STAT(4, BlockRec::rawlen(r));
 				e.bits(BlockRec::raw(r), BlockRec::rawlen(r));
 				const int w = BlockRec::w(r), gc = BlockRec::gctx(r);
 				while (mask) {
@@ -186,6 +206,7 @@ void tree_rec_fast(Mux& m, const uint64_t* rec, const uint8_t* pin, const BandVi
 				const int idx = (kmean[ctx] + (1 << 9)) >> 10;
 				const uint16_t h = HIGH ? kHuff_HIGH[idx][k - 1] : kHuff_LOW[idx][k];
 				const uint32_t rl = BlockRec::rawlen(r);
+				RIC_STAT(3, h & 31); RIC_STAT(4, rl);
 				e.bits(((uint32_t)(h >> 5) << rl) | BlockRec::raw(r), (h & 31) + rl);
 				const int gc = (int)k - 1;
 				GeoRegE gr;
