@@ -1872,9 +1872,12 @@ __device__ __forceinline__ void gen_block(const FqArgs& a, const int* thr, const
 // level's LL TSUQ.  The levels
 // that take this kernel are small and latency-bound: the wide block phase
 // replaces the two dependent rounds of a wave-per-segment form.
-template <typename TI, typename TO>
+// GR: rows per workgroup (a multiple of 8; each wave lifts GR / 4 rows)
+template <typename TI, typename TO, int GR>
 __device__ __forceinline__ void fwdq_gen_body(const FqArgs& a, const GenLL& ll, int nseg)
 {
+	static_assert(GR % 8 == 0, "whole block rows per workgroup");
+	constexpr int WR = GR / 4;   // rows lifted per wave
 	__shared__ int s_thres[3][16];
 	__shared__ FqTables s_F __attribute__((aligned(16)));
 	__shared__ uint32_t s_tpk[3][17 * 8];
@@ -1882,7 +1885,7 @@ __device__ __forceinline__ void fwdq_gen_body(const FqArgs& a, const GenLL& ll, 
 	const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 	const int seg = blockIdx.y;
 	const int strip = blockIdx.x;
-	const int y0 = seg * kGenRows;
+	const int y0 = seg * GR;
 	FwdArgs<TI, TO> f;
 	f.src = reinterpret_cast<const TI*>(a.src); f.sp = a.sp; f.W = a.W; f.H = a.H;
 #pragma unroll
@@ -1895,12 +1898,12 @@ __device__ __forceinline__ void fwdq_gen_body(const FqArgs& a, const GenLL& ll, 
 	// the four waves lift two rows each (own halo rows): a lifting wave is
 	// instruction-latency-bound, and 5 row pairs per wave instead of 8
 	// shorten the chain that the whole segment waits for
-	if (y0 + 2 * w < a.H) {
+	if (y0 + WR * w < a.H) {
 		const int X0 = strip * kStripValid - kCols;
 		if constexpr (sizeof(TI) == 2 && sizeof(TO) == 2)
-			fwd97p_seg<2, false>(f, X0 + lane * kCols, lane, y0 + 2 * w);     // packed 16-bit lifting
+			fwd97p_seg<WR, false>(f, X0 + lane * kCols, lane, y0 + WR * w);     // packed 16-bit lifting
 		else
-			fwd_seg<CDF97, TI, TO, 2, false>(f, X0 + lane * kCols, lane, y0 + 2 * w);
+			fwd_seg<CDF97, TI, TO, WR, false>(f, X0 + lane * kCols, lane, y0 + WR * w);
 	}
 	if (wgt && lane == 0 && w == 0) wgt[1] = __builtin_amdgcn_s_memrealtime();
 	fq_stage_tables<256>(a, s_thres, s_F, s_tpk);
@@ -1911,16 +1914,17 @@ __device__ __forceinline__ void fwdq_gen_body(const FqArgs& a, const GenLL& ll, 
 	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 	if (wgt && threadIdx.x == 0) wgt[3] = __builtin_amdgcn_s_memrealtime();
 	const TO* d[3] = {f.d[0], f.d[1], f.d[2]};
-	const int ky = y0 >> 3;
-	for (int i = threadIdx.x; i < 3 * kGenBlocks; i += 256) {
-		const int b = i / kGenBlocks, kx = strip * kGenBlocks + (i - b * kGenBlocks);
+	constexpr int NB = 3 * kGenBlocks * (GR / 8);     // the segment's blocks: band, block row, column
+	for (int i = threadIdx.x; i < NB; i += 256) {
+		const int b = i / (kGenBlocks * (GR / 8)), rem = i - b * kGenBlocks * (GR / 8);
+		const int ky = (y0 >> 3) + rem / kGenBlocks, kx = strip * kGenBlocks + rem % kGenBlocks;
 		if (kx < a.bw[b] && ky < a.bh[b]) gen_block<TO>(a, s_thres[b], s_tpk[b], s_F, d, b, kx, ky);
 	}
 	if (wgt && lane == 0) wgt[4 + w] = __builtin_amdgcn_s_memrealtime();
 	if (ll.on) {
 		// CBand::TSUQ with Thres 0.5 on this segment's LL samples: all loads first
 		constexpr bool SH = sizeof(TO) == 2;
-		constexpr int NLL = (kGenRows / 2) * (kStripValid / 2);
+		constexpr int NLL = (GR / 2) * (kStripValid / 2);
 		constexpr int PER = (NLL + 255) / 256;
 		const int ldx = a.W >> 1, ldy = a.H >> 1, c0 = strip * (kStripValid / 2), r0 = y0 >> 1;
 		int val[PER];
@@ -1946,11 +1950,11 @@ __device__ __forceinline__ void fwdq_gen_body(const FqArgs& a, const GenLL& ll, 
 }
 
 template <typename TI, typename TO>
-__global__ void __launch_bounds__(256) k_fwdq_gen(FqArgs a, GenLL ll, int nseg) { fwdq_gen_body<TI, TO>(a, ll, nseg); }
-template <typename TI, typename TO>
+__global__ void __launch_bounds__(256) k_fwdq_gen(FqArgs a, GenLL ll, int nseg) { fwdq_gen_body<TI, TO, kGenRows>(a, ll, nseg); }
+template <typename TI, typename TO, int GR>
 __global__ void __launch_bounds__(256) k_fwdq_gen_z(const FqArgs* __restrict__ az, GenLL ll, int nseg)
 {
-	fwdq_gen_body<TI, TO>(az[blockIdx.z], ll, nseg);
+	fwdq_gen_body<TI, TO, GR>(az[blockIdx.z], ll, nseg);
 }
 
 // ---------------------------------------------------------- inverse level
@@ -2658,8 +2662,10 @@ int launch_fwdq_level_z(const Pyramid& P, int l, const ZFrames& fr, int vec8, in
 	if (zargs_put(z, v.data(), v.size() * sizeof(FqArgs), st)) return -1;
 	const FqArgs* d = (const FqArgs*)z.dev;
 	const dim3 grid((L.w + kFqStrip - 1) / kFqStrip, v[0].nseg, fr.nz);
-	// the one-producer form on level 0 (VALU-bound), two producers above (see fq_launch_pc)
-	if (l == 0) hipLaunchKernelGGL(k_fwdq_pc_z<true>, grid, dim3(256), 0, st, d, S, 0);
+	// the one-producer form on level 0 (VALU-bound), two producers above (see
+	// fq_launch_pc); knob RIC_FQZ_PC1 = the last level on one producer
+	static const int pc1 = [] { const char* e = getenv("RIC_FQZ_PC1"); return e ? atoi(e) : 0; }();
+	if (l <= pc1) hipLaunchKernelGGL(k_fwdq_pc_z<true>, grid, dim3(256), 0, st, d, S, 0);
 	else hipLaunchKernelGGL(k_fwdq_pc2_z<true>, grid, dim3(320), 0, st, d, S, 0);
 	return 0;
 }
@@ -2668,7 +2674,12 @@ int launch_fwdq_gen_level_z(const Pyramid& P, int l, const ZFrames& fr, int vec8
                             int ll_iQ, int ll_T0, ZArgs& z, hipStream_t st)
 {
 	const Level& L = P.L[l];
-	const int nseg = (L.h + kGenRows - 1) / kGenRows;
+	// rows per workgroup in a batch (knob RIC_GENZ_ROWS = 8 / 16 / 32): a
+	// batch has workgroups to spare, so longer segments (less halo lifting
+	// per row, fewer workgroups) than the single frame's 8
+	static const int gr_env = [] { const char* e = getenv("RIC_GENZ_ROWS"); return e ? atoi(e) : 0; }();
+	const int GR = (gr_env == 8 || gr_env == 16 || gr_env == 32) ? gr_env : 16;
+	const int nseg = (L.h + GR - 1) / GR;
 	std::vector<FqArgs> v(fr.nz);
 	for (int f = 0; f < fr.nz; f++) {
 		v[f] = fq_args(P, l, (const char*)fr.src + f * fr.sstride, fr.sp, vec8, 0, qp, fr.arena + f * fr.astride, true);
@@ -2678,9 +2689,15 @@ int launch_fwdq_gen_level_z(const Pyramid& P, int l, const ZFrames& fr, int vec8
 	const FqArgs* d = (const FqArgs*)z.dev;
 	const GenLL ll = {ll_on, ll_iQ, ll_T0};
 	const dim3 grid((L.w + kStripValid - 1) / kStripValid, nseg, fr.nz);
-	if (!L.in_is_int && !L.is_int) hipLaunchKernelGGL((k_fwdq_gen_z<int16_t, int16_t>), grid, dim3(256), 0, st, d, ll, nseg);
-	else if (!L.in_is_int) hipLaunchKernelGGL((k_fwdq_gen_z<int16_t, int32_t>), grid, dim3(256), 0, st, d, ll, nseg);
-	else hipLaunchKernelGGL((k_fwdq_gen_z<int32_t, int32_t>), grid, dim3(256), 0, st, d, ll, nseg);
+	auto go = [&](auto gr) {
+		constexpr int G = decltype(gr)::value;
+		if (!L.in_is_int && !L.is_int) hipLaunchKernelGGL((k_fwdq_gen_z<int16_t, int16_t, G>), grid, dim3(256), 0, st, d, ll, nseg);
+		else if (!L.in_is_int) hipLaunchKernelGGL((k_fwdq_gen_z<int16_t, int32_t, G>), grid, dim3(256), 0, st, d, ll, nseg);
+		else hipLaunchKernelGGL((k_fwdq_gen_z<int32_t, int32_t, G>), grid, dim3(256), 0, st, d, ll, nseg);
+	};
+	if (GR == 8) go(std::integral_constant<int, 8>());
+	else if (GR == 32) go(std::integral_constant<int, 32>());
+	else go(std::integral_constant<int, 16>());
 	return 0;
 }
 
