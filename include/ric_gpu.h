@@ -165,6 +165,14 @@ int ric_batch_decode(ric_batch* b, const uint8_t* const* ric, const size_t* len,
  * to host out[i]), in groups of `slots` frames, pipelined. */
 int ric_batch_roundtrip(ric_batch* b, const uint8_t* const* pix, int n, int q, int trans, uint8_t* const* out,
                         const size_t* cap, size_t* len, uint8_t* const* pix_out);
+/* The whole CompressImage of n <= slots gray frames on the GPU, the serial
+ * coder included (one wave per frame's stream): pix[i] device pixels; the
+ * .ric file of frame i to out + i * ostride (DEVICE memory, cap <= ostride
+ * bytes each), its size to len[i] (host).  Byte-identical to ric_batch_encode.
+ * No reference counterpart (the reference's CompressImage is one stream on
+ * one host thread). */
+int ric_batch_encode_gpu(ric_batch* b, const uint8_t* const* pix, int n, int q, int trans, uint8_t* out, size_t ostride,
+                         size_t cap, size_t* len);
 /* Stage timers of the batch (no reference counterpart): 0 pixel conversion
  * in, 1..8 forward level 0..7 (fused DWT + quantiser + records), 9 D2H of
  * bands + records, 10 host encode, 11 host decode, 12 H2D of the bands,

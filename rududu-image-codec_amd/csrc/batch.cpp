@@ -32,6 +32,7 @@
 #include "ric_image.h"
 #include "entropy.h"
 #include "codec_params.h"
+#include "gcoder.h"
 
 using namespace ric;
 
@@ -204,6 +205,11 @@ struct ric_batch {
 	std::vector<Mux> enc, dec;                     // per slot
 	Pool* pool = nullptr;
 	BProf prof;
+	// GPU stream coder (gcoder.hip): argument block, per-slot results
+	GEncArgs genc{};
+	GEncArgs* d_genc = nullptr;
+	uint32_t* d_res = nullptr;                     // 2 per slot
+	uint32_t* h_res = nullptr;                     // pinned
 
 	int nslot() const { return 2 * slots; }
 	char* arena(int s) const { return d_arena + (size_t)s * astride; }
@@ -229,7 +235,7 @@ int lambda_of(int q, int p) { return q ? quants(q + 13 + (p ? 8 : 0)) : 0; }
 // conversion (p == 0), every forward level + quantiser + block records as one
 // launch per level over the group, then the bands + records of every frame
 // to the host mirrors (one strided copy).  pix: device pixels of each frame.
-int gpu_encode_plane(ric_batch* b, int set, int n, int p, const uint8_t* const* pix, int q, int trans)
+int gpu_encode_plane(ric_batch* b, int set, int n, int p, const uint8_t* const* pix, int q, int trans, bool d2h = true)
 {
 	Pyramid& P = b->P;
 	const int s0 = set * b->slots;
@@ -287,6 +293,7 @@ int gpu_encode_plane(ric_batch* b, int set, int n, int p, const uint8_t* const* 
 				launch_blocks_level(P, l, !fused[l], l + 1 < P.nlev && !fused[l + 1], ar, b->st);
 	}
 	BCHK(hipGetLastError());
+	if (!d2h) return RIC_OK;
 	auto sp = b->prof.begin(B_D2H, n, b->st);
 	BCHK(hipMemcpy2DAsync(b->harena(s0), b->hstride, b->arena(s0), b->astride, P.b_end, n, hipMemcpyDeviceToHost, b->st));
 	b->prof.end(sp);
@@ -526,6 +533,9 @@ void ric_batch_destroy(ric_batch* b)
 	if (b->h_arena) (void)hipHostFree(b->h_arena);
 	if (b->d_planes) (void)hipFree(b->d_planes);
 	if (b->d_stage) (void)hipFree(b->d_stage);
+	if (b->d_genc) (void)hipFree(b->d_genc);
+	if (b->d_res) (void)hipFree(b->d_res);
+	if (b->h_res) (void)hipHostFree(b->h_res);
 	if (b->st) (void)hipStreamDestroy(b->st);
 	delete b;
 }
@@ -679,6 +689,53 @@ int ric_batch_roundtrip(ric_batch* b, const uint8_t* const* pix, int n, int q, i
 	if (!ok) return RIC_E_HIP;
 	b->prof.harvest();
 	return stream_err ? RIC_E_STREAM : RIC_OK;
+}
+
+// The whole CompressImage of n gray frames on the GPU: pixel conversion,
+// fused forward levels, then the serial coder of every frame's stream on one
+// wave each (gcoder.hip k_gc_encode).  pix: device pixels; the .ric file of
+// frame i goes to out + i * ostride (device, cap bytes each), its size to
+// len[i] (host).  Byte-identical to ric_batch_encode.
+int ric_batch_encode_gpu(ric_batch* b, const uint8_t* const* pix, int n, int q, int trans, uint8_t* out, size_t ostride,
+                         size_t cap, size_t* len)
+{
+	if (!b || !pix || !out || !len || n < 0 || n > b->slots || q < 0 || q > 31 || trans < 0 || trans > 2 || cap > ostride ||
+	    cap > 0xFFFFFFF0u)
+		return RIC_E_ARG;
+	if (b->channels != 1) return RIC_E_ARG;      // one plane per stream here; colour goes through ric_batch_encode
+	if (n == 0) return RIC_OK;
+	if (set_dev(b->device)) return RIC_E_HIP;
+	int rc = gpu_encode_plane(b, 0, n, 0, pix, q, trans, false);
+	if (rc) return rc;
+	if (!b->d_genc) {
+		BCHK(hipMalloc(&b->d_genc, sizeof(GEncArgs)));
+		BCHK(hipMalloc(&b->d_res, sizeof(uint32_t) * 2 * b->nslot()));
+		BCHK(hipHostMalloc(&b->h_res, sizeof(uint32_t) * 2 * b->nslot(), 0));
+	}
+	GEncArgs& a = b->genc;
+	a.arena = b->arena(0); a.astride = b->astride;
+	a.out = out; a.ostride = ostride; a.cap = cap;
+	a.res = b->d_res;
+	a.status_off = (uint32_t)b->P.status_off;
+	a.w = b->w; a.h = b->h; a.q = q; a.trans = trans;
+	gc_bands(b->P, a.ll, a.b, a.nb);
+	BCHK(hipMemcpyAsync(b->d_genc, &a, sizeof(GEncArgs), hipMemcpyHostToDevice, b->st));
+	auto sp = b->prof.begin(B_HENC, n, b->st);
+	if (launch_gc_encode(b->d_genc, n, b->st)) return bfail(hipGetLastError(), "k_gc_encode") ? RIC_E_HIP : RIC_E_HIP;
+	b->prof.end(sp);
+	BCHK(hipMemcpyAsync(b->h_res, b->d_res, sizeof(uint32_t) * 2 * n, hipMemcpyDeviceToHost, b->st));
+	BCHK(hipStreamSynchronize(b->st));
+	b->prof.harvest();
+	for (int i = 0; i < n; i++) {
+		len[i] = b->h_res[2 * i];
+		if (b->h_res[2 * i + 1] == 2) {
+			clear_status(b);
+			set_last_error("fused level kernel: LDS ring hand-off timed out (device status word set; output discarded)");
+			return RIC_E_HIP;
+		}
+		if (b->h_res[2 * i + 1]) return RIC_E_CAPACITY;
+	}
+	return RIC_OK;
 }
 
 // Diagnostics: the GPU stages alone, `iters` times over n frames (slot set

@@ -1,0 +1,65 @@
+// gcoder.h -- launch interface of the GPU stream coder (gcoder.hip): the
+// serial .ric coder with one wave per frame's stream.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstddef>
+#include "ric_types.h"
+
+namespace ric {
+
+// One band as the stream coder sees it: offsets into the frame's arena.
+struct GBandDesc {
+	uint32_t off;        // band (pitch elements, is_int ? int32 : int16)
+	uint32_t rec_off;    // u64 block records, raster order (symbols.h)
+	uint32_t pin_off;    // u8 parent info, raster order
+	int dx, dy, pitch, is_int;
+	int high;            // finest level (HIGH Huffman tables, k >= 1)
+	int has_pin;         // has a parent level (not the coarsest)
+	int par;             // decoder: index into b[] of the parent band, or -1
+};
+
+// Frames f = 0..n-1 (blockIdx.x): arena + f * astride, out + f * ostride.
+// b[] in coding order: coarsest level first, V, H, D (CodeBand order).
+struct GEncArgs {
+	const char* arena;
+	size_t astride;
+	uint8_t* out;
+	size_t ostride;
+	size_t cap;                      // bytes available at each out
+	uint32_t* res;                   // per frame: file length, status (0 ok, 1 capacity, 2 ring timeout)
+	uint32_t status_off;
+	int w, h, q, trans;
+	int nb;
+	GBandDesc ll;
+	GBandDesc b[3 * kMaxLevels];
+};
+
+// k_gc_encode over n frames: the whole .ric file of each (gray, one plane).
+// dev_args: the argument block in device memory.
+int launch_gc_encode(const GEncArgs* dev_args, int nframes, hipStream_t st);
+
+// Fill the band descriptors (coding order) of a pyramid.
+inline void gc_bands(const Pyramid& P, GBandDesc& ll, GBandDesc* b, int& nb)
+{
+	auto desc = [&](const Band& B, GBandDesc& d) {
+		d.off = (uint32_t)B.off; d.dx = B.dx; d.dy = B.dy; d.pitch = B.pitch; d.is_int = B.is_int;
+		d.rec_off = d.pin_off = 0; d.high = 0; d.has_pin = 0; d.par = -1;
+	};
+	desc(P.L[P.nlev - 1].b[BL], ll);
+	nb = 0;
+	const int order[3] = {BV, BH, BD};
+	for (int l = P.nlev - 1; l >= 0; l--)
+		for (int k = 0; k < 3; k++) {
+			GBandDesc& d = b[nb];
+			desc(P.L[l].b[order[k]], d);
+			d.rec_off = (uint32_t)P.rec_off[l][order[k]];
+			d.pin_off = (uint32_t)P.pin_off[l][order[k]];
+			d.high = l == 0;
+			d.has_pin = l + 1 < P.nlev;
+			d.par = l + 1 < P.nlev ? nb - 3 : -1;
+			nb++;
+		}
+}
+
+}  // namespace ric

@@ -89,6 +89,7 @@ def lib():
         "ric_batch_decode": (_I, [_P, _P, _P, _I, _P, _I]),
         "ric_batch_roundtrip": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _P]),
         "ric_batch_prof_enable": (_I, [_P, _I]),
+        "ric_batch_encode_gpu": (_I, [_P, _P, _I, _I, _I, _P, ctypes.c_size_t, ctypes.c_size_t, _P]),
         "ric_batch_diag_gpu": (_I, [_P, _P, _I, _I, _I, _I, _P]),
         "ric_batch_prof_read": (_I, [_P, _P, _P, _P, _I]),
     }
@@ -318,6 +319,16 @@ class Batch:
         _chk(lib().ric_batch_encode(self.h, _ptrs(frames), n, int(dev), q, trans, _ptrs(outs), caps, lens),
              "ric_batch_encode")
         return [outs[i][:lens[i]].tobytes() for i in range(n)]
+
+    def compress_gpu(self, frames, out, ostride, q=9, trans=0):
+        """Whole encode on the GPU (ric_batch_encode_gpu): frames are device
+        pixel pointers/tensors, out a device buffer of len(frames) * ostride
+        bytes; returns the files' sizes (the files stay in device memory)."""
+        n = len(frames)
+        lens = (ctypes.c_size_t * n)()
+        _chk(lib().ric_batch_encode_gpu(self.h, _ptrs(frames), n, q, trans, _ptr(out), ostride, ostride, lens),
+             "ric_batch_encode_gpu")
+        return [lens[i] for i in range(n)]
 
     def decompress(self, rics, pix_out=None):
         """Host mode: returns a list of (channels, h, w) uint8 arrays.  Device
