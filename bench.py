@@ -99,6 +99,12 @@ def parse():
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-gather", action="store_true", help="N>1: skip the per-step stream gather to rank 0")
     ap.add_argument("--no-split", action="store_true", help="skip the encode-only / decode-only timing")
+    ap.add_argument("--coder", default="host", choices=["host", "hybrid", "gpu"],
+                    help="serial coder: host threads; hybrid = GPU stream encoder + host decoder; gpu = GPU stream "
+                         "encoder and decoder (one wave per stream), host threads doing whole round trips beside it")
+    ap.add_argument("--pool", type=int, default=512, help="hybrid: frames per GPU stream-coder launch")
+    ap.add_argument("--n-host", type=int, default=-1,
+                    help="hybrid: frames per step encoded on the host while the first coder launch runs (default 16 per thread)")
     return ap.parse_args()
 
 
@@ -247,9 +253,21 @@ def main():
     gathered = [0]
     container = [None]
 
+    hybrid = a.coder in ("hybrid", "gpu") and CH == 1 and b is not None
+    gpu_dec = a.coder == "gpu"
+    n_host = 0
+    if hybrid:
+        n_host = a.n_host if a.n_host >= 0 else min(nfr, 16 * threads)
+        # stream capacity: 3 bits per pixel (a q9 C3 stream is 1.7), 16-byte multiple
+        b.cp_pool = min(a.pool, max(nfr - n_host, 1))
+        b.hybrid_config(b.cp_pool, (W * H * 3 // 8 + 65536) // 16 * 16)
+
     def step():
         if b is not None:
-            b.roundtrip(frames, outs, q=a.q, trans=a.trans)
+            if hybrid:
+                b.roundtrip_hybrid(frames, outs, n_host, q=a.q, trans=a.trans, gpu_decode=gpu_dec)
+            else:
+                b.roundtrip(frames, outs, q=a.q, trans=a.trans)
         if gather and a.workload == "C4":
             # C4: the tile streams to rank 0 into one RTL1 container, and the
             # decode side of the exchange: the container's tiles scattered
@@ -310,6 +328,12 @@ def main():
             ok &= r0 == chk.encode_ric(host0, a.q, a.trans)
             ok &= bool(np.array_equal(outs[0].cpu().numpy(), chk.decode_ric(r0)[0]))
             notes.append("frame %d vs oracle port" % mine[0][0])
+            if hybrid and n_host < nfr:
+                k = n_host                     # the first frame the GPU stream coder encoded
+                rk = b.stream(k)
+                ok &= rk == chk.encode_ric(frames[k].cpu().numpy(), a.q, a.trans)
+                ok &= bool(np.array_equal(outs[k].cpu().numpy(), chk.decode_ric(rk)[0]))
+                notes.append("frame %d (GPU stream coder) vs oracle port" % mine[k][0])
             gold = json.load(open(os.path.join(REPO, "tests", "golden", "golden.json")))["large"]
             want = None
             if a.q == 9 and a.trans == 0:
@@ -410,7 +434,12 @@ def main():
         "dtype": "int16",
         "data": "synthetic (SURVEY.md §8(d) generator), resident in HBM",
         "config": {"workload": wl, "frames_per_gpu_per_step": nfr, "frames_per_launch": slots,
-                   "host_coder_threads_per_gpu": threads, "parallelism": "frames sharded over %d GPU(s)" % world},
+                   "host_coder_threads_per_gpu": threads, "parallelism": "frames sharded over %d GPU(s)" % world,
+                   "coder": ("GPU stream coder (one wave per stream, %d streams per launch): encode%s of %d of %d "
+                             "frames; host threads: %s" % (b.cp_pool, " and decode" if gpu_dec else "", nfr - n_host, nfr,
+                                                           "round trips of the rest" if gpu_dec else
+                                                           "round trips of the rest and every decode")) if hybrid
+                   else "host threads (encode and decode)"},
         "verified": verified,
         "verified_against": vnote,
         "roofline": {"bound": "hbm",

@@ -173,10 +173,27 @@ int ric_batch_roundtrip(ric_batch* b, const uint8_t* const* pix, int n, int q, i
  * one host thread). */
 int ric_batch_encode_gpu(ric_batch* b, const uint8_t* const* pix, int n, int q, int trans, uint8_t* out, size_t ostride,
                          size_t cap, size_t* len);
+/* The whole DecompressImage of n <= slots gray frames on the GPU, the serial
+ * decoder included (one wave per stream): the .ric files at in + i * istride
+ * (DEVICE memory, istride a multiple of 16), their sizes len[i]; pixels to
+ * device pix_out[i].  RIC_E_STREAM as ric_batch_decode. */
+int ric_batch_decode_gpu(ric_batch* b, const uint8_t* in, size_t istride, const size_t* len, int n, uint8_t* const* pix_out);
+/* Hybrid round trip (gray): the serial encoder runs on the GPU (one wave per
+ * stream, launches of `pool_frames` frames, each stream up to stream_cap
+ * bytes: a multiple of 16; a longer stream fails the call with
+ * RIC_E_CAPACITY), the serial decoder on the host pool.  Configure once. */
+int ric_batch_hybrid_config(ric_batch* b, int pool_frames, size_t stream_cap);
+/* As ric_batch_roundtrip (device pixels in and out, .ric files to host
+ * out[i]): frames [0, n_host) encoded and decoded on the host; frames
+ * [n_host, n) encoded by the GPU stream coder and decoded by the GPU stream
+ * decoder (gpu_decode) or on the host.  Byte-identical streams either way. */
+int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, int n_host, int gpu_decode, int q,
+                               int trans, uint8_t* const* out, const size_t* cap, size_t* len, uint8_t* const* pix_out);
 /* Stage timers of the batch (no reference counterpart): 0 pixel conversion
  * in, 1..8 forward level 0..7 (fused DWT + quantiser + records), 9 D2H of
  * bands + records, 10 host encode, 11 host decode, 12 H2D of the bands,
- * 13..20 inverse level 0..7 (fused TSUQi), 21 pixel conversion out.  ms are
+ * 13..20 inverse level 0..7 (fused TSUQi), 21 pixel conversion out.  With the
+ * GPU stream coder, stage 10 is its launches (frames = streams coded).  ms are
  * sums; frames = frames covered; launches = GPU launches (host: frames). */
 #define RIC_BATCH_STAGES 22
 /* Diagnostics: the batch's GPU stages alone, iters times over n <= slots

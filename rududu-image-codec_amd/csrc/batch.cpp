@@ -113,6 +113,11 @@ public:
 		std::unique_lock<std::mutex> lk(mu_);
 		cv_.wait(lk, [this] { return left_ <= 0; });
 	}
+	bool wait_for_ms(int ms)
+	{
+		std::unique_lock<std::mutex> lk(mu_);
+		return cv_.wait_for(lk, std::chrono::milliseconds(ms), [this] { return left_ <= 0; });
+	}
 
 private:
 	std::mutex mu_;
@@ -208,8 +213,25 @@ struct ric_batch {
 	// GPU stream coder (gcoder.hip): argument block, per-slot results
 	GEncArgs genc{};
 	GEncArgs* d_genc = nullptr;
+	GDecArgs gdec{};
+	GDecArgs* d_gdec = nullptr;
 	uint32_t* d_res = nullptr;                     // 2 per slot
 	uint32_t* h_res = nullptr;                     // pinned
+	// hybrid round trip: the pool of frames the GPU stream coder works on
+	struct CoderPool {
+		int n = 0;                                 // frames per coder launch
+		size_t abstride = 0, ocap = 0;             // A+B bytes per frame, stream bytes per frame
+		char* d_ab = nullptr;                      // 2 halves of n frames' bands + records
+		uint8_t* d_out = nullptr;                  // 2 halves of n streams
+		GEncArgs* d_args = nullptr;                // argument blocks, one per half
+		GDecArgs* d_dargs = nullptr;
+		GEncArgs args[2];
+		GDecArgs dargs[2];
+		uint32_t* d_res = nullptr;                 // per half: 2 n encoder words, n decoder words
+		uint32_t* h_res = nullptr;                 // pinned mirror
+		hipStream_t st[2] = {nullptr, nullptr};    // coder stream of each half
+		hipEvent_t ev_fwd[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr};
+	} cp;
 
 	int nslot() const { return 2 * slots; }
 	char* arena(int s) const { return d_arena + (size_t)s * astride; }
@@ -303,13 +325,15 @@ int gpu_encode_plane(ric_batch* b, int set, int n, int p, const uint8_t* const* 
 // The GPU half of DecompressImage for plane p of n frames of set `set`: the
 // host-decoded bands to the device (one strided copy), then every inverse
 // level with the fused TSUQi factors of each frame, as one launch per level.
-int gpu_decode_plane(ric_batch* b, int set, int n, int p, const int* qs, int trans)
+int gpu_decode_plane(ric_batch* b, int set, int n, int p, const int* qs, int trans, bool h2d = true)
 {
 	Pyramid& P = b->P;
 	const int s0 = set * b->slots;
-	auto sp = b->prof.begin(B_H2D, n, b->st);
-	BCHK(hipMemcpy2DAsync(b->arena(s0), b->astride, b->harena(s0), b->hstride, P.a_end, n, hipMemcpyHostToDevice, b->st));
-	b->prof.end(sp);
+	if (h2d) {
+		auto sp = b->prof.begin(B_H2D, n, b->st);
+		BCHK(hipMemcpy2DAsync(b->arena(s0), b->astride, b->harena(s0), b->hstride, P.a_end, n, hipMemcpyHostToDevice, b->st));
+		b->prof.end(sp);
+	}
 	P.set_weight(trans);
 	std::vector<int> qf(4 * n);
 	for (int l = P.nlev - 1; l >= 0; l--) {
@@ -534,8 +558,25 @@ void ric_batch_destroy(ric_batch* b)
 	if (b->d_planes) (void)hipFree(b->d_planes);
 	if (b->d_stage) (void)hipFree(b->d_stage);
 	if (b->d_genc) (void)hipFree(b->d_genc);
+	if (b->d_gdec) (void)hipFree(b->d_gdec);
 	if (b->d_res) (void)hipFree(b->d_res);
 	if (b->h_res) (void)hipHostFree(b->h_res);
+	{
+		auto& c = b->cp;
+		for (int h = 0; h < 2; h++)
+			if (c.st[h]) (void)hipStreamSynchronize(c.st[h]);
+		if (c.d_ab) (void)hipFree(c.d_ab);
+		if (c.d_out) (void)hipFree(c.d_out);
+		if (c.d_args) (void)hipFree(c.d_args);
+		if (c.d_dargs) (void)hipFree(c.d_dargs);
+		if (c.d_res) (void)hipFree(c.d_res);
+		if (c.h_res) (void)hipHostFree(c.h_res);
+		for (int h = 0; h < 2; h++) {
+			if (c.ev_fwd[h]) (void)hipEventDestroy(c.ev_fwd[h]);
+			if (c.ev_done[h]) (void)hipEventDestroy(c.ev_done[h]);
+			if (c.st[h]) (void)hipStreamDestroy(c.st[h]);
+		}
+	}
 	if (b->st) (void)hipStreamDestroy(b->st);
 	delete b;
 }
@@ -736,6 +777,358 @@ int ric_batch_encode_gpu(ric_batch* b, const uint8_t* const* pix, int n, int q, 
 		if (b->h_res[2 * i + 1]) return RIC_E_CAPACITY;
 	}
 	return RIC_OK;
+}
+
+// The whole DecompressImage of n gray frames on the GPU: the serial decoder
+// of every stream on one wave each (gcoder.hip k_gc_decode) into the bands of
+// slot set 0, then the inverse levels and the pixel conversion.  in: the .ric
+// files at in + i * istride (device, istride a multiple of 16), len[i] their
+// sizes (host); pix_out[i] device pixels.  RIC_E_STREAM when a stream ran past
+// its end (the frames are still written), as ric_batch_decode.
+int ric_batch_decode_gpu(ric_batch* b, const uint8_t* in, size_t istride, const size_t* len, int n, uint8_t* const* pix_out)
+{
+	if (!b || !in || !len || !pix_out || n < 0 || n > b->slots || (istride & 15) || istride > 0xFFFFFFF0u) return RIC_E_ARG;
+	if (b->channels != 1) return RIC_E_ARG;
+	if (n == 0) return RIC_OK;
+	if (set_dev(b->device)) return RIC_E_HIP;
+	if (!b->d_genc) {
+		BCHK(hipMalloc(&b->d_genc, sizeof(GEncArgs)));
+		BCHK(hipMalloc(&b->d_res, sizeof(uint32_t) * 2 * b->nslot()));
+		BCHK(hipHostMalloc(&b->h_res, sizeof(uint32_t) * 2 * b->nslot(), 0));
+	}
+	if (!b->d_gdec) BCHK(hipMalloc(&b->d_gdec, sizeof(GDecArgs)));
+	int q0 = -1, t0 = -1;
+	std::vector<int> qs(n);
+	for (int i = 0; i < n; i++) {
+		if (len[i] > istride || len[i] > 0xFFFFFFF0u) return RIC_E_ARG;
+		// the header: the host reads it from device memory (9 bytes per frame)
+		uint8_t hd[9];
+		BCHK(hipMemcpy(hd, in + (size_t)i * istride, 9, hipMemcpyDeviceToHost));
+		int w, h, ch, q, t;
+		int rc = ric_read_header(hd, len[i], &w, &h, &ch, &q, &t);
+		if (rc) return rc;
+		if (w != b->w || h != b->h || ch != 1 || t > 2) return RIC_E_ARG;
+		if (t0 >= 0 && t != t0) return RIC_E_ARG;
+		t0 = t; q0 = q; qs[i] = q;
+	}
+	(void)q0;
+	// lengths to the device (the coder reads them per frame)
+	for (int i = 0; i < n; i++) b->h_res[2 * i] = (uint32_t)len[i];
+	BCHK(hipMemcpyAsync(b->d_res, b->h_res, sizeof(uint32_t) * 2 * n, hipMemcpyHostToDevice, b->st));
+	GDecArgs& a = b->gdec;
+	a.arena = b->arena(0); a.astride = b->astride;
+	a.in = in; a.istride = istride;
+	a.lens = b->d_res; a.lens_stride = 2;
+	a.res = b->d_res + 2 * b->slots;          // after the lengths (2 words per frame)
+	a.w = b->w; a.h = b->h;
+	gc_bands(b->P, a.ll, a.b, a.nb);
+	BCHK(hipMemcpyAsync(b->d_gdec, &a, sizeof(GDecArgs), hipMemcpyHostToDevice, b->st));
+	auto sp = b->prof.begin(B_HDEC, n, b->st);
+	if (launch_gc_decode(b->d_gdec, n, b->st)) return bfail(hipGetLastError(), "k_gc_decode") ? RIC_E_HIP : RIC_E_HIP;
+	b->prof.end(sp);
+	int rc = gpu_decode_plane(b, 0, n, 0, qs.data(), t0, false);
+	if (rc) return rc;
+	rc = gpu_pix_out(b, 0, n, qs.data(), pix_out, 1);
+	if (rc) return rc;
+	BCHK(hipMemcpyAsync(b->h_res + 2 * b->slots, b->d_res + 2 * b->slots, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, b->st));
+	BCHK(hipStreamSynchronize(b->st));
+	b->prof.harvest();
+	int result = RIC_OK;
+	for (int i = 0; i < n; i++) {
+		const uint32_t r = b->h_res[2 * b->slots + i];
+		if (r == 3) { set_last_error("GPU stream decoder: staging overrun (pathological stream)"); return RIC_E_CAPACITY; }
+		if (r == 1) result = RIC_E_STREAM;
+	}
+	return result;
+}
+
+// ------------------------------------------------------------ hybrid
+// Round trips with the serial coder on the GPU (gcoder.hip: one wave per
+// frame's stream).  Frames go to the GPU coder in launches of `pool_frames`:
+// their forward levels run in groups of `slots` on the batch stream and each
+// group's bands + records are copied into one half of the pool; then, on that
+// half's coder stream, k_gc_encode codes them all and (gpu_decode) k_gc_decode
+// decodes the streams back into the pool, whose bands go through the inverse
+// levels in groups.  Without gpu_decode the host pool decodes the streams.
+// A coder launch takes seconds (a wave codes one whole stream), so two
+// launches are in flight (the two halves) and the host threads meanwhile do
+// whole round trips of the first n_host frames.
+int ric_batch_hybrid_config(ric_batch* b, int pool_frames, size_t stream_cap)
+{
+	if (!b || pool_frames < 1 || pool_frames > 65536 || stream_cap < 64 || (stream_cap & 15) || stream_cap > 0xFFFFFFF0u)
+		return RIC_E_ARG;
+	if (b->channels != 1) return RIC_E_ARG;
+	if (set_dev(b->device)) return RIC_E_HIP;
+	auto& c = b->cp;
+	for (int h = 0; h < 2; h++)
+		if (c.st[h]) BCHK(hipStreamSynchronize(c.st[h]));
+	if (c.d_ab) { BCHK(hipFree(c.d_ab)); c.d_ab = nullptr; }
+	if (c.d_out) { BCHK(hipFree(c.d_out)); c.d_out = nullptr; }
+	if (c.d_res) { BCHK(hipFree(c.d_res)); c.d_res = nullptr; }
+	if (c.h_res) { BCHK(hipHostFree(c.h_res)); c.h_res = nullptr; }
+	c.n = pool_frames;
+	c.abstride = (b->P.b_end + 65535) / 65536 * 65536;
+	c.ocap = stream_cap;
+	BCHK(hipMalloc(&c.d_ab, 2 * c.abstride * c.n));
+	BCHK(hipMalloc(&c.d_out, 2 * c.ocap * c.n));
+	BCHK(hipMalloc(&c.d_res, sizeof(uint32_t) * 6 * c.n));          // per half: 2 n encoder words, n decoder words
+	BCHK(hipHostMalloc(&c.h_res, sizeof(uint32_t) * 6 * c.n, 0));
+	if (!c.d_args) BCHK(hipMalloc(&c.d_args, 2 * sizeof(GEncArgs)));
+	if (!c.d_dargs) BCHK(hipMalloc(&c.d_dargs, 2 * sizeof(GDecArgs)));
+	for (int h = 0; h < 2; h++) {
+		if (!c.st[h]) BCHK(hipStreamCreateWithFlags(&c.st[h], hipStreamNonBlocking));
+		if (!c.ev_fwd[h]) BCHK(hipEventCreateWithFlags(&c.ev_fwd[h], hipEventDisableTiming));
+		if (!c.ev_done[h]) BCHK(hipEventCreateWithFlags(&c.ev_done[h], hipEventDisableTiming));
+	}
+	return RIC_OK;
+}
+
+namespace {
+
+// one group of at most `slots` frames through a slot set
+struct HGroup {
+	int f0 = 0, m = 0;
+	bool gpu = false;         // stream coded on the GPU (tasks: decode only)
+	int half = 0;             // its streams' half of cp.d_out
+	int k0 = 0;               // index of f0 in that half
+};
+
+}  // namespace
+
+int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, int n_host, int gpu_decode, int q,
+                               int trans, uint8_t* const* out, const size_t* cap, size_t* len, uint8_t* const* pix_out)
+{
+	if (!b || !pix || !out || !cap || !len || !pix_out || n < 0 || n_host < 0 || n_host > n || q < 0 || q > 31 ||
+	    trans < 0 || trans > 2)
+		return RIC_E_ARG;
+	if (b->channels != 1) return RIC_E_ARG;
+	if (n_host < n && !b->cp.d_ab) return RIC_E_ARG;    // ric_batch_hybrid_config first
+	if (n == 0) return RIC_OK;
+	if (set_dev(b->device)) return RIC_E_HIP;
+	auto& c = b->cp;
+	Pyramid& P = b->P;
+	const int S = b->slots;
+	auto res_enc = [&](int h) { return (size_t)h * 3 * c.n; };           // word offsets into d_res / h_res
+	auto res_dec = [&](int h) { return (size_t)h * 3 * c.n + 2 * (size_t)c.n; };
+	if (c.d_ab) {
+		for (int h = 0; h < 2; h++) {
+			GEncArgs& a = c.args[h];
+			a.arena = c.d_ab + (size_t)h * c.n * c.abstride; a.astride = c.abstride;
+			a.out = c.d_out + (size_t)h * c.n * c.ocap; a.ostride = c.ocap; a.cap = c.ocap;
+			a.res = c.d_res + res_enc(h);
+			a.status_off = (uint32_t)P.status_off;
+			a.w = b->w; a.h = b->h; a.q = q; a.trans = trans;
+			gc_bands(P, a.ll, a.b, a.nb);
+			GDecArgs& d = c.dargs[h];
+			d.arena = (char*)a.arena; d.astride = a.astride;
+			d.in = a.out; d.istride = c.ocap;
+			d.lens = a.res; d.lens_stride = 2;
+			d.res = c.d_res + res_dec(h);
+			d.w = b->w; d.h = b->h;
+			gc_bands(P, d.ll, d.b, d.nb);
+		}
+		BCHK(hipMemcpy(c.d_args, c.args, sizeof(c.args), hipMemcpyHostToDevice));
+		BCHK(hipMemcpy(c.d_dargs, c.dargs, sizeof(c.dargs), hipMemcpyHostToDevice));
+	}
+	std::deque<HGroup> ready_host, ready_dec;
+	for (int f0 = 0; f0 < n_host; f0 += S) ready_host.push_back({f0, std::min(S, n_host - f0), false, 0, 0});
+	const int ng = n - n_host;
+	const int nbatch = ng > 0 ? (ng + c.n - 1) / c.n : 0;
+	int kicked = 0, finished = 0;
+	std::vector<Latch> copied(nbatch > 0 ? nbatch : 1);   // host decode: a batch's streams are out of d_out
+	int rc = RIC_OK;
+	bool stream_err = false;
+	std::vector<int> qs(S, q);
+	auto batch_f0 = [&](int j) { return n_host + j * c.n; };
+	auto batch_m = [&](int j) { return std::min(c.n, n - batch_f0(j)); };
+	auto abslot = [&](int h, int k) { return c.d_ab + ((size_t)h * c.n + k) * c.abstride; };
+	// batch j: forward levels in groups of S (slot set 0; stream order keeps it
+	// clear of the groups using the arenas), bands + records into pool half
+	// j & 1, then the coder launches on that half's stream
+	auto kick = [&](int j) -> int {
+		const int f0 = batch_f0(j), m = batch_m(j), h = j & 1;
+		for (int g0 = 0; g0 < m; g0 += S) {
+			const int gm = std::min(S, m - g0);
+			int r = gpu_encode_plane(b, 0, gm, 0, pix + f0 + g0, q, trans, false);
+			if (r) return r;
+			BCHK(hipMemcpy2DAsync(abslot(h, g0), c.abstride, b->arena(0), b->astride, P.b_end, gm, hipMemcpyDeviceToDevice,
+			                      b->st));
+		}
+		BCHK(hipEventRecord(c.ev_fwd[h], b->st));
+		BCHK(hipStreamWaitEvent(c.st[h], c.ev_fwd[h], 0));
+		auto sp = b->prof.begin(B_HENC, m, c.st[h]);
+		if (launch_gc_encode(c.d_args + h, m, c.st[h])) return bfail(hipGetLastError(), "k_gc_encode") ? RIC_E_HIP : RIC_E_HIP;
+		b->prof.end(sp);
+		if (gpu_decode) {
+			auto sd = b->prof.begin(B_HDEC, m, c.st[h]);
+			if (launch_gc_decode(c.d_dargs + h, m, c.st[h]))
+				return bfail(hipGetLastError(), "k_gc_decode") ? RIC_E_HIP : RIC_E_HIP;
+			b->prof.end(sd);
+		}
+		BCHK(hipMemcpyAsync(c.h_res + res_enc(h), c.d_res + res_enc(h), sizeof(uint32_t) * 3 * c.n, hipMemcpyDeviceToHost,
+		                    c.st[h]));
+		BCHK(hipEventRecord(c.ev_done[h], c.st[h]));
+		copied[j].reset(gpu_decode ? 0 : m);
+		return RIC_OK;
+	};
+	// batch j's coder launches are done: (host decode) its decode groups become
+	// ready; (gpu_decode) its frames go through the inverse levels right away
+	auto harvest = [&](int j) -> int {
+		const int f0 = batch_f0(j), m = batch_m(j), h = j & 1;
+		const uint32_t* re = c.h_res + res_enc(h);
+		const uint32_t* rd = c.h_res + res_dec(h);
+		for (int k = 0; k < m; k++) {
+			if (re[2 * k + 1] == 2) {
+				clear_status(b);
+				set_last_error("fused level kernel: LDS ring hand-off timed out (device status word set; output discarded)");
+				return RIC_E_HIP;
+			}
+			if (re[2 * k + 1]) {
+				set_last_error("GPU stream coder: a stream larger than the pool's stream capacity");
+				return RIC_E_CAPACITY;
+			}
+			if (re[2 * k] > cap[f0 + k]) return RIC_E_CAPACITY;
+			len[f0 + k] = re[2 * k];
+			if (gpu_decode) {
+				if (rd[k] == 3) { set_last_error("GPU stream decoder: staging overrun"); return RIC_E_CAPACITY; }
+				stream_err |= rd[k] == 1;
+			}
+		}
+		if (!gpu_decode) {
+			for (int g0 = 0; g0 < m; g0 += S) ready_dec.push_back({f0 + g0, std::min(S, m - g0), true, h, g0});
+			return RIC_OK;
+		}
+		for (int g0 = 0; g0 < m; g0 += S) {
+			const int gm = std::min(S, m - g0);
+			BCHK(hipMemcpy2DAsync(b->arena(0), b->astride, abslot(h, g0), c.abstride, P.a_end, gm, hipMemcpyDeviceToDevice,
+			                      b->st));
+			int r = gpu_decode_plane(b, 0, gm, 0, qs.data(), trans, false);
+			if (!r) r = gpu_pix_out(b, 0, gm, qs.data(), pix_out + f0 + g0, 1);
+			if (r) return r;
+		}
+		for (int k = 0; k < m; k++)
+			BCHK(hipMemcpyAsync(out[f0 + k], c.d_out + ((size_t)h * c.n + k) * c.ocap, len[f0 + k], hipMemcpyDeviceToHost,
+			                    b->st));
+		return RIC_OK;
+	};
+	struct Flight {
+		HGroup g;
+		int set;
+		hipEvent_t ev;
+		Latch done;
+		FirstErr err;
+	};
+	std::deque<Flight> fl;
+	std::vector<hipEvent_t> evs(2, nullptr);
+	for (auto& e : evs) BCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+	bool set_busy[2] = {false, false};
+	auto launch_group = [&](const HGroup& g) -> int {
+		const int set = set_busy[0] ? 1 : 0;
+		set_busy[set] = true;
+		fl.emplace_back();
+		Flight& F = fl.back();
+		F.g = g; F.set = set; F.ev = evs[set];
+		if (!g.gpu) {
+			int r = gpu_encode_plane(b, set, g.m, 0, pix + g.f0, q, trans);
+			if (r) return r;
+			BCHK(hipEventRecord(F.ev, b->st));
+		}
+		F.done.reset(g.m);
+		for (int i = 0; i < g.m; i++) {
+			const int slot = set * S + i, f = g.f0 + i;
+			Flight* pf = &F;
+			if (!g.gpu) {
+				b->pool->submit([=] {
+					int r1 = bfail(hipEventSynchronize(pf->ev), "hipEventSynchronize") ? RIC_E_HIP : RIC_OK;
+					if (!r1) r1 = host_encode_plane(b, slot, 0, q, trans, out[f], cap[f], &len[f]);
+					if (!r1) r1 = host_decode_plane(b, slot, 0, out[f], len[f]);
+					pf->err.put(r1);
+					pf->done.done();
+				});
+			} else {
+				const uint8_t* src = c.d_out + ((size_t)g.half * c.n + g.k0 + i) * c.ocap;
+				Latch* cl = &copied[(f - n_host) / c.n];
+				b->pool->submit([=] {
+					int r1 = set_dev(b->device);
+					if (!r1) r1 = bfail(hipMemcpy(out[f], src, len[f], hipMemcpyDeviceToHost), "hipMemcpy stream") ? RIC_E_HIP
+					                                                                                            : RIC_OK;
+					cl->done();
+					// the set's mirrors: the previous group's H2D from them has passed
+					if (!r1) r1 = bfail(hipEventSynchronize(pf->ev), "hipEventSynchronize") ? RIC_E_HIP : RIC_OK;
+					if (!r1) r1 = host_decode_plane(b, slot, 0, out[f], len[f]);
+					pf->err.put(r1);
+					pf->done.done();
+				});
+			}
+		}
+		return RIC_OK;
+	};
+	auto finish_group = [&]() -> int {
+		Flight& F = fl.front();
+		const int r = F.err.get();
+		int r2 = RIC_OK;
+		if (r && r != RIC_E_STREAM) r2 = r;
+		stream_err |= r == RIC_E_STREAM;
+		if (!r2) r2 = gpu_decode_plane(b, F.set, F.g.m, 0, qs.data(), trans);
+		if (!r2) r2 = gpu_pix_out(b, F.set, F.g.m, qs.data(), pix_out + F.g.f0, 1);
+		if (!r2) BCHK(hipEventRecord(F.ev, b->st));   // the set's mirrors are free once this passes
+		set_busy[F.set] = false;
+		fl.pop_front();
+		return r2;
+	};
+	bool running[2] = {false, false};
+	while (rc == RIC_OK && (finished < nbatch || !ready_host.empty() || !ready_dec.empty() || !fl.empty())) {
+		// the oldest coder batch (batches finish in order: one per half, alternating)
+		if (finished < kicked) {
+			const int h = finished & 1;
+			const hipError_t e = hipEventQuery(c.ev_done[h]);
+			if (e == hipSuccess) {
+				running[h] = false;
+				rc = harvest(finished);
+				finished++;
+				if (rc) break;
+			} else if (e != hipErrorNotReady) {
+				rc = bfail(e, "coder stream") ? RIC_E_HIP : RIC_E_HIP;
+				break;
+			}
+		}
+		// kick the next batch when its half is free: the batch before it on that
+		// half has been harvested and (host decode) its streams copied out
+		while (rc == RIC_OK && kicked < nbatch && kicked - finished < 2 &&
+		       (kicked < 2 || copied[kicked - 2].wait_for_ms(0))) {
+			rc = kick(kicked);
+			running[kicked & 1] = rc == RIC_OK;
+			kicked++;
+		}
+		if (rc) break;
+		while (fl.size() < 2 && (!ready_dec.empty() || !ready_host.empty())) {
+			HGroup g;
+			if (!ready_dec.empty()) { g = ready_dec.front(); ready_dec.pop_front(); }
+			else { g = ready_host.front(); ready_host.pop_front(); }
+			rc = launch_group(g);
+			if (rc) break;
+		}
+		if (rc) break;
+		if (!fl.empty()) {
+			if (fl.front().done.wait_for_ms(finished < kicked ? 2 : 20)) {
+				rc = finish_group();
+				if (rc) break;
+			}
+		} else {
+			std::this_thread::sleep_for(std::chrono::milliseconds(1));
+		}
+	}
+	// on an error: let queued tasks and the coder finish before returning
+	while (!fl.empty()) { fl.front().done.wait(); fl.pop_front(); }
+	for (int h = 0; h < 2; h++)
+		if (c.st[h]) (void)hipStreamSynchronize(c.st[h]);
+	const bool ok = !bfail(hipStreamSynchronize(b->st), "hipStreamSynchronize");
+	for (auto& e : evs) (void)hipEventDestroy(e);
+	if (rc == RIC_E_HIP) clear_status(b);
+	if (rc) return rc;
+	if (!ok) return RIC_E_HIP;
+	b->prof.harvest();
+	return stream_err ? RIC_E_STREAM : RIC_OK;
 }
 
 // Diagnostics: the GPU stages alone, `iters` times over n frames (slot set

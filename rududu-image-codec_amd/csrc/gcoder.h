@@ -35,6 +35,25 @@ struct GEncArgs {
 	GBandDesc b[3 * kMaxLevels];
 };
 
+// Frames f = 0..n-1 (blockIdx.x): the .ric file at in + f * istride (istride
+// bytes readable, a multiple of 16), its length lens[f * lens_stride]; the
+// decoded bands to arena + f * astride.  res[f]: 0 ok, 1 the stream ran past
+// its end (RIC_E_STREAM, bands still written), 3 LDS staging overrun.
+struct GDecArgs {
+	char* arena;
+	size_t astride;
+	const uint8_t* in;
+	size_t istride;
+	const uint32_t* lens;
+	int lens_stride;
+	uint32_t* res;
+	int w, h;
+	int nb;
+	GBandDesc ll;
+	GBandDesc b[3 * kMaxLevels];
+};
+int launch_gc_decode(const GDecArgs* dev_args, int nframes, hipStream_t st);
+
 // k_gc_encode over n frames: the whole .ric file of each (gray, one plane).
 // dev_args: the argument block in device memory.
 int launch_gc_encode(const GEncArgs* dev_args, int nframes, hipStream_t st);

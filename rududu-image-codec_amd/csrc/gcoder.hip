@@ -86,14 +86,9 @@ struct GEnc {
 	uint32_t flushed;                // bytes [0, flushed) are in HBM
 	uint32_t hdr0, hdr1, hdr2;       // the 9-byte .ric header (ric.cpp:142-152)
 
-	GC_DI void put(uint32_t slot, uint32_t v)
-	{
-		if (slot < cap) {
-			if (lane_id() == 0) g_ring[slot & (kRing - 1)] = (uint8_t)v;
-		} else {
-			ovf |= 1;
-		}
-	}
+	// every lane writes the same byte (no exec-mask change per byte); the
+	// capacity is checked where bytes leave the ring (maybe_flush / end)
+	GC_DI void put(uint32_t slot, uint32_t v) { g_ring[slot & (kRing - 1)] = (uint8_t)v; }
 	// copy ring bytes [flushed, upto) (upto a multiple of 16, or the end) to HBM
 	GC_DI void flush_to(uint32_t upto)
 	{
@@ -108,7 +103,7 @@ struct GEnc {
 		const uint32_t l = lane_id();
 		for (uint32_t b = flushed; b < upto; b += 64 * 16) {
 			const uint32_t o = b + l * 16;
-			if (o < upto && o + 16 <= ((cap + 15) & ~15u)) {
+			if (o < upto && o + 16 <= cap) {
 				const u32x4 v = *(const u32x4*)(g_ring + (o & (kRing - 1)));
 				*gst((u32x4*)(out + o)) = v;
 			}
@@ -122,6 +117,7 @@ struct GEnc {
 	GC_DI void maybe_flush()
 	{
 		if (p - flushed > kRing - 64) ovf |= 2;
+		if (p > cap) ovf |= 1;
 		uint32_t lw = reserved ? (reserved < q0 ? reserved : q0) : q0;
 		if (lw - flushed >= kFlush) {
 			lw &= ~(kFlush - 1);
@@ -130,11 +126,14 @@ struct GEnc {
 	}
 	GC_DI void raw_byte(uint32_t b)
 	{
-		if (!reserved) put(p++, b);
-		else { put(reserved, b); reserved = 0; }
+		const uint32_t slot = reserved ? reserved : p;
+		p += reserved ? 0u : 1u;
+		reserved = 0;
+		put(slot, b);
 	}
 	GC_DI void drain()                                   // emptyBuffer, muxcodec.cpp:536-548
 	{
+#pragma clang loop vectorize(disable) unroll(disable)
 		while (ebits >= 8) {
 			ebits -= 8;
 			raw_byte((uint32_t)(ebuf >> ebits) & 255u);
@@ -144,24 +143,28 @@ struct GEnc {
 	{
 		drain();                                         // flushBuffer<false>: complete bytes,
 		if (ebits > 0 && !reserved) reserved = p++;      // then reserve the partial one
+		uint32_t it = 0;
 		do {
 			put(q0, low >> 24);
 			if (((low + range - 1) ^ low) >= 0x01000000u) range = (0u - low) & 4095u;
 			q0 = q1; q1 = q2; q2 = q3; q3 = p++;
 			range <<= 8;
 			low <<= 8;
+			// a zero range would spin here forever (never on a valid stream;
+			// a wave that never ends takes the whole GPU down): stop and flag
+			if (__builtin_expect(++it > 4, 0)) { ovf |= 4; range = 1u << 16; }
 		} while (range <= 4096u);
 	}
 	GC_DI void bin(uint32_t freq, uint32_t bit)         // codeBin, muxcodec.h:156-163
 	{
-		if (range <= 4096u) norm();
+		if (__builtin_expect(range <= 4096u, 0)) norm();
 		const uint32_t t = (range * freq) >> 12;
 		low += t & (0u - bit);
 		range = t + ((range - 2 * t) & (0u - bit));
 	}
 	GC_DI void bits(uint32_t v, uint32_t len)           // bitsCode, 64-bit FIFO (entropy.h)
 	{
-		if (ebits + len > 64) drain();
+		if (__builtin_expect(ebits + len > 64, 0)) drain();
 		ebuf = (ebuf << len) | v;
 		ebits += len;
 	}
@@ -209,7 +212,7 @@ struct GBit {
 		e.bin(freq, s ^ 1);
 		freq = (freq + (s << (9 - sh)) - (freq >> (3 + sh))) & 0xFFFFu;
 		const uint32_t th = lget(T.bit_thr, sh), t0 = th & 0xFFFFu, t1 = th >> 16;
-		if (((freq - t1) & 0xFFFFu) > t0 - t1) {
+		if (__builtin_expect(((freq - t1) & 0xFFFFu) > t0 - t1, 0)) {
 			if (freq > t0) {
 				if (sh == 0) { mps ^= 1; freq = 4096u - freq; sh = 1; }
 				else sh--;
@@ -232,7 +235,9 @@ struct GGeoCtx {
 		const uint32_t ks = lget(T.geo_ks, idx), k = ks & 0xFFu, s = ks >> 8;
 		const uint32_t f = freq;
 		uint32_t fr = freq;
-		for (uint32_t l = sym >> k; l > 0; l--) {
+		uint32_t run = sym >> k;
+		if (__builtin_expect(run > (1u << 20), 0)) { run = 0; e.ovf |= 4; }   // not a coefficient of this path
+		for (uint32_t l = run; l > 0; l--) {
 			e.bin(f, 1);
 			fr -= fr >> (3 + s);
 		}
@@ -241,7 +246,7 @@ struct GGeoCtx {
 		else if (k > 0) e.bits(sym & ((1u << k) - 1), k);
 		fr = (fr + ((4096u - fr) >> (3 + s))) & 0xFFFFu;
 		const uint32_t th = lget(T.geo_thr, s), t0 = th & 0xFFFFu, t1 = th >> 16;
-		if (((fr - t0) & 0xFFFFu) > t1 - t0) {
+		if (__builtin_expect(((fr - t0) & 0xFFFFu) > t1 - t0, 0)) {
 			if (fr < t0) { if (idx < 24) idx++; }
 			else if (idx > 0) idx--;
 			if (idx >= 9) fr = 2048;
@@ -260,17 +265,23 @@ GC_DI uint32_t geo_init_lane(const uint8_t* kinit)          // setCtx, geomcodec
 
 // taboo code, n = 2 (initTaboo / tabooCode, muxcodec.cpp:113-129, 210-240):
 // nb[] is the Fibonacci run 1, 1, 2, 3, ...; sum[] its prefix sums.
-GC_DI void taboo_code(GEnc& e, uint32_t nbv)
+GC_DI void taboo_lanes(uint32_t& nbl, uint32_t& suml)   // lane i < 32: nb[i], sum[i]
 {
 	const uint32_t l = lane_id();
 	uint32_t fa = 1, fb = 1, sm = 0;
-	for (uint32_t i = 0; i < 32; i++) {                 // lane l: nb[l], sum[l]
+	for (uint32_t i = 0; i < 32; i++) {
 		const uint32_t cur = i < 2 ? 1u : fa + fb;
 		if (i >= 2) { fa = fb; fb = cur; }
 		sm += cur;
 		if (i == l) break;
 	}
-	const uint32_t nbl = l < 2 ? 1u : fb, suml = sm;
+	nbl = l < 2 ? 1u : fb;
+	suml = sm;
+}
+GC_DI void taboo_code(GEnc& e, uint32_t nbv)
+{
+	uint32_t nbl, suml;
+	taboo_lanes(nbl, suml);
 	const uint32_t nt = 2;
 	int i = 0, len;
 	uint32_t r = 0, nb = nbv;
@@ -513,7 +524,7 @@ __global__ void __launch_bounds__(64) k_gc_encode(const GEncArgs* __restrict__ a
 	const uint32_t end = e.end();
 	uint32_t rc = 0;
 	if (status) rc = 2;                                  // a fused kernel's ring timeout
-	else if (e.ovf & 2) rc = 3;                          // the LDS ring overran (pathological stream)
+	else if (e.ovf & 6) rc = 3;                          // the LDS ring overran (pathological stream) / guard
 	else if (e.ovf) rc = 1;
 	if (lane_id() == 0) {
 		gst(a.res)[2 * f] = rc ? 0u : end;               // file length = 9 + (end - 7) - 2
@@ -521,12 +532,519 @@ __global__ void __launch_bounds__(64) k_gc_encode(const GEncArgs* __restrict__ a
 	}
 }
 
+
+// ============================================================ the decoder
+// CMuxCodec decoder over a .ric file in HBM.  The reference decodes from a
+// copy of the payload with two zero bytes in front and zero padding behind
+// (src/ric/ric.cpp:203-205): virtual byte x is 0 for x < 2 or x >= 2 + n, else
+// file byte x + 7.  The file is staged into an LDS ring ahead of the walk
+// (1 KiB per 64-lane load, refilled between chunks of blocks); a chunk that
+// reads past what was staged (a pathological stream) is flagged.
+constexpr uint32_t kDRing = 8192;
+constexpr uint32_t kDAhead = 3072;     // bytes staged past the read position at each refill
+__shared__ __attribute__((aligned(16))) uint8_t g_dring[kDRing];
+__shared__ int32_t g_blk[64 * 16];     // the current chunk's decoded blocks, 16 values each
+
+struct GDec {
+	const uint8_t* file;
+	uint32_t n;                        // payload bytes read (ric.cpp: at most W*H)
+	uint32_t flen;                     // file bytes that may be loaded
+	uint32_t range, low, code, nbits, buffer;
+	uint32_t p, limit;
+	uint32_t ovf;                      // 1: read past the end (RIC_E_STREAM), 2: ring overrun
+	uint32_t st_hi;                    // file bytes [.., st_hi) are in the ring
+	uint32_t pend;                     // file offset of the 1 KiB in flight in `stage`
+	u32x4 stage;
+
+	GC_DI uint32_t byte(uint32_t x) const
+	{
+		const uint32_t b = g_dring[(x + 7) & (kDRing - 1)];
+		return (x < 2 || x >= n + 2) ? 0u : b;
+	}
+	GC_DI uint32_t next()
+	{
+		const uint32_t b = byte(p);
+		if (p < limit) p++; else ovf |= 1;
+		return b;
+	}
+	GC_DI u32x4 load_kib(uint32_t off) const
+	{
+		const uint32_t o = off + lane_id() * 16;
+		u32x4 v = {0, 0, 0, 0};
+		if (o + 16 <= flen) v = *gld((const u32x4*)(file + o));
+		return v;
+	}
+	GC_DI void put_kib(uint32_t off, const u32x4& v)
+	{
+		*(u32x4*)(g_dring + ((off + lane_id() * 16) & (kDRing - 1))) = v;
+	}
+	// between chunks: the bytes a chunk may read are staged; flags a chunk
+	// that read past them
+	GC_DI void refill()
+	{
+		if (p + 7 + 8 > st_hi) ovf |= 2;
+		put_kib(pend, stage);
+		st_hi = pend + 1024;
+		while (st_hi < p + 7 + kDAhead) {             // fell behind: synchronous loads
+			const u32x4 v = load_kib(st_hi);
+			put_kib(st_hi, v);
+			st_hi += 1024;
+		}
+		pend = st_hi;
+		stage = load_kib(pend);
+	}
+	// f: the file, len its size, cap the bytes readable at f (a multiple of 16)
+	GC_DI void init(const uint8_t* f, uint32_t len, uint32_t cap, uint32_t npay)
+	{
+		file = f; n = npay;
+		flen = (len + 15) & ~15u;
+		if (flen > cap) flen = cap;
+		st_hi = 0;
+		for (uint32_t off = 0; off < 2 * 1024 + 1024; off += 1024) { put_kib(off, load_kib(off)); st_hi = off + 1024; }
+		pend = st_hi;
+		stage = load_kib(pend);
+		limit = npay + 2 + 65536 - 16;
+		range = 1u << 16;
+		nbits = 0; buffer = 0; ovf = 0;
+		p = 2;
+		code = low = (byte(2) << 8) | byte(3);
+		p = 4;
+	}
+	GC_DI void norm()                                    // normalize_dec, muxcodec.cpp:76-85
+	{
+		uint32_t it = 0;
+		do {
+			if (((code - low + range - 1) ^ (code - low)) >= 0x01000000u) range = (low - code) & 4095u;
+			const uint32_t b = next();
+			low = (low << 8) | b;
+			code = (code << 8) | b;
+			range <<= 8;
+			if (__builtin_expect(++it > 4, 0)) { ovf |= 1; range = 1u << 16; }   // corrupt stream: no spin
+		} while (range <= 4096u);
+	}
+	GC_DI uint32_t bit(uint32_t freq)                    // getBit, muxcodec.h:205-213
+	{
+		if (__builtin_expect(range <= 4096u, 0)) norm();
+		const uint32_t t = (range * freq) >> 12;
+		const uint32_t tst = (uint32_t)(low < t) - 1u;
+		low -= t & tst;
+		range = t + ((range - 2 * t) & tst);
+		return tst & 1u;
+	}
+	GC_DI void fill(uint32_t len)                        // fillBuffer, muxcodec.cpp:572-579
+	{
+		do {
+			nbits += 8;
+			buffer = (buffer << 8) | next();
+		} while (nbits < len);
+	}
+	GC_DI uint32_t bits(uint32_t len)                    // bitsDecode, muxcodec.h:233-239
+	{
+		if (nbits < len) fill(len);
+		nbits -= len;
+		return (buffer >> nbits) & ((1u << len) - 1);
+	}
+	// huffDecode (muxcodec.h:241-276): lane s tests code s of the table row
+	// (hrow: (code << 5) | len per lane, 0 past the row); the first match wins
+	GC_DI uint32_t huff(uint32_t hrow, uint32_t nsym)
+	{
+		const uint32_t c = (((buffer << 16) | (byte(p) << 8) | byte(p + 1)) >> nbits) & 0xFFFFu;
+		const uint32_t l = lane_id();
+		const uint32_t len_l = hrow & 31u;
+		const bool hit = l < nsym && len_l > 0 && (c >> (16 - len_l)) == (hrow >> 5);
+		const uint64_t m = __ballot(hit);
+		uint32_t sym, len;
+		if (m) { sym = (uint32_t)__builtin_ctzll(m); len = lget(len_l, sym); }
+		else { sym = 0; len = lget(len_l, 0); }
+		p -= (uint32_t)((int)(nbits - len) >> 3);
+		if (p > limit) { p = limit; ovf |= 1; }
+		if (nbits < len) buffer = byte(p - 1);
+		nbits = (nbits - len) & 7;
+		return sym;
+	}
+	// enum_code's code part (muxcodec.cpp:391-393); cnk lane i = (n-1)*8 + k-1:
+	// CnkLen | CnkLost << 8, in two lane arrays
+	GC_DI uint32_t enum_code(const uint32_t (&cnk)[2], uint32_t k, uint32_t nmax)
+	{
+		const uint32_t i = (nmax - 1) * 8 + (k - 1);
+		const uint32_t e = i < 64 ? lget(cnk[0], i) : lget(cnk[1], i - 64);
+		const uint32_t lost = e >> 8;
+		uint32_t c = bits((e & 255u) - 1);
+		if (c >= lost) c = ((c << 1) | bits(1)) - lost;
+		return c;
+	}
+	// enumDecode (muxcodec.cpp:381-405); binom lane (r - 1) * 16 + n = C(n, r)
+	GC_DI uint32_t enum_n(const uint32_t (&cnk)[2], const uint32_t (&binom)[2], uint32_t k, uint32_t nmax, bool guard16)
+	{
+		int n = (int)nmax - 1;
+		uint32_t out = 0;
+		if (k > ((nmax + 1) >> 1)) { k = nmax - k; out = (1u << nmax) - 1; }
+		int row = (int)k - 1;
+		uint32_t c = enum_code(cnk, k, nmax);
+		if (guard16) {
+			// the host's table decode (decoder.cpp enum16) reads code 0 for a
+			// code >= C(16, k) (corrupt streams only); C(16, k) = C(15, k) + C(15, k - 1)
+			const uint32_t i1 = (k - 1) * 16 + 15, i0 = (k - 2) * 16 + 15;
+			const uint32_t a1 = i1 < 64 ? lget(binom[0], i1) : lget(binom[1], i1 - 64);
+			const uint32_t a0 = k < 2 ? 1u : (i0 < 64 ? lget(binom[0], i0) : lget(binom[1], i0 - 64));
+			if (c >= a1 + a0) c = 0;
+		}
+		while (row >= 0 && n >= 0) {
+			const uint32_t bi = (uint32_t)row * 16 + (uint32_t)n;
+			const uint32_t v = bi < 64 ? lget(binom[0], bi) : lget(binom[1], bi - 64);
+			if (c >= v) { out ^= 1u << n; c -= v; row--; }
+			n--;
+		}
+		return out;
+	}
+	GC_DI uint32_t max_dec(uint32_t max)                 // maxDecode, muxcodec.cpp:526-534
+	{
+		uint32_t value = 0;
+		const uint32_t len = (uint32_t)bitlen(max), lost = (1u << len) - max - 1;
+		if (len > 1) value = bits(len - 1);
+		if (value >= lost) value = ((value << 1) | bits(1)) - lost;
+		return value;
+	}
+	GC_DI uint32_t taboo()                               // tabooDecode, muxcodec.cpp:242-280
+	{
+		uint32_t nbl, suml;
+		taboo_lanes(nbl, suml);
+		const uint32_t nt = 2;
+		int i, l = nt;
+		uint32_t nb = 0;
+		if (nbits < nt) fill(nt);
+		uint32_t t = ((1u << nt) - 1) << (nbits - nt);
+		while ((~buffer & t) != t) {
+			l++;
+			if (l > (int)nbits) { fill((uint32_t)l); t <<= 8; }
+			t >>= 1;
+			if (l > 25) { ovf |= 1; return 0; }
+		}
+		nbits -= (uint32_t)l;
+		const uint32_t cd = buffer >> (nbits + nt + 1);
+		i = l - (int)nt;
+		if (i > 0) { i--; nb += lget(suml, (uint32_t)i); }
+		while (i > (int)nt) {
+			uint32_t j = 1;
+			while (j < (uint32_t)i && ((cd >> (i - (int)j)) & 1) == 0) j++;
+			nb += lget(suml, (uint32_t)(i - (int)j)) - lget(suml, (uint32_t)(i - (int)nt));
+			i -= (int)j;
+		}
+		if (i == (int)nt) nb -= 1;
+		nb += cd & ((1u << i) - 1);
+		return nb;
+	}
+};
+
+struct GBitD {                                          // CBitCodec::decode, bitcodec.h:62-70
+	uint32_t st;
+	GC_DI void init() { st = 2048u; }
+	GC_DI uint32_t decode(GDec& d, const GTabs& T, uint32_t c)
+	{
+		const uint32_t v = lget(st, c);
+		uint32_t freq = v & 0xFFFFu, sh = (v >> 16) & 0xFFu, mps = v >> 24;
+		uint32_t sym = d.bit(freq) ^ 1;
+		freq = (freq + (sym << (9 - sh)) - (freq >> (3 + sh))) & 0xFFFFu;
+		sym ^= mps;
+		const uint32_t th = lget(T.bit_thr, sh), t0 = th & 0xFFFFu, t1 = th >> 16;
+		if (__builtin_expect(((freq - t1) & 0xFFFFu) > t0 - t1, 0)) {
+			if (freq > t0) {
+				if (sh == 0) { mps ^= 1; freq = 4096u - freq; sh = 1; }
+				else sh--;
+			} else if (sh < 9) sh++;
+		}
+		st = lset(st, c, freq | sh << 16 | mps << 24);
+		return sym;
+	}
+};
+
+struct GGeoD {                                          // one CGeomCodec context in scalars
+	uint32_t freq, idx;
+	GC_DI void load(uint32_t arr, uint32_t c) { const uint32_t v = lget(arr, c); freq = v & 0xFFFFu; idx = v >> 16; }
+	GC_DI uint32_t packed() const { return freq | idx << 16; }
+	// SIGNED: magnitude - 1 then the raw sign (decoder.cpp GeoReg::decode_signed);
+	// else the plain geometric value (GeoM::decode).  lmax: the unary guard.
+	template <bool SIGNED>
+	GC_DI int decode(GDec& d, const GTabs& T, uint32_t lmax)
+	{
+		const uint32_t ks = lget(T.geo_ks, idx), k = ks & 0xFFu, s = ks >> 8;
+		const uint32_t f = freq;
+		uint32_t fr = freq, l = 0;
+		while (d.bit(f)) {
+			fr -= fr >> (3 + s);
+			if (++l > lmax) break;
+		}
+		int out;
+		if (SIGNED) {
+			const uint32_t v = d.bits(k + 1);
+			const int mag = (int)((l << k) | (v >> 1)) + 1;
+			out = (v & 1) ? -mag : mag;
+		} else {
+			if (k > 0) l = (l << k) | d.bits(k);
+			out = (int)l;
+		}
+		fr = (fr + ((4096u - fr) >> (3 + s))) & 0xFFFFu;
+		const uint32_t th = lget(T.geo_thr, s), t0 = th & 0xFFFFu, t1 = th >> 16;
+		if (__builtin_expect(((fr - t0) & 0xFFFFu) > t1 - t0, 0)) {
+			if (fr < t0) { if (idx < 24) idx++; }
+			else if (idx > 0) idx--;
+			if (idx >= 9) fr = 2048;
+		}
+		freq = fr;
+		return out;
+	}
+};
+
+GC_DI int trunc_c(int is_int, int v) { return is_int ? v : (int)(int16_t)v; }
+GC_DI int ldc(const char* band, int is_int, long e)
+{
+	return is_int ? (int)gld((const int32_t*)band)[e] : (int)gld((const int16_t*)band)[e];
+}
+GC_DI void stc(char* band, int is_int, long e, int v)
+{
+	if (is_int) gst((int32_t*)band)[e] = v;
+	else gst((int16_t*)band)[e] = (int16_t)v;
+}
+
+// CBandCodec::pred<decode> (LL DPCM), bandcodec.cpp:62-104: the previous row
+// comes in 64-column runs through the lanes; a run of decoded values is stored
+// by the lanes at its end.
+GC_DI void pred_dec(GDec& d, const GTabs& T, const GBandDesc& B, char* arena)
+{
+	static constexpr uint8_t ginit[16] = {9,10,11,12,13,14,15,16,17,18,19,20,21,22,23,15};
+	char* c = arena + B.off;
+	const long st = B.pitch;
+	const int dx = B.dx, dy = B.dy, is_int = B.is_int;
+	uint32_t geo = geo_init_lane(ginit);
+	const uint32_t l = lane_id();
+	for (int j = 0; j < dy; j++) {
+		int left = 0, upleft = 0;
+		for (int x0 = 0; x0 < dx; x0 += 64) {
+			__threadfence();                          // the previous row's stores
+			const int i = x0 + (int)l;
+			const int up = (j > 0 && i < dx) ? ldc(c, is_int, (long)(j - 1) * st + i) : 0;
+			uint32_t cur = 0;
+			const int nx = dx - x0 < 64 ? dx - x0 : 64;
+			for (int q = 0; q < nx; q++) {
+				const int x = x0 + q;
+				int v;
+				if (j == 0 && x == 0) {
+					v = trunc_c(is_int, u2s((int)d.taboo()));
+				} else {
+					uint32_t ctx = 15;
+					int pred;
+					const int u = (int)lget((uint32_t)up, (uint32_t)q);
+					if (j == 0) pred = left;
+					else if (x == 0) pred = u;
+					else {
+						const int a = left - upleft, bb = u - upleft;
+						int var = bitlen((uint32_t)((a < 0 ? -a : a) + (bb < 0 ? -bb : bb)));
+						ctx = (uint32_t)(var > 15 ? 15 : var);
+						pred = left + u - upleft;
+					}
+					GGeoD g;
+					g.load(geo, ctx);
+					const int r = g.decode<false>(d, T, 1u << 20);
+					geo = lset(geo, ctx, g.packed());
+					v = trunc_c(is_int, pred + u2s(r));
+					upleft = u;
+				}
+				if (j > 0 && x == 0) upleft = (int)lget((uint32_t)up, 0);
+				left = v;
+				cur = lset(cur, (uint32_t)q, (uint32_t)v);
+			}
+			if (i < dx) stc(c, is_int, (long)j * st + i, (int)cur);
+			d.refill();
+		}
+	}
+	__threadfence();
+}
+
+// Per block of a chunk (lane j = scan position s0 + j): what the parent band
+// and the geometry say, computed by the lanes before the walk.
+//  bits 0-4 tree context, 5 full (not an edge block), 6 propagated (parent
+//  anchor holds INSIGNIF), 7 clear the parent anchor, 8-9 w - 1, 10-11 h - 1
+GC_DI uint32_t block_info(const GBandDesc& B, const GBandDesc* P, const char* arena, int nblk, int s, int& bx, int& by)
+{
+	bx = by = 0;
+	if (s >= nblk) return 0;
+	scan_block(s, B.dx, B.dy, bx, by);
+	const int w = B.dx - bx * 4 < 4 ? B.dx - bx * 4 : 4, h = B.dy - by * 4 < 4 ? B.dy - by * 4 : 4;
+	const bool full = w == 4 && by * 4 + 4 <= B.dy;
+	uint32_t info = (uint32_t)(w - 1) << 8 | (uint32_t)(h - 1) << 10 | (full ? 1u << 5 : 0u);
+	uint32_t ctx = 15;
+	if (P) {
+		const char* pb = arena + P->off;
+		const long pst = P->pitch;
+		const int px = bx * 2, py = by * 2;
+		if (full) {
+			const int a = ldc(pb, P->is_int, (long)py * pst + px);
+			if (a == kInsignif) {
+				info |= 1u << 6 | 1u << 7;
+			} else {
+				// maxLen<2, decode> (bandcodec.cpp:324-344)
+				int mx = 0, mn = 0;
+				for (int jj = 0; jj < 2; jj++)
+					for (int ii = 0; ii < 2; ii++) {
+						const int v = ldc(pb, P->is_int, (long)(py + jj) * pst + px + ii);
+						mx = v > mx ? v : mx;
+						mn = v < mn ? v : mn;
+					}
+				mn = trunc_c(P->is_int, -mn);
+				ctx = (uint32_t)bitlen((uint32_t)(mn > mx ? mn : mx));
+			}
+		} else if (px < P->dx && (by * 4 + 4 <= B.dy || py < P->dy)) {
+			if (ldc(pb, P->is_int, (long)py * pst + px) == kInsignif) info |= 1u << 7;
+		}
+	}
+	return info | (ctx & 31u);
+}
+
+// CBandCodec::tree<decode> (bandcodec.cpp:484-589; decoder.cpp tree_dec):
+// chunks of 64 blocks in scan order; each chunk's values are built in LDS and
+// stored by the lanes (every position of every block, so no Clear() pass), the
+// parent anchors the chunk consumed are cleared by the lanes too.
+GC_DI void tree_dec(GDec& d, const GTabs& T, const GBandDesc& B, const GBandDesc* P, char* arena,
+                    const uint32_t (&cnk)[2], const uint32_t (&binom)[2])
+{
+	const bool high = B.high;
+	char* band = arena + B.off;
+	const int is_int = B.is_int;
+	const long st = B.pitch;
+	const int dx = B.dx, dy = B.dy;
+	const int nblk = ((dx + 3) >> 2) * ((dy + 3) >> 2);
+	const uint32_t l = lane_id();
+	const int mval = high ? 0 : kInsignif;             // the INSIGNIF mark, where the band has children
+	const uint32_t gidx = l == 0 ? 5u : (l < 12 ? 9u : (l < 15 ? 10u : 11u));
+	uint32_t geo = (gidx >= 9 ? 2048u : (uint32_t)((kGeoThres[gidx - 1] + kGeoThres[gidx]) >> 1)) | gidx << 16;
+	GBitD tree, bord;
+	tree.init(); bord.init();
+	uint32_t kmean = l < 8 ? (uint32_t)((l < 4 ? l + 2 : (l == 4 ? 8 : (l == 5 ? 11 : (l == 6 ? 13 : 14)))) << 10)
+	                       : 15u << 10;
+	const uint32_t hbase = high ? 0u : 256u, hn = high ? 16u : 17u;
+	const uint32_t lmax = is_int ? (1u << 20) : (1u << 15);
+	for (int s0 = 0; s0 < nblk; s0 += 64) {
+		int bx, by;
+		const uint32_t info = block_info(B, P, arena, nblk, s0 + (int)l, bx, by);
+		// the chunk's blocks: zeros, and the marks of the propagated ones
+		RIC_UNROLL
+		for (int i = 0; i < 16; i++) g_blk[l * 16 + i] = 0;
+		if ((info >> 6) & 1) {
+			g_blk[l * 16 + 0] = mval; g_blk[l * 16 + 2] = mval; g_blk[l * 16 + 8] = mval; g_blk[l * 16 + 10] = mval;
+		}
+		__threadfence_block();
+		const int nj = nblk - s0 < 64 ? nblk - s0 : 64;
+		for (int j = 0; j < nj; j++) {
+			const uint32_t in = lget(info, (uint32_t)j);
+			const uint32_t ob = (uint32_t)j * 16;
+			if ((in >> 5) & 1) {
+				if ((in >> 6) & 1) continue;                   // propagated
+				const uint32_t ctx = in & 31u;
+				if (tree.decode(d, T, ctx)) {
+					g_blk[ob + 0] = mval; g_blk[ob + 2] = mval; g_blk[ob + 8] = mval; g_blk[ob + 10] = mval;
+					continue;
+				}
+				const uint32_t km = lget(kmean, ctx);
+				const uint32_t idx = (km + (1u << 9)) >> 10;
+				const uint32_t hrow = l < hn ? (uint32_t)g_huff[hbase + idx * hn + l] : 0u;
+				const uint32_t k = d.huff(hrow, hn) + (high ? 1u : 0u);
+				if (high || k != 0) {
+					uint32_t sig = k != 16 ? d.enum_n(cnk, binom, k, 16, true) : 0xFFFFu;
+					GGeoD g;
+					g.load(geo, k - 1);
+					while (sig) {
+						const uint32_t b = 31u - (uint32_t)__builtin_clz(sig);      // bit 15 = raster 0
+						sig &= ~(1u << b);
+						g_blk[ob + 15 - b] = trunc_c(is_int, g.decode<true>(d, T, lmax));
+					}
+					geo = lset(geo, k - 1, g.packed());
+				}
+				const uint32_t kk = high ? k - 1 : k;
+				kmean = lset(kmean, ctx, (km + (kk << 7) - (km >> 3)) & 0xFFFFu);
+			} else {
+				if (bord.decode(d, T, 0)) continue;
+				const uint32_t w = ((in >> 8) & 3) + 1, h = ((in >> 10) & 3) + 1, cnt = w * h;
+				uint32_t k = high ? d.max_dec(cnt - 1) + 1 : d.max_dec(cnt);
+				if (k > cnt) k = cnt;
+				if (high || k != 0) {
+					uint32_t sig = k != cnt ? d.enum_n(cnk, binom, k, cnt, false) : (1u << cnt) - 1;
+					const uint32_t gc = kKConv2[kKConv1[cnt]][k - 1];
+					GGeoD g;
+					g.load(geo, gc);
+					for (uint32_t q = 0; q < cnt; q++) {
+						if (sig & (1u << (cnt - 1))) {
+							const uint32_t r = w == 4 ? q >> 2 : q / w, cc = q - r * w;
+							g_blk[ob + r * 4 + cc] = trunc_c(is_int, g.decode<true>(d, T, lmax));
+						}
+						sig <<= 1;
+					}
+					geo = lset(geo, gc, g.packed());
+				}
+			}
+		}
+		__threadfence_block();
+		// the lanes store the chunk
+		if (s0 + (int)l < nblk) {
+			const int w = (int)((info >> 8) & 3) + 1, h = (int)((info >> 10) & 3) + 1;
+			for (int r = 0; r < h; r++)
+				for (int q = 0; q < w; q++) stc(band, is_int, (long)(by * 4 + r) * st + bx * 4 + q, g_blk[l * 16 + r * 4 + q]);
+			if (((info >> 7) & 1) && P) stc(arena + P->off, P->is_int, (long)(by * 2) * P->pitch + bx * 2, 0);
+		}
+		d.refill();
+	}
+	__threadfence();
+}
+
+// One frame's stream per workgroup (one wave): DecompressImage's decoding
+// order (src/ric/ric.cpp:207-225 -> CWavelet2D::DecodeBand,
+// src/lib/wavelet2d.cpp:179-222): the coarsest LL, then coarse to fine V, H, D.
+// The bands land in the frame's arena, ready for the inverse kernels.
+__global__ void __launch_bounds__(64) k_gc_decode(const GDecArgs* __restrict__ ap)
+{
+	const GDecArgs& a = *ap;
+	const int f = blockIdx.x;
+	char* arena = a.arena + (size_t)f * a.astride;
+	const uint8_t* file = a.in + (size_t)f * a.istride;
+	const uint32_t len = gld(a.lens)[(size_t)f * a.lens_stride];
+	for (int i = (int)threadIdx.x; i < 16 * 16 + 17 * 17; i += 64)
+		g_huff[i] = i < 256 ? kHuff_HIGH[i >> 4][i & 15] : kHuff_LOW[(i - 256) / 17][(i - 256) % 17];
+	const uint32_t l = lane_id();
+	uint32_t cnk[2], binom[2];
+	for (int h = 0; h < 2; h++) {
+		const uint32_t i = (uint32_t)h * 64 + l;        // (nmax - 1) * 8 + (k - 1)
+		cnk[h] = (uint32_t)kCnkLen[i >> 3][i & 7] | (uint32_t)kCnkLost[i >> 3][i & 7] << 8;
+		const uint32_t r = (i >> 4) + 1, nn = i & 15;   // C(nn, r)
+		uint32_t cb = 1;
+		if (nn < r) cb = 0;
+		else for (uint32_t t = 1; t <= r; t++) cb = cb * (nn - r + t) / t;
+		binom[h] = cb;
+	}
+	__syncthreads();
+	GTabs T;
+	T.init();
+	GDec d;
+	const uint32_t npay = len > 9 ? (len - 9 < (uint32_t)(a.w * a.h) ? len - 9 : (uint32_t)(a.w * a.h)) : 0u;
+	d.init(file, len, (uint32_t)a.istride, npay);
+	pred_dec(d, T, a.ll, arena);
+	for (int b = 0; b < a.nb; b++) {
+		const GBandDesc& B = a.b[b];
+		tree_dec(d, T, B, B.par >= 0 ? &a.b[B.par] : nullptr, arena, cnk, binom);
+	}
+	if (l == 0) gst(a.res)[f] = d.ovf & 2 ? 3u : (d.ovf ? 1u : 0u);
+}
 }  // namespace
 
 int launch_gc_encode(const GEncArgs* dev_args, int nframes, hipStream_t st)
 {
 	if (nframes <= 0) return 0;
 	hipLaunchKernelGGL(k_gc_encode, dim3(nframes), dim3(64), 0, st, dev_args);
+	return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_gc_decode(const GDecArgs* dev_args, int nframes, hipStream_t st)
+{
+	if (nframes <= 0) return 0;
+	hipLaunchKernelGGL(k_gc_decode, dim3(nframes), dim3(64), 0, st, dev_args);
 	return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

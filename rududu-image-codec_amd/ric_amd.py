@@ -90,6 +90,9 @@ def lib():
         "ric_batch_roundtrip": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _P]),
         "ric_batch_prof_enable": (_I, [_P, _I]),
         "ric_batch_encode_gpu": (_I, [_P, _P, _I, _I, _I, _P, ctypes.c_size_t, ctypes.c_size_t, _P]),
+        "ric_batch_hybrid_config": (_I, [_P, _I, ctypes.c_size_t]),
+        "ric_batch_decode_gpu": (_I, [_P, _P, ctypes.c_size_t, _P, _I, _P]),
+        "ric_batch_roundtrip_hybrid": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
         "ric_batch_diag_gpu": (_I, [_P, _P, _I, _I, _I, _I, _P]),
         "ric_batch_prof_read": (_I, [_P, _P, _P, _P, _I]),
     }
@@ -330,6 +333,16 @@ class Batch:
              "ric_batch_encode_gpu")
         return [lens[i] for i in range(n)]
 
+    def decompress_gpu(self, src, istride, lens, pix_out):
+        """Whole decode on the GPU (ric_batch_decode_gpu): src a device buffer
+        holding the files at multiples of istride, pix_out device tensors."""
+        n = len(lens)
+        ls = (ctypes.c_size_t * n)(*lens)
+        rc = lib().ric_batch_decode_gpu(self.h, _ptr(src), istride, ls, n, _ptrs(pix_out))
+        if rc not in (RIC_OK, RIC_E_STREAM):
+            _chk(rc, "ric_batch_decode_gpu")
+        return rc
+
     def decompress(self, rics, pix_out=None):
         """Host mode: returns a list of (channels, h, w) uint8 arrays.  Device
         mode: pass device tensors / pointers in pix_out.  Returns the status
@@ -359,6 +372,25 @@ class Batch:
         rc = lib().ric_batch_roundtrip(self.h, _ptrs(frames), n, q, trans, _ptrs(outs), caps, lens, _ptrs(pix_out))
         if rc not in (RIC_OK, RIC_E_STREAM):
             _chk(rc, "ric_batch_roundtrip")
+        self._lens = [lens[i] for i in range(n)]
+        return self._lens
+
+    def hybrid_config(self, pool_frames, stream_cap):
+        """Pool of the GPU stream coder (ric_batch_hybrid_config)."""
+        _chk(lib().ric_batch_hybrid_config(self.h, pool_frames, stream_cap), "ric_batch_hybrid_config")
+
+    def roundtrip_hybrid(self, frames, pix_out, n_host, q=9, trans=0, gpu_decode=False):
+        """ric_batch_roundtrip_hybrid: frames[:n_host] round trips on the host,
+        the rest encoded by the GPU stream coder and decoded by the GPU stream
+        decoder (gpu_decode) or on the host."""
+        n = len(frames)
+        outs = self._out_bufs(n)
+        caps = (ctypes.c_size_t * n)(*([self.cap] * n))
+        lens = (ctypes.c_size_t * n)()
+        rc = lib().ric_batch_roundtrip_hybrid(self.h, _ptrs(frames), n, n_host, int(gpu_decode), q, trans, _ptrs(outs),
+                                              caps, lens, _ptrs(pix_out))
+        if rc not in (RIC_OK, RIC_E_STREAM):
+            _chk(rc, "ric_batch_roundtrip_hybrid")
         self._lens = [lens[i] for i in range(n)]
         return self._lens
 

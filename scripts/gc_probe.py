@@ -11,6 +11,8 @@ import os
 import sys
 import time
 
+import numpy as np
+
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "rududu-image-codec_amd"))
 sys.path.insert(0, REPO)
@@ -43,6 +45,17 @@ def main():
     b.prof_enable(True)
     b.compress_gpu(frames, out, ostride, a.q, 0)
     p = b.prof_read()
+    # the GPU stream decoder on the streams just written
+    pix = [torch.zeros((1, a.h, a.w), dtype=torch.uint8, device="cuda") for _ in range(a.n)]
+    b.decompress_gpu(out, ostride, lens, pix)
+    torch.cuda.synchronize()
+    t0 = time.time()
+    b.decompress_gpu(out, ostride, lens, pix)
+    torch.cuda.synchronize()
+    dec_s = time.time() - t0
+    b.prof_enable(True)
+    b.decompress_gpu(out, ostride, lens, pix)
+    pd = b.prof_read()
     host = out.cpu().numpy()
     nc = min(a.check, a.n)
     ref = b.compress([frames[i] for i in range(nc)], a.q, 0, on_device=True)
@@ -55,13 +68,19 @@ def main():
         d = next((k for k in range(min(len(g), len(ref[i]))) if g[k] != ref[i][k]), min(len(g), len(ref[i])))
         print("frame %d: gpu %d bytes, host %d bytes, first difference at %d" % (i, len(g), len(ref[i]), d))
         ok.append(False)
+    dok = []
+    for i in range(nc):
+        want = b.decompress([ref[i]])[0]
+        dok.append(bool(np.array_equal(pix[i].cpu().numpy().reshape(want.shape), want)))
     t0 = time.time()
-    b.compress([frames[i] for i in range(a.n)], a.q, 0, on_device=True)
-    host_t = time.time() - t0
+    nh = min(a.n, 16)                     # host coder reference timing on one group
+    b.compress([frames[i] for i in range(nh)], a.q, 0, on_device=True)
+    host_t = (time.time() - t0) * a.n / nh
     print(json.dumps({"w": a.w, "h": a.h, "n": a.n, "q": a.q, "equal": ok, "lens": lens[:4],
                       "gpu_encode_s": round(best, 4), "first_call_s": round(first, 3),
                       "gpu_frames_per_s": round(a.n / best, 2), "coder_kernel_ms": round(p["host_enc"][0], 2),
-                      "host_encode_s_16thr": round(host_t, 4)}))
+                      "host_encode_s_16thr": round(host_t, 4), "decode_equal": dok, "gpu_decode_s": round(dec_s, 4),
+                      "decoder_kernel_ms": round(pd["host_dec"][0], 2)}))
 
 
 if __name__ == "__main__":

@@ -57,3 +57,78 @@ def test_gpu_coder_large_sha(ric, name):
     frame = ric.synth(w, h, 1, e["frame"])
     got = _gpu_encode(ric, [frame], e["q"], e["trans"])[0]
     assert hashlib.sha256(got).hexdigest() == e["ric_sha256"]
+
+
+@pytest.mark.parametrize("gpu_decode", [False, True])
+@pytest.mark.parametrize("w,h,q,t,n,n_host,pool,slots", [(640, 480, 9, 0, 11, 3, 4, 3), (328, 200, 20, 0, 7, 0, 3, 2),
+                                                         (257, 129, 9, 0, 5, 5, 2, 2), (1024, 768, 9, 0, 9, 2, 8, 4),
+                                                         (128, 96, 0, 1, 6, 1, 2, 4), (96, 80, 9, 2, 7, 0, 2, 2)])
+def test_hybrid_roundtrip(ric, port, w, h, q, t, n, n_host, pool, slots, gpu_decode):
+    """GPU-encoded and host-encoded frames in one pipelined call (several
+    coder launches, both halves of the stream buffer, both slot sets)."""
+    import torch
+    host = [ric.synth(w, h, 1, 80 + i) for i in range(n)]
+    frames = [torch.from_numpy(x).cuda() for x in host]
+    outs = [torch.empty_like(f) for f in frames]
+    b = ric.Batch(w, h, 1, slots=slots, threads=3)
+    b.hybrid_config(pool, (w * h * 2 + 65536 + 15) // 16 * 16)
+    for rep in range(2):
+        lens = b.roundtrip_hybrid(frames, outs, n_host, q, t, gpu_decode=gpu_decode)
+        for i in range(n):
+            r = b.stream(i)
+            assert len(r) == lens[i]
+            assert r == port.encode_ric(host[i], q, t), (rep, i)
+            assert np.array_equal(outs[i].cpu().numpy(), port.decode_ric(r)[0]), (rep, i)
+
+
+def _gpu_decode(ric, rics, w, h):
+    import torch
+    istride = (max(len(r) for r in rics) + 4095) // 4096 * 4096
+    buf = np.zeros(len(rics) * istride, np.uint8)
+    for i, r in enumerate(rics):
+        buf[i * istride:i * istride + len(r)] = np.frombuffer(r, np.uint8)
+    src = torch.from_numpy(buf).cuda()
+    outs = [torch.zeros((1, h, w), dtype=torch.uint8, device="cuda") for _ in rics]
+    b = ric.Batch(w, h, 1, slots=len(rics), threads=1)
+    rc = b.decompress_gpu(src, istride, [len(r) for r in rics], outs)
+    return rc, [o.cpu().numpy() for o in outs]
+
+
+@pytest.mark.parametrize("w,h,q,t", [(1024, 768, 9, 0), (640, 480, 0, 1), (328, 200, 20, 0), (257, 129, 9, 0),
+                                     (128, 96, 9, 2), (33, 47, 9, 0), (17, 16, 0, 1), (100, 60, 31, 0),
+                                     (129, 77, 1, 1), (520, 392, 5, 0), (1001, 603, 0, 1)])
+def test_gpu_decoder_matches_oracle(ric, port, w, h, q, t):
+    frames = [ric.synth(w, h, 1, 90 + i) for i in range(3)]
+    rics = [port.encode_ric(f, q, t) for f in frames]
+    rc, got = _gpu_decode(ric, rics, w, h)
+    for r, g in zip(rics, got):
+        assert np.array_equal(g.reshape(h, w), port.decode_ric(r)[0].reshape(h, w))
+
+
+def test_gpu_decoder_golden_small(ric):
+    n = 0
+    for e in G["small"]:
+        if e["channels"] != 1:
+            continue
+        r = open(os.path.join(HERE, "golden", e["name"] + ".ric"), "rb").read()
+        rc, got = _gpu_decode(ric, [r], e["w"], e["h"])
+        assert hashlib.sha256(got[0].tobytes()).hexdigest() == e["decoded_sha256"], e["name"]
+        n += 1
+    assert n >= 8
+
+
+@pytest.mark.parametrize("name", ["C3_7680x4320_q9", "C2_4096x4096_q9"])
+def test_gpu_roundtrip_large_sha(ric, name):
+    """Encode and decode on the GPU: the reference's SHA-256 of both."""
+    import torch
+    e = [x for x in G["large"] if x["name"] == name][0]
+    w, h = e["w"], e["h"]
+    frame = torch.from_numpy(ric.synth(w, h, 1, e["frame"])).cuda()
+    b = ric.Batch(w, h, 1, slots=1, threads=1)
+    ostride = (w * h * 2 + 65536 + 4095) // 4096 * 4096
+    out = torch.zeros(ostride, dtype=torch.uint8, device="cuda")
+    lens = b.compress_gpu([frame], out, ostride, e["q"], e["trans"])
+    assert hashlib.sha256(out[:lens[0]].cpu().numpy().tobytes()).hexdigest() == e["ric_sha256"]
+    pix = torch.zeros((1, h, w), dtype=torch.uint8, device="cuda")
+    b.decompress_gpu(out, ostride, lens, [pix])
+    assert hashlib.sha256(pix.cpu().numpy().tobytes()).hexdigest() == e["decoded_sha256"]
