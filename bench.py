@@ -102,7 +102,8 @@ def parse():
     ap.add_argument("--coder", default="host", choices=["host", "hybrid", "gpu"],
                     help="serial coder: host threads; hybrid = GPU stream encoder + host decoder; gpu = GPU stream "
                          "encoder and decoder (one wave per stream), host threads doing whole round trips beside it")
-    ap.add_argument("--pool", type=int, default=512, help="hybrid: frames per GPU stream-coder launch")
+    ap.add_argument("--pool", type=int, default=512, help="hybrid / gpu: frames per GPU stream-coder launch")
+    ap.add_argument("--distinct", type=int, default=256, help="distinct frames resident in HBM (inputs, outputs)")
     ap.add_argument("--n-host", type=int, default=-1,
                     help="hybrid: frames per step encoded on the host while the first coder launch runs (default 16 per thread)")
     return ap.parse_args()
@@ -235,8 +236,13 @@ def main():
     slots = max(1, min(a.slots or threads, max(nfr, 1)))
 
     # synthetic frames, uploaded to HBM before timing
+    # at most --distinct distinct frames in HBM (inputs and outputs): a longer
+    # step reuses them cyclically; every frame is still encoded and decoded in full
     frames, rgb = [], None
-    for (_, f, crop) in mine:
+    for k, (_, f, crop) in enumerate(mine):
+        if k >= a.distinct:
+            frames.append(frames[k % a.distinct])
+            continue
         if crop is None:
             host = ric_amd.synth(W, H, CH, f)
         else:
@@ -245,7 +251,8 @@ def main():
             _, _, x0, y0, w, h = crop
             host = np.ascontiguousarray(rgb[:, y0:y0 + h, x0:x0 + w])
         frames.append(torch.from_numpy(host).to(dev))
-    outs = [torch.empty((CH, H, W), dtype=torch.uint8, device=dev) for _ in range(nfr)]
+    outs = [torch.empty((CH, H, W), dtype=torch.uint8, device=dev) for _ in range(min(nfr, a.distinct))]
+    outs = [outs[k % len(outs)] for k in range(nfr)]
     torch.cuda.synchronize()
 
     b = ric_amd.Batch(W, H, CH, slots=slots, threads=threads, device=local) if nfr else None

@@ -178,6 +178,9 @@ int ric_batch_encode_gpu(ric_batch* b, const uint8_t* const* pix, int n, int q, 
  * (DEVICE memory, istride a multiple of 16), their sizes len[i]; pixels to
  * device pix_out[i].  RIC_E_STREAM as ric_batch_decode. */
 int ric_batch_decode_gpu(ric_batch* b, const uint8_t* in, size_t istride, const size_t* len, int n, uint8_t* const* pix_out);
+/* Diagnostics: the stream decoder dumps 8 words of coder state after the LL
+ * and after each band (64 slots per frame) into dev_buf (null: off). */
+int ric_diag_gdec_dbg(void* dev_buf);
 /* Hybrid round trip (gray): the serial encoder runs on the GPU (one wave per
  * stream, launches of `pool_frames` frames, each stream up to stream_cap
  * bytes: a multiple of 16; a longer stream fails the call with

@@ -779,6 +779,14 @@ int ric_batch_encode_gpu(ric_batch* b, const uint8_t* const* pix, int n, int q, 
 	return RIC_OK;
 }
 
+// diagnostics: device buffer for the stream decoder's per-band state dumps
+static void* g_gdec_dbg = nullptr;
+extern "C" int ric_diag_gdec_dbg(void* dev_buf)
+{
+	g_gdec_dbg = dev_buf;
+	return RIC_OK;
+}
+
 // The whole DecompressImage of n gray frames on the GPU: the serial decoder
 // of every stream on one wave each (gcoder.hip k_gc_decode) into the bands of
 // slot set 0, then the inverse levels and the pixel conversion.  in: the .ric
@@ -820,6 +828,7 @@ int ric_batch_decode_gpu(ric_batch* b, const uint8_t* in, size_t istride, const 
 	a.in = in; a.istride = istride;
 	a.lens = b->d_res; a.lens_stride = 2;
 	a.res = b->d_res + 2 * b->slots;          // after the lengths (2 words per frame)
+	a.dbg = (uint32_t*)g_gdec_dbg;
 	a.w = b->w; a.h = b->h;
 	gc_bands(b->P, a.ll, a.b, a.nb);
 	BCHK(hipMemcpyAsync(b->d_gdec, &a, sizeof(GDecArgs), hipMemcpyHostToDevice, b->st));
@@ -836,7 +845,10 @@ int ric_batch_decode_gpu(ric_batch* b, const uint8_t* in, size_t istride, const 
 	int result = RIC_OK;
 	for (int i = 0; i < n; i++) {
 		const uint32_t r = b->h_res[2 * b->slots + i];
-		if (r == 3) { set_last_error("GPU stream decoder: staging overrun (pathological stream)"); return RIC_E_CAPACITY; }
+		if ((r & 15) == 3) {
+			set_last_error("GPU stream decoder: staging overrun (pathological stream) at byte " + std::to_string(r >> 4));
+			return RIC_E_CAPACITY;
+		}
 		if (r == 1) result = RIC_E_STREAM;
 	}
 	return result;
@@ -924,6 +936,7 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 			d.in = a.out; d.istride = c.ocap;
 			d.lens = a.res; d.lens_stride = 2;
 			d.res = c.d_res + res_dec(h);
+			d.dbg = nullptr;
 			d.w = b->w; d.h = b->h;
 			gc_bands(P, d.ll, d.b, d.nb);
 		}
@@ -990,7 +1003,11 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 			if (re[2 * k] > cap[f0 + k]) return RIC_E_CAPACITY;
 			len[f0 + k] = re[2 * k];
 			if (gpu_decode) {
-				if (rd[k] == 3) { set_last_error("GPU stream decoder: staging overrun"); return RIC_E_CAPACITY; }
+				if ((rd[k] & 15) == 3) {
+					set_last_error("GPU stream decoder: staging overrun at byte " + std::to_string(rd[k] >> 4) + " of frame " +
+					               std::to_string(f0 + k) + " (stream " + std::to_string(re[2 * k]) + " bytes)");
+					return RIC_E_CAPACITY;
+				}
 				stream_err |= rd[k] == 1;
 			}
 		}

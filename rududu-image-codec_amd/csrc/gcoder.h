@@ -47,6 +47,7 @@ struct GDecArgs {
 	const uint32_t* lens;
 	int lens_stride;
 	uint32_t* res;
+	uint32_t* dbg;                   // diagnostics: 8 words of coder state after the LL and each band, per frame (or null)
 	int w, h;
 	int nb;
 	GBandDesc ll;

@@ -237,9 +237,11 @@ struct GGeoCtx {
 		uint32_t fr = freq;
 		uint32_t run = sym >> k;
 		if (__builtin_expect(run > (1u << 20), 0)) { run = 0; e.ovf |= 4; }   // not a coefficient of this path
-		for (uint32_t l = run; l > 0; l--) {
-			e.bin(f, 1);
-			fr -= fr >> (3 + s);
+		if (__builtin_expect(run != 0, 0)) {             // most runs are empty: fall through
+			for (uint32_t l = run; l > 0; l--) {
+				e.bin(f, 1);
+				fr -= fr >> (3 + s);
+			}
 		}
 		e.bin(f, 0);
 		if (SIGNED) e.bits(((sym & ((1u << k) - 1)) << 1) | sign, k + 1);
@@ -561,8 +563,27 @@ struct GDec {
 		const uint32_t b = g_dring[(x + 7) & (kDRing - 1)];
 		return (x < 2 || x >= n + 2) ? 0u : b;
 	}
+	// a read near the end of what is staged (a long unary run: a corrupt or
+	// desynchronised stream, e.g. the reference's maxDecode(0)) stages more now
+	GC_DI void stage_now()
+	{
+		put_kib(pend, stage);
+		st_hi = pend + 1024;
+		while (st_hi < p + 7 + kDAhead) {
+			const u32x4 v = load_kib(st_hi);
+			put_kib(st_hi, v);
+			st_hi += 1024;
+		}
+		pend = st_hi;
+		stage = load_kib(pend);
+	}
+	GC_DI void ensure(uint32_t x)                      // byte x (and x + 1) are staged
+	{
+		if (__builtin_expect(x + 7 + 2 >= st_hi, 0)) stage_now();
+	}
 	GC_DI uint32_t next()
 	{
+		ensure(p);
 		const uint32_t b = byte(p);
 		if (p < limit) p++; else ovf |= 1;
 		return b;
@@ -580,18 +601,12 @@ struct GDec {
 	}
 	// between chunks: the bytes a chunk may read are staged; flags a chunk
 	// that read past them
+	// (pend == st_hi: the next KiB is in flight.)  Staging only advances with
+	// the read position, so the ring always keeps the bytes just behind it.
 	GC_DI void refill()
 	{
-		if (p + 7 + 8 > st_hi) ovf |= 2;
-		put_kib(pend, stage);
-		st_hi = pend + 1024;
-		while (st_hi < p + 7 + kDAhead) {             // fell behind: synchronous loads
-			const u32x4 v = load_kib(st_hi);
-			put_kib(st_hi, v);
-			st_hi += 1024;
-		}
-		pend = st_hi;
-		stage = load_kib(pend);
+		if (st_hi >= p + 7 + kDAhead) return;
+		stage_now();
 	}
 	// f: the file, len its size, cap the bytes readable at f (a multiple of 16)
 	GC_DI void init(const uint8_t* f, uint32_t len, uint32_t cap, uint32_t npay)
@@ -648,6 +663,7 @@ struct GDec {
 	// (hrow: (code << 5) | len per lane, 0 past the row); the first match wins
 	GC_DI uint32_t huff(uint32_t hrow, uint32_t nsym)
 	{
+		ensure(p);
 		const uint32_t c = (((buffer << 16) | (byte(p) << 8) | byte(p + 1)) >> nbits) & 0xFFFFu;
 		const uint32_t l = lane_id();
 		const uint32_t len_l = hrow & 31u;
@@ -770,9 +786,11 @@ struct GGeoD {                                          // one CGeomCodec contex
 		const uint32_t ks = lget(T.geo_ks, idx), k = ks & 0xFFu, s = ks >> 8;
 		const uint32_t f = freq;
 		uint32_t fr = freq, l = 0;
-		while (d.bit(f)) {
-			fr -= fr >> (3 + s);
-			if (++l > lmax) break;
+		if (__builtin_expect(d.bit(f), 0)) {             // most runs are empty: fall through
+			do {
+				fr -= fr >> (3 + s);
+				if (++l > lmax) break;
+			} while (d.bit(f));
 		}
 		int out;
 		if (SIGNED) {
@@ -1025,12 +1043,39 @@ __global__ void __launch_bounds__(64) k_gc_decode(const GDecArgs* __restrict__ a
 	GDec d;
 	const uint32_t npay = len > 9 ? (len - 9 < (uint32_t)(a.w * a.h) ? len - 9 : (uint32_t)(a.w * a.h)) : 0u;
 	d.init(file, len, (uint32_t)a.istride, npay);
+	auto dump = [&](int k) {
+		if (a.dbg && l == 0) {
+			GAS uint32_t* o = gst(a.dbg) + (size_t)f * 2048 + (size_t)k * 8;
+			o[0] = d.range; o[1] = d.low; o[2] = d.code; o[3] = d.nbits; o[4] = d.buffer; o[5] = d.p; o[6] = d.ovf; o[7] = 0xC0DE;
+		}
+	};
 	pred_dec(d, T, a.ll, arena);
+	dump(0);
+	if (a.dbg) {                                     // the decoded LL, row-major (first 1024 values)
+		const GBandDesc& B = a.ll;
+		for (int i = (int)l; i < B.dx * B.dy && i < 1024; i += 64)
+			gst(a.dbg)[(size_t)f * 2048 + 1024 + i] = (uint32_t)ldc(arena + B.off, B.is_int, (long)(i / B.dx) * B.pitch + i % B.dx);
+	}
 	for (int b = 0; b < a.nb; b++) {
 		const GBandDesc& B = a.b[b];
 		tree_dec(d, T, B, B.par >= 0 ? &a.b[B.par] : nullptr, arena, cnk, binom);
+		dump(b + 1);
 	}
-	if (l == 0) gst(a.res)[f] = d.ovf & 2 ? 3u : (d.ovf ? 1u : 0u);
+	// status in bits 0-3; on a staging overrun, the read position (diagnostic)
+	if (a.dbg && f == 0) {                           // every band, the host harness's order (finest first, D H V, LL)
+		__threadfence();
+		size_t o = 2048;
+		for (int k = 0; k <= a.nb; k++) {
+			// a.b is coarse -> fine V, H, D: band i of the harness order
+			const int lev = k / 3, ori = k % 3;          // harness: level lev, orientation D=0, H=1, V=2
+			const GBandDesc* B = k == a.nb ? &a.ll : &a.b[a.nb - 3 - 3 * lev + (2 - ori)];
+			const int cnt = B->dx * B->dy;
+			for (int i = (int)l; i < cnt; i += 64)
+				gst(a.dbg)[o + i] = (uint32_t)ldc(arena + B->off, B->is_int, (long)(i / B->dx) * B->pitch + i % B->dx);
+			o += cnt;
+		}
+	}
+	if (l == 0) gst(a.res)[f] = d.ovf & 2 ? 3u | (d.p < (1u << 27) ? d.p << 4 : 0xFFFFFFF0u) : (d.ovf ? 1u : 0u);
 }
 }  // namespace
 

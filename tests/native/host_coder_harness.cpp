@@ -179,4 +179,34 @@ long hc_decode(const uint8_t* in, long len, int nplanes, int w, int h, int level
 	if (secs) *secs = t;
 	return off;
 }
+
+// coder state after the LL and after each band when decoding a .ric file
+// (init_decoder_payload, as the batch path): 8 words per band, as the GPU
+// stream decoder's diagnostic dump
+long hc_decode_states(const uint8_t* ric, long len, int w, int h, uint32_t* st_out)
+{
+	HostPyr hp(w, h, 5, 1);
+	Mux m;
+	const long pay = std::min(len - 9, (long)w * h);
+	m.init_decoder_payload(ric + 9, pay);
+	long k = 0;
+	auto dump = [&]() {
+		const Mux::DecState d = m.dec_state();
+		uint32_t* o = st_out + 8 * k++;
+		o[0] = d.range; o[1] = d.low; o[2] = d.code; o[3] = d.nbits; o[4] = d.buffer;
+		o[5] = (uint32_t)(d.p - m.buffer()); o[6] = d.ovf; o[7] = 0xC0DE;
+	};
+	pred_decode(m, hp.view(hp.P.coarsest_ll()));
+	dump();
+	for (int l = hp.P.nlev - 1; l >= 0; l--) {
+		const int order[3] = {BV, BH, BD};
+		for (int b = 0; b < 3; b++) {
+			BandView par;
+			if (l + 1 < hp.P.nlev) par = hp.view(hp.P.L[l + 1].b[order[b]]);
+			tree_decode_fast(m, hp.view(hp.P.L[l].b[order[b]]), par, l == 0, l > 0);
+			dump();
+		}
+	}
+	return k;
+}
 }
