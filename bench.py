@@ -390,9 +390,36 @@ def main():
         except Exception:
             traffic = None
 
+    # ---- the stream coder's launches (per launch: kernel time = a wave's time
+    # to code one whole stream, with every stream of the launch in flight)
+    coder = None
+    if hybrid:
+        coder = {"streams_per_launch": b.cp_pool, "frames_host_round_trip": n_host}
+        for k, name in (("gpu_enc", "encode"), ("gpu_dec", "decode")):
+            if k in per_launch:
+                ms, fr, ln = prof[k]
+                coder[name] = {"launches": ln, "streams": fr, "ms_per_launch": round(ms / ln, 1),
+                               "streams_per_s": round(fr / (ms * 1e-3), 1)}
+
+    # ---- the level-0 fused kernel alone (rank 0, after timing): in the timed
+    # region it shares every CU with the stream coder's waves
+    iso = None
+    if rank == 0 and b is not None and hybrid:
+        b.prof_enable(True)
+        b.diag_gpu(frames[:slots], a.q, a.trans, 3, outs[:slots])
+        pi = b.prof_read()
+        if pi["fwd_l0"][1]:
+            t_iso = pi["fwd_l0"][0] / pi["fwd_l0"][1]
+            ach = l0_bytes / (t_iso * 1e-3) / 1e9
+            fi = [pi["fwd_l%d" % l][0] / pi["fwd_l%d" % l][1] for l in range(nlev) if pi["fwd_l%d" % l][1]]
+            iso = {"avg_launch_ms": round(pi["fwd_l0"][0] / pi["fwd_l0"][2], 4), "achieved": round(ach, 1),
+                   "frac": round(ach / HBM_PEAK_GBS, 4), "gpu_wavelet_encode": _frac(sum(fi), enc_bytes),
+                   "note": "GPU stages alone (ric_batch_diag_gpu), %d frames per launch, 3 iterations, after the "
+                           "timed region" % slots}
+
     # ---- encode-only and decode-only rates of the same path (rank 0, after timing)
     split = None
-    if rank == 0 and b is not None and not a.no_split:
+    if rank == 0 and b is not None and not a.no_split and not hybrid:
         streams = [b.stream(i) for i in range(nfr)]
         torch.cuda.synchronize()
         te = time.perf_counter()
@@ -468,6 +495,10 @@ def main():
         out["host_serial"] = hs
     if split:
         out["gpu_path_split"] = split
+    if coder:
+        out["stream_coder"] = coder
+    if iso:
+        out["roofline_isolated"] = iso
     if gather:
         out["gather"] = {"backend": backend, "bytes_to_rank0_per_step": gathered[0]}
         if a.workload == "C4":

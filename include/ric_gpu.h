@@ -195,10 +195,10 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 /* Stage timers of the batch (no reference counterpart): 0 pixel conversion
  * in, 1..8 forward level 0..7 (fused DWT + quantiser + records), 9 D2H of
  * bands + records, 10 host encode, 11 host decode, 12 H2D of the bands,
- * 13..20 inverse level 0..7 (fused TSUQi), 21 pixel conversion out.  With the
- * GPU stream coder, stage 10 is its launches (frames = streams coded).  ms are
+ * 13..20 inverse level 0..7 (fused TSUQi), 21 pixel conversion out, 22 / 23 the
+ * GPU stream encoder / decoder launches (ms = kernel time, frames = streams).  ms are
  * sums; frames = frames covered; launches = GPU launches (host: frames). */
-#define RIC_BATCH_STAGES 22
+#define RIC_BATCH_STAGES 24
 /* Diagnostics: the batch's GPU stages alone, iters times over n <= slots
  * device frames (forward levels + D2H, H2D + inverse levels of the bands just
  * quantised, pixel output to pix_out if given); no host coding. */

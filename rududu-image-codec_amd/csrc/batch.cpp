@@ -128,8 +128,11 @@ private:
 // Stage timers: GPU stages by event pairs on the batch's stream (harvested
 // after the call's final sync), host stages by a steady clock per frame.
 // Stage order: pix_in, fwd level 0..7, d2h, host_enc, host_dec, h2d,
-// inv level 0..7, pix_out (RIC_BATCH_STAGES).
-enum { B_PIXIN = 0, B_FWD = 1, B_D2H = 9, B_HENC = 10, B_HDEC = 11, B_H2D = 12, B_INV = 13, B_PIXOUT = 21, B_COUNT = 22 };
+// inv level 0..7, pix_out, gpu stream encode, gpu stream decode
+// (RIC_BATCH_STAGES; the stream coder stages are per launch: ms = kernel
+// time, frames = streams).
+enum { B_PIXIN = 0, B_FWD = 1, B_D2H = 9, B_HENC = 10, B_HDEC = 11, B_H2D = 12, B_INV = 13, B_PIXOUT = 21, B_GENC = 22, B_GDEC = 23,
+       B_COUNT = 24 };
 
 struct BProf {
 	bool on = false;
@@ -761,7 +764,7 @@ int ric_batch_encode_gpu(ric_batch* b, const uint8_t* const* pix, int n, int q, 
 	a.w = b->w; a.h = b->h; a.q = q; a.trans = trans;
 	gc_bands(b->P, a.ll, a.b, a.nb);
 	BCHK(hipMemcpyAsync(b->d_genc, &a, sizeof(GEncArgs), hipMemcpyHostToDevice, b->st));
-	auto sp = b->prof.begin(B_HENC, n, b->st);
+	auto sp = b->prof.begin(B_GENC, n, b->st);
 	if (launch_gc_encode(b->d_genc, n, b->st)) return bfail(hipGetLastError(), "k_gc_encode") ? RIC_E_HIP : RIC_E_HIP;
 	b->prof.end(sp);
 	BCHK(hipMemcpyAsync(b->h_res, b->d_res, sizeof(uint32_t) * 2 * n, hipMemcpyDeviceToHost, b->st));
@@ -832,7 +835,7 @@ int ric_batch_decode_gpu(ric_batch* b, const uint8_t* in, size_t istride, const 
 	a.w = b->w; a.h = b->h;
 	gc_bands(b->P, a.ll, a.b, a.nb);
 	BCHK(hipMemcpyAsync(b->d_gdec, &a, sizeof(GDecArgs), hipMemcpyHostToDevice, b->st));
-	auto sp = b->prof.begin(B_HDEC, n, b->st);
+	auto sp = b->prof.begin(B_GDEC, n, b->st);
 	if (launch_gc_decode(b->d_gdec, n, b->st)) return bfail(hipGetLastError(), "k_gc_decode") ? RIC_E_HIP : RIC_E_HIP;
 	b->prof.end(sp);
 	int rc = gpu_decode_plane(b, 0, n, 0, qs.data(), t0, false);
@@ -969,11 +972,11 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 		}
 		BCHK(hipEventRecord(c.ev_fwd[h], b->st));
 		BCHK(hipStreamWaitEvent(c.st[h], c.ev_fwd[h], 0));
-		auto sp = b->prof.begin(B_HENC, m, c.st[h]);
+		auto sp = b->prof.begin(B_GENC, m, c.st[h]);
 		if (launch_gc_encode(c.d_args + h, m, c.st[h])) return bfail(hipGetLastError(), "k_gc_encode") ? RIC_E_HIP : RIC_E_HIP;
 		b->prof.end(sp);
 		if (gpu_decode) {
-			auto sd = b->prof.begin(B_HDEC, m, c.st[h]);
+			auto sd = b->prof.begin(B_GDEC, m, c.st[h]);
 			if (launch_gc_decode(c.d_dargs + h, m, c.st[h]))
 				return bfail(hipGetLastError(), "k_gc_decode") ? RIC_E_HIP : RIC_E_HIP;
 			b->prof.end(sd);

@@ -66,7 +66,7 @@ struct GTabs {
 // lanes, 16-byte stores) once no reservation slot points into them: single
 // byte stores would each hold the vector-memory counter the walk's prefetch
 // loads are waited on with.
-constexpr uint32_t kRing = 16384;       // bytes of LDS per wave
+constexpr uint32_t kRing = 8192;        // bytes of LDS per wave (small: the wave shares its CU with the level kernels)
 constexpr uint32_t kFlush = 1024;
 __shared__ __attribute__((aligned(16))) uint8_t g_ring[kRing];
 __shared__ uint16_t g_huff[16 * 16 + 17 * 17];  // kHuff_HIGH rows, then kHuff_LOW rows
@@ -542,8 +542,8 @@ __global__ void __launch_bounds__(64) k_gc_encode(const GEncArgs* __restrict__ a
 // file byte x + 7.  The file is staged into an LDS ring ahead of the walk
 // (1 KiB per 64-lane load, refilled between chunks of blocks); a chunk that
 // reads past what was staged (a pathological stream) is flagged.
-constexpr uint32_t kDRing = 8192;
-constexpr uint32_t kDAhead = 3072;     // bytes staged past the read position at each refill
+constexpr uint32_t kDRing = 4096;
+constexpr uint32_t kDAhead = 2048;     // bytes staged past the read position at each refill
 __shared__ __attribute__((aligned(16))) uint8_t g_dring[kDRing];
 __shared__ int32_t g_blk[64 * 16];     // the current chunk's decoded blocks, 16 values each
 

@@ -78,9 +78,9 @@ def main():
     host_t = (time.time() - t0) * a.n / nh
     print(json.dumps({"w": a.w, "h": a.h, "n": a.n, "q": a.q, "equal": ok, "lens": lens[:4],
                       "gpu_encode_s": round(best, 4), "first_call_s": round(first, 3),
-                      "gpu_frames_per_s": round(a.n / best, 2), "coder_kernel_ms": round(p["host_enc"][0], 2),
+                      "gpu_frames_per_s": round(a.n / best, 2), "coder_kernel_ms": round(p["gpu_enc"][0], 2),
                       "host_encode_s_16thr": round(host_t, 4), "decode_equal": dok, "gpu_decode_s": round(dec_s, 4),
-                      "decoder_kernel_ms": round(pd["host_dec"][0], 2)}))
+                      "decoder_kernel_ms": round(pd["gpu_dec"][0], 2)}))
 
 
 if __name__ == "__main__":
