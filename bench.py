@@ -99,14 +99,25 @@ def parse():
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-gather", action="store_true", help="N>1: skip the per-step stream gather to rank 0")
     ap.add_argument("--no-split", action="store_true", help="skip the encode-only / decode-only timing")
-    ap.add_argument("--coder", default="host", choices=["host", "hybrid", "gpu"],
+    ap.add_argument("--coder", default=None, choices=["host", "hybrid", "gpu", "mix"],
                     help="serial coder: host threads; hybrid = GPU stream encoder + host decoder; gpu = GPU stream "
-                         "encoder and decoder (one wave per stream), host threads doing whole round trips beside it")
+                         "encoder and decoder (one wave per stream), host threads doing whole round trips beside it; "
+                         "mix = GPU stream encoder, each launch decoded by the host threads or the GPU stream decoder "
+                         "(whichever has room)")
     ap.add_argument("--pool", type=int, default=512, help="hybrid / gpu: frames per GPU stream-coder launch")
-    ap.add_argument("--distinct", type=int, default=256, help="distinct frames resident in HBM (inputs, outputs)")
+    ap.add_argument("--distinct", type=int, default=128,
+                    help="distinct frames resident in HBM (inputs, outputs) and host stream buffers; a longer step cycles them")
     ap.add_argument("--n-host", type=int, default=-1,
-                    help="hybrid: frames per step encoded on the host while the first coder launch runs (default 16 per thread)")
-    return ap.parse_args()
+                    help="hybrid / gpu / mix: frames per step round-tripped by the host threads beside the GPU stream "
+                         "coder (default: gpu 50 per thread, else 16 per thread)")
+    a = ap.parse_args()
+    if a.coder is None:   # C3 (one large gray frame per stream): the GPU stream coder; C4 (RGB) / C5: host
+        a.coder = "gpu" if a.workload == "C3" else "host"
+    return a
+
+
+def default_n_host(a, threads):
+    return a.n_host if a.n_host >= 0 else (50 if a.coder == "gpu" else 16) * threads
 
 
 def host_info():
@@ -190,7 +201,11 @@ def workload_frames(a, rank, world, threads):
     """(W, H, channels, [(global index, synth frame, crop)], scaling)"""
     if a.workload == "C3":
         W, H = 7680, 4320
-        n = a.frames or a.batch or 8 * threads
+        if a.coder in ("hybrid", "gpu", "mix"):
+            # two stream-coder launches in flight plus the host threads' round trips
+            n = a.frames or a.batch or 2 * a.pool + default_n_host(a, threads)
+        else:
+            n = a.frames or a.batch or 8 * threads
         return W, H, 1, [(rank * n + i, rank * n + i, None) for i in range(n)], "weak"
     if a.workload == "C5":
         W, H = 4096, 4096
@@ -260,19 +275,24 @@ def main():
     gathered = [0]
     container = [None]
 
-    hybrid = a.coder in ("hybrid", "gpu") and CH == 1 and b is not None
-    gpu_dec = a.coder == "gpu"
+    hybrid = a.coder in ("hybrid", "gpu", "mix") and CH == 1 and b is not None
+    gpu_dec = {"hybrid": 0, "gpu": 1, "mix": 2}.get(a.coder, 0)
     n_host = 0
     if hybrid:
-        n_host = a.n_host if a.n_host >= 0 else min(nfr, 16 * threads)
+        n_host = min(nfr, default_n_host(a, threads))
         # stream capacity: 3 bits per pixel (a q9 C3 stream is 1.7), 16-byte multiple
         b.cp_pool = min(a.pool, max(nfr - n_host, 1))
-        b.hybrid_config(b.cp_pool, (W * H * 3 // 8 + 65536) // 16 * 16)
+        scap = (W * H * 3 // 8 + 65536) // 16 * 16
+        b.hybrid_config(b.cp_pool, scap)
+        # host buffers of the .ric files, cycled like the frames (frame k and
+        # frame k + distinct are the same picture, so the same bytes)
+        sb = [np.empty(scap, np.uint8) for _ in range(min(nfr, a.distinct))]
+        sbufs = [sb[k % len(sb)] for k in range(nfr)]
 
     def step():
         if b is not None:
             if hybrid:
-                b.roundtrip_hybrid(frames, outs, n_host, q=a.q, trans=a.trans, gpu_decode=gpu_dec)
+                b.roundtrip_hybrid(frames, outs, n_host, q=a.q, trans=a.trans, gpu_decode=gpu_dec, streams=sbufs)
             else:
                 b.roundtrip(frames, outs, q=a.q, trans=a.trans)
         if gather and a.workload == "C4":
@@ -296,8 +316,11 @@ def main():
                 raise RuntimeError("rank %d: scattered tile streams differ from the encoded ones" % rank)
         elif gather:
             # the path's one exchange: every rank's .ric streams to rank 0
-            # (SURVEY.md §8(e)); rank 0 keeps them on the device
-            streams = [b.stream(i) for i in range(nfr)] if b is not None else []
+            # (SURVEY.md §8(e)); rank 0 keeps them on the device.  With the
+            # stream coder a step holds ~1800 frames per rank (13 GB of
+            # streams): the distinct ones (--distinct, the rest repeat them) go
+            ng = min(nfr, a.distinct) if hybrid else nfr
+            streams = [b.stream(i) for i in range(ng)] if b is not None else []
             got = shard.gather_streams(streams, dist, device=cdev, to_host=False)
             if rank == 0:
                 gathered[0] = int(sum(int(s[1:1 + int(s[0])].sum()) for s in got[1]))
@@ -470,9 +493,13 @@ def main():
         "config": {"workload": wl, "frames_per_gpu_per_step": nfr, "frames_per_launch": slots,
                    "host_coder_threads_per_gpu": threads, "parallelism": "frames sharded over %d GPU(s)" % world,
                    "coder": ("GPU stream coder (one wave per stream, %d streams per launch): encode%s of %d of %d "
-                             "frames; host threads: %s" % (b.cp_pool, " and decode" if gpu_dec else "", nfr - n_host, nfr,
-                                                           "round trips of the rest" if gpu_dec else
-                                                           "round trips of the rest and every decode")) if hybrid
+                             "frames; host threads: %s" % (b.cp_pool, {0: "", 1: " and decode", 2: " (and decode of the "
+                                                                        "launches the host threads have no room for)"}[gpu_dec],
+                                                           nfr - n_host, nfr,
+                                                           {0: "round trips of the rest and every decode",
+                                                            1: "round trips of the rest",
+                                                            2: "round trips of the rest and the decode of the other "
+                                                               "launches"}[gpu_dec])) if hybrid
                    else "host threads (encode and decode)"},
         "verified": verified,
         "verified_against": vnote,

@@ -557,35 +557,31 @@ struct GDec {
 	uint32_t st_hi;                    // file bytes [.., st_hi) are in the ring
 	uint32_t pend;                     // file offset of the 1 KiB in flight in `stage`
 	u32x4 stage;
+	uint64_t win;                      // file bytes [wf, wf + 8)
+	uint32_t wf, nxt;
 
-	GC_DI uint32_t byte(uint32_t x) const
+	// The bytes around the read position in registers: file bytes [wf, wf + 8)
+	// (wf a multiple of 4, p + 7 in [wf, wf + 4)), the next dword read from the
+	// LDS ring one step ahead.  The read position only moves forward (huffDecode
+	// moves it by at most 2, never back: it is entered with nbits < 8).
+	GC_DI uint32_t rd_dword(uint32_t f) const { return *(const uint32_t*)(g_dring + (f & (kDRing - 1))); }
+	GC_DI void wadvance()
 	{
-		const uint32_t b = g_dring[(x + 7) & (kDRing - 1)];
+		if (__builtin_expect(wf + 24 >= st_hi, 0)) stage_now();
+		win = (win >> 32) | ((uint64_t)nxt << 32);
+		wf += 4;
+		nxt = rd_dword(wf + 8);
+	}
+	GC_DI uint32_t byte(uint32_t x) const            // x + 7 in [wf, wf + 8)
+	{
+		const uint32_t b = (uint32_t)(win >> (((x + 7) - wf) * 8)) & 255u;
 		return (x < 2 || x >= n + 2) ? 0u : b;
-	}
-	// a read near the end of what is staged (a long unary run: a corrupt or
-	// desynchronised stream, e.g. the reference's maxDecode(0)) stages more now
-	GC_DI void stage_now()
-	{
-		put_kib(pend, stage);
-		st_hi = pend + 1024;
-		while (st_hi < p + 7 + kDAhead) {
-			const u32x4 v = load_kib(st_hi);
-			put_kib(st_hi, v);
-			st_hi += 1024;
-		}
-		pend = st_hi;
-		stage = load_kib(pend);
-	}
-	GC_DI void ensure(uint32_t x)                      // byte x (and x + 1) are staged
-	{
-		if (__builtin_expect(x + 7 + 2 >= st_hi, 0)) stage_now();
 	}
 	GC_DI uint32_t next()
 	{
-		ensure(p);
 		const uint32_t b = byte(p);
 		if (p < limit) p++; else ovf |= 1;
+		if (p + 7 >= wf + 4) wadvance();
 		return b;
 	}
 	GC_DI u32x4 load_kib(uint32_t off) const
@@ -598,6 +594,20 @@ struct GDec {
 	GC_DI void put_kib(uint32_t off, const u32x4& v)
 	{
 		*(u32x4*)(g_dring + ((off + lane_id() * 16) & (kDRing - 1))) = v;
+	}
+	// stage file bytes up to kDAhead past the read position (pend == st_hi: the
+	// next KiB is in flight in `stage`)
+	GC_DI void stage_now()
+	{
+		put_kib(pend, stage);
+		st_hi = pend + 1024;
+		while (st_hi < p + 7 + kDAhead) {
+			const u32x4 v = load_kib(st_hi);
+			put_kib(st_hi, v);
+			st_hi += 1024;
+		}
+		pend = st_hi;
+		stage = load_kib(pend);
 	}
 	// between chunks: the bytes a chunk may read are staged; flags a chunk
 	// that read past them
@@ -621,7 +631,9 @@ struct GDec {
 		limit = npay + 2 + 65536 - 16;
 		range = 1u << 16;
 		nbits = 0; buffer = 0; ovf = 0;
-		p = 2;
+		wf = 8;
+		win = (uint64_t)rd_dword(8) | (uint64_t)rd_dword(12) << 32;
+		nxt = rd_dword(16);
 		code = low = (byte(2) << 8) | byte(3);
 		p = 4;
 	}
@@ -641,10 +653,13 @@ struct GDec {
 	{
 		if (__builtin_expect(range <= 4096u, 0)) norm();
 		const uint32_t t = (range * freq) >> 12;
-		const uint32_t tst = (uint32_t)(low < t) - 1u;
+		// low < t as arithmetic (a bool-to-int on the scalar unit would take a
+		// round trip through a VGPR)
+		const uint32_t lt = (uint32_t)(((uint64_t)low - (uint64_t)t) >> 63);
+		const uint32_t tst = lt - 1u;
 		low -= t & tst;
 		range = t + ((range - 2 * t) & tst);
-		return tst & 1u;
+		return 1u - lt;
 	}
 	GC_DI void fill(uint32_t len)                        // fillBuffer, muxcodec.cpp:572-579
 	{
@@ -663,7 +678,6 @@ struct GDec {
 	// (hrow: (code << 5) | len per lane, 0 past the row); the first match wins
 	GC_DI uint32_t huff(uint32_t hrow, uint32_t nsym)
 	{
-		ensure(p);
 		const uint32_t c = (((buffer << 16) | (byte(p) << 8) | byte(p + 1)) >> nbits) & 0xFFFFu;
 		const uint32_t l = lane_id();
 		const uint32_t len_l = hrow & 31u;
@@ -676,6 +690,7 @@ struct GDec {
 		if (p > limit) { p = limit; ovf |= 1; }
 		if (nbits < len) buffer = byte(p - 1);
 		nbits = (nbits - len) & 7;
+		while (p + 7 >= wf + 4) wadvance();
 		return sym;
 	}
 	// enum_code's code part (muxcodec.cpp:391-393); cnk lane i = (n-1)*8 + k-1:

@@ -369,6 +369,7 @@ class Batch:
         outs = self._out_bufs(n)
         caps = (ctypes.c_size_t * n)(*([self.cap] * n))
         lens = (ctypes.c_size_t * n)()
+        self._streams = None
         rc = lib().ric_batch_roundtrip(self.h, _ptrs(frames), n, q, trans, _ptrs(outs), caps, lens, _ptrs(pix_out))
         if rc not in (RIC_OK, RIC_E_STREAM):
             _chk(rc, "ric_batch_roundtrip")
@@ -379,14 +380,16 @@ class Batch:
         """Pool of the GPU stream coder (ric_batch_hybrid_config)."""
         _chk(lib().ric_batch_hybrid_config(self.h, pool_frames, stream_cap), "ric_batch_hybrid_config")
 
-    def roundtrip_hybrid(self, frames, pix_out, n_host, q=9, trans=0, gpu_decode=False):
+    def roundtrip_hybrid(self, frames, pix_out, n_host, q=9, trans=0, gpu_decode=False, streams=None):
         """ric_batch_roundtrip_hybrid: frames[:n_host] round trips on the host,
         the rest encoded by the GPU stream coder and decoded by the GPU stream
-        decoder (gpu_decode) or on the host."""
+        decoder (gpu_decode 1), on the host (0), or per launch by whichever
+        has room (2)."""
         n = len(frames)
-        outs = self._out_bufs(n)
-        caps = (ctypes.c_size_t * n)(*([self.cap] * n))
+        outs = streams if streams is not None else self._out_bufs(n)   # host buffers of the .ric files
+        caps = (ctypes.c_size_t * n)(*[o.size for o in outs])
         lens = (ctypes.c_size_t * n)()
+        self._streams = outs
         rc = lib().ric_batch_roundtrip_hybrid(self.h, _ptrs(frames), n, n_host, int(gpu_decode), q, trans, _ptrs(outs),
                                               caps, lens, _ptrs(pix_out))
         if rc not in (RIC_OK, RIC_E_STREAM):
@@ -395,7 +398,8 @@ class Batch:
         return self._lens
 
     def stream(self, i):
-        return self._outs[i][:self._lens[i]].tobytes()
+        bufs = getattr(self, "_streams", None) or self._outs
+        return bufs[i][:self._lens[i]].tobytes()
 
     def diag_gpu(self, frames, q=9, trans=0, iters=1, pix_out=None):
         """GPU stages only (kernel timing), see ric_batch_diag_gpu."""
