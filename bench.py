@@ -201,7 +201,7 @@ def workload_frames(a, rank, world, threads):
     """(W, H, channels, [(global index, synth frame, crop)], scaling)"""
     if a.workload == "C3":
         W, H = 7680, 4320
-        if a.coder in ("hybrid", "gpu", "mix"):
+        if getattr(a, "coder", "host") in ("hybrid", "gpu", "mix"):
             # two stream-coder launches in flight plus the host threads' round trips
             n = a.frames or a.batch or 2 * a.pool + default_n_host(a, threads)
         else:

@@ -92,6 +92,7 @@ def lib():
         "ric_batch_encode_gpu": (_I, [_P, _P, _I, _I, _I, _P, ctypes.c_size_t, ctypes.c_size_t, _P]),
         "ric_batch_hybrid_config": (_I, [_P, _I, ctypes.c_size_t]),
         "ric_batch_decode_gpu": (_I, [_P, _P, ctypes.c_size_t, _P, _I, _P]),
+        "ric_diag_gdec_dbg": (_I, [_P]),
         "ric_batch_roundtrip_hybrid": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
         "ric_batch_diag_gpu": (_I, [_P, _P, _I, _I, _I, _I, _P]),
         "ric_batch_prof_read": (_I, [_P, _P, _P, _P, _I]),
