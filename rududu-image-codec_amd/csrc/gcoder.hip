@@ -564,17 +564,19 @@ struct GDec {
 	// (wf a multiple of 4, p + 7 in [wf, wf + 4)), the next dword read from the
 	// LDS ring one step ahead.  The read position only moves forward (huffDecode
 	// moves it by at most 2, never back: it is entered with nbits < 8).
-	GC_DI uint32_t rd_dword(uint32_t f) const { return *(const uint32_t*)(g_dring + (f & (kDRing - 1))); }
+	// big-endian: file byte wf + o is bits 56 - 8 o of win (the byte swap is one
+	// VALU op on the dword read from LDS)
+	GC_DI uint32_t rd_dword(uint32_t f) const { return __builtin_bswap32(*(const uint32_t*)(g_dring + (f & (kDRing - 1)))); }
 	GC_DI void wadvance()
 	{
 		if (__builtin_expect(wf + 24 >= st_hi, 0)) stage_now();
-		win = (win >> 32) | ((uint64_t)nxt << 32);
+		win = (win << 32) | nxt;
 		wf += 4;
 		nxt = rd_dword(wf + 8);
 	}
 	GC_DI uint32_t byte(uint32_t x) const            // x + 7 in [wf, wf + 8)
 	{
-		const uint32_t b = (uint32_t)(win >> (((x + 7) - wf) * 8)) & 255u;
+		const uint32_t b = (uint32_t)(win >> (56 - ((x + 7) - wf) * 8)) & 255u;
 		return (x < 2 || x >= n + 2) ? 0u : b;
 	}
 	GC_DI uint32_t next()
@@ -632,7 +634,7 @@ struct GDec {
 		range = 1u << 16;
 		nbits = 0; buffer = 0; ovf = 0;
 		wf = 8;
-		win = (uint64_t)rd_dword(8) | (uint64_t)rd_dword(12) << 32;
+		win = (uint64_t)rd_dword(8) << 32 | rd_dword(12);
 		nxt = rd_dword(16);
 		code = low = (byte(2) << 8) | byte(3);
 		p = 4;
@@ -663,6 +665,19 @@ struct GDec {
 	}
 	GC_DI void fill(uint32_t len)                        // fillBuffer, muxcodec.cpp:572-579
 	{
+		// the nb bytes fillBuffer reads one at a time, taken from the window at
+		// once when they all lie inside the payload (the window holds >= 5 bytes
+		// at the read position; nb <= 4)
+		const uint32_t nb = (len - nbits + 7) >> 3;
+		if (__builtin_expect(p + nb <= n + 2 && nb <= 4, 1)) {
+			const uint32_t o = p + 7 - wf;
+			const uint32_t v = (uint32_t)((win << (8 * o)) >> (64 - 8 * nb));
+			buffer = (uint32_t)(((uint64_t)buffer << (8 * nb)) | v);
+			nbits += 8 * nb;
+			p += nb;
+			while (p + 7 >= wf + 4) wadvance();
+			return;
+		}
 		do {
 			nbits += 8;
 			buffer = (buffer << 8) | next();
@@ -720,11 +735,21 @@ struct GDec {
 			const uint32_t a0 = k < 2 ? 1u : (i0 < 64 ? lget(binom[0], i0) : lget(binom[1], i0 - 64));
 			if (c >= a1 + a0) c = 0;
 		}
+		// the reference scans n downwards and takes each n with C(n, row + 1) <= c:
+		// per row that is the largest such n, found by the lanes at once (lane
+		// 16 (row & 3) + j of binom[row >> 2] holds C(j, row + 1); C(0, r) = 0, so
+		// some lane always qualifies while n >= 0)
+		const uint32_t l = lane_id();
 		while (row >= 0 && n >= 0) {
-			const uint32_t bi = (uint32_t)row * 16 + (uint32_t)n;
-			const uint32_t v = bi < 64 ? lget(binom[0], bi) : lget(binom[1], bi - 64);
-			if (c >= v) { out ^= 1u << n; c -= v; row--; }
-			n--;
+			const uint32_t vrow = row < 4 ? binom[0] : binom[1];
+			const bool ok = (l >> 4) == ((uint32_t)row & 3u) && (l & 15u) <= (uint32_t)n && vrow <= c;
+			const uint64_t m = __ballot(ok);
+			const uint32_t idx = 63u - (uint32_t)__builtin_clzll(m);
+			const uint32_t nn = idx & 15u;
+			out ^= 1u << nn;
+			c -= lget(vrow, idx);
+			row--;
+			n = (int)nn - 1;
 		}
 		return out;
 	}
