@@ -219,6 +219,7 @@ def workload_frames(a, rank, world, threads):
 
 
 def main():
+    t_start = time.perf_counter()
     a = parse()
     import torch
     import torch.distributed as dist
@@ -255,6 +256,8 @@ def main():
     # step reuses them cyclically; every frame is still encoded and decoded in full
     frames, rgb = [], None
     for k, (_, f, crop) in enumerate(mine):
+        if k and k % 32 == 0 and k < a.distinct and rank == 0:
+            print("[bench] frames %d/%d" % (k, min(nfr, a.distinct)), file=sys.stderr, flush=True)
         if k >= a.distinct:
             frames.append(frames[k % a.distinct])
             continue
@@ -325,16 +328,24 @@ def main():
             if rank == 0:
                 gathered[0] = int(sum(int(s[1:1 + int(s[0])].sum()) for s in got[1]))
 
-    for _ in range(a.warmup):
+    def progress(what):
+        # a line on stderr per step: a step with the stream coder takes seconds
+        # and the harness takes a silent run for a hung one
+        if rank == 0:
+            print("[bench] %s %.1f s" % (what, time.perf_counter() - t_start), file=sys.stderr, flush=True)
+
+    for i in range(a.warmup):
         step()
+        progress("warmup step %d/%d" % (i + 1, a.warmup))
     if b is not None:
         b.prof_enable(True)
 
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
+    for i in range(a.steps):
         step()
+        progress("step %d/%d" % (i + 1, a.steps))
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     barrier()
