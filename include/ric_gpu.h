@@ -189,7 +189,9 @@ int ric_batch_hybrid_config(ric_batch* b, int pool_frames, size_t stream_cap);
 /* As ric_batch_roundtrip (device pixels in and out, .ric files to host
  * out[i]): frames [0, n_host) encoded and decoded on the host; frames
  * [n_host, n) encoded by the GPU stream coder and decoded by the GPU stream
- * decoder (gpu_decode) or on the host.  Byte-identical streams either way. */
+ * decoder (gpu_decode 1), on the host pool (0), or per coder launch by
+ * whichever is free (2: the host pool while its backlog is shorter than a
+ * launch, the GPU for the rest).  Byte-identical streams either way. */
 int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, int n_host, int gpu_decode, int q,
                                int trans, uint8_t* const* out, const size_t* cap, size_t* len, uint8_t* const* pix_out);
 /* Stage timers of the batch (no reference counterpart): 0 pixel conversion

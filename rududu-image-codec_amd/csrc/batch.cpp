@@ -864,7 +864,8 @@ int ric_batch_decode_gpu(ric_batch* b, const uint8_t* in, size_t istride, const 
 // group's bands + records are copied into one half of the pool; then, on that
 // half's coder stream, k_gc_encode codes them all and (gpu_decode) k_gc_decode
 // decodes the streams back into the pool, whose bands go through the inverse
-// levels in groups.  Without gpu_decode the host pool decodes the streams.
+// levels in groups.  Without gpu_decode the host pool decodes the streams;
+// gpu_decode 2 decides per launch (host pool first, the GPU for the excess).
 // A coder launch takes seconds (a wave codes one whole stream), so two
 // launches are in flight (the two halves) and the host threads meanwhile do
 // whole round trips of the first n_host frames.
@@ -952,6 +953,15 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 	const int nbatch = ng > 0 ? (ng + c.n - 1) / c.n : 0;
 	int kicked = 0, finished = 0;
 	std::vector<Latch> copied(nbatch > 0 ? nbatch : 1);   // host decode: a batch's streams are out of d_out
+	// per batch: decoded on the GPU (1) or by the host pool (0).  gpu_decode 2
+	// decides at each launch: the host pool takes a batch when its own backlog
+	// would run dry before the batch's encode ends, the GPU decodes the rest.
+	std::vector<char> bgpu(nbatch > 0 ? nbatch : 1, 0);
+	std::vector<double> t_kick(nbatch > 0 ? nbatch : 1, 0.0);
+	const double px = (double)b->w * b->h;
+	double enc_ms_est = px * 1.3e-4;                      // a stream coder launch (C3: ~4.3 s), refined as launches end
+	std::atomic<long> dec_us{0}, dec_n{0};                // host decode time per frame, measured
+	auto host_dec_ms = [&]() { const long k = dec_n.load(); return k > 0 ? dec_us.load() * 1e-3 / k : px * 4e-6; };
 	int rc = RIC_OK;
 	bool stream_err = false;
 	std::vector<int> qs(S, q);
@@ -975,7 +985,21 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 		auto sp = b->prof.begin(B_GENC, m, c.st[h]);
 		if (launch_gc_encode(c.d_args + h, m, c.st[h])) return bfail(hipGetLastError(), "k_gc_encode") ? RIC_E_HIP : RIC_E_HIP;
 		b->prof.end(sp);
-		if (gpu_decode) {
+		if (gpu_decode == 1) bgpu[j] = 1;
+		else if (gpu_decode == 2) {
+			// the host pool's backlog (frames to decode, round trips queued), in seconds of its threads
+			long dec_frames = 0;
+			for (const auto& g : ready_dec) dec_frames += g.m;
+			for (int k = finished; k < j; k++)
+				if (!bgpu[k]) dec_frames += batch_m(k);
+			long rt_frames = 0;
+			for (const auto& g : ready_host) rt_frames += g.m;
+			const double thr = (double)b->pool->size();
+			const double backlog_ms = (dec_frames * host_dec_ms() + rt_frames * 2.0 * host_dec_ms()) / thr;
+			bgpu[j] = backlog_ms > enc_ms_est ? 1 : 0;
+		}
+		t_kick[j] = now_ms();
+		if (bgpu[j]) {
 			auto sd = b->prof.begin(B_GDEC, m, c.st[h]);
 			if (launch_gc_decode(c.d_dargs + h, m, c.st[h]))
 				return bfail(hipGetLastError(), "k_gc_decode") ? RIC_E_HIP : RIC_E_HIP;
@@ -984,7 +1008,7 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 		BCHK(hipMemcpyAsync(c.h_res + res_enc(h), c.d_res + res_enc(h), sizeof(uint32_t) * 3 * c.n, hipMemcpyDeviceToHost,
 		                    c.st[h]));
 		BCHK(hipEventRecord(c.ev_done[h], c.st[h]));
-		copied[j].reset(gpu_decode ? 0 : m);
+		copied[j].reset(bgpu[j] ? 0 : m);
 		return RIC_OK;
 	};
 	// batch j's coder launches are done: (host decode) its decode groups become
@@ -1005,7 +1029,7 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 			}
 			if (re[2 * k] > cap[f0 + k]) return RIC_E_CAPACITY;
 			len[f0 + k] = re[2 * k];
-			if (gpu_decode) {
+			if (bgpu[j]) {
 				if ((rd[k] & 15) == 3) {
 					set_last_error("GPU stream decoder: staging overrun at byte " + std::to_string(rd[k] >> 4) + " of frame " +
 					               std::to_string(f0 + k) + " (stream " + std::to_string(re[2 * k]) + " bytes)");
@@ -1014,7 +1038,8 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 				stream_err |= rd[k] == 1;
 			}
 		}
-		if (!gpu_decode) {
+		if (!bgpu[j]) {
+			enc_ms_est = 0.5 * enc_ms_est + 0.5 * (now_ms() - t_kick[j]);
 			for (int g0 = 0; g0 < m; g0 += S) ready_dec.push_back({f0 + g0, std::min(S, m - g0), true, h, g0});
 			return RIC_OK;
 		}
@@ -1068,6 +1093,8 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 			} else {
 				const uint8_t* src = c.d_out + ((size_t)g.half * c.n + g.k0 + i) * c.ocap;
 				Latch* cl = &copied[(f - n_host) / c.n];
+				std::atomic<long>* pdec_us = &dec_us;
+				std::atomic<long>* pdec_n = &dec_n;
 				b->pool->submit([=] {
 					int r1 = set_dev(b->device);
 					if (!r1) r1 = bfail(hipMemcpy(out[f], src, len[f], hipMemcpyDeviceToHost), "hipMemcpy stream") ? RIC_E_HIP
@@ -1075,7 +1102,10 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 					cl->done();
 					// the set's mirrors: the previous group's H2D from them has passed
 					if (!r1) r1 = bfail(hipEventSynchronize(pf->ev), "hipEventSynchronize") ? RIC_E_HIP : RIC_OK;
+					const double t0 = now_ms();
 					if (!r1) r1 = host_decode_plane(b, slot, 0, out[f], len[f]);
+					pdec_us->fetch_add((long)((now_ms() - t0) * 1e3));
+					pdec_n->fetch_add(1);
 					pf->err.put(r1);
 					pf->done.done();
 				});

@@ -59,7 +59,7 @@ def test_gpu_coder_large_sha(ric, name):
     assert hashlib.sha256(got).hexdigest() == e["ric_sha256"]
 
 
-@pytest.mark.parametrize("gpu_decode", [False, True])
+@pytest.mark.parametrize("gpu_decode", [0, 1, 2])
 @pytest.mark.parametrize("w,h,q,t,n,n_host,pool,slots", [(640, 480, 9, 0, 11, 3, 4, 3), (328, 200, 20, 0, 7, 0, 3, 2),
                                                          (257, 129, 9, 0, 5, 5, 2, 2), (1024, 768, 9, 0, 9, 2, 8, 4),
                                                          (128, 96, 0, 1, 6, 1, 2, 4), (96, 80, 9, 2, 7, 0, 2, 2)])
