@@ -223,16 +223,19 @@ struct GBit {
 };
 
 // One CGeomCodec context in scalars (geomcodec.h:41-57, 88-97): freq, idx.
+// The idx-dependent parameters (k, shift, the shift's thresholds) are read
+// from the lane tables when the context is loaded and again only when idx
+// moves, not per coded value.
 struct GGeoCtx {
-	uint32_t freq, idx;
-	GC_DI void load(uint32_t arr, uint32_t c) { const uint32_t v = lget(arr, c); freq = v & 0xFFFFu; idx = v >> 16; }
+	uint32_t freq, idx, k, s, thr;
+	GC_DI void params(const GTabs& T) { const uint32_t ks = lget(T.geo_ks, idx); k = ks & 0xFFu; s = ks >> 8; thr = lget(T.geo_thr, s); }
+	GC_DI void load(uint32_t arr, uint32_t c, const GTabs& T) { const uint32_t v = lget(arr, c); freq = v & 0xFFFFu; idx = v >> 16; params(T); }
 	GC_DI uint32_t packed() const { return freq | idx << 16; }
 	// magnitude - 1 (unary + k raw bits) then, if SIGNED, one raw sign bit:
 	// the remainder and the sign as one chunk
 	template <bool SIGNED>
 	GC_DI void code(GEnc& e, const GTabs& T, uint32_t sym, uint32_t sign)
 	{
-		const uint32_t ks = lget(T.geo_ks, idx), k = ks & 0xFFu, s = ks >> 8;
 		const uint32_t f = freq;
 		uint32_t fr = freq;
 		uint32_t run = sym >> k;
@@ -247,11 +250,12 @@ struct GGeoCtx {
 		if (SIGNED) e.bits(((sym & ((1u << k) - 1)) << 1) | sign, k + 1);
 		else if (k > 0) e.bits(sym & ((1u << k) - 1), k);
 		fr = (fr + ((4096u - fr) >> (3 + s))) & 0xFFFFu;
-		const uint32_t th = lget(T.geo_thr, s), t0 = th & 0xFFFFu, t1 = th >> 16;
+		const uint32_t t0 = thr & 0xFFFFu, t1 = thr >> 16;
 		if (__builtin_expect(((fr - t0) & 0xFFFFu) > t1 - t0, 0)) {
 			if (fr < t0) { if (idx < 24) idx++; }
 			else if (idx > 0) idx--;
 			if (idx >= 9) fr = 2048;
+			params(T);
 		}
 		freq = fr;
 	}
@@ -343,7 +347,7 @@ GC_DI void pred_enc(GEnc& e, const GTabs& T, const GBandDesc& B, const char* are
 				if (j == 0 && x0 + q == 0) { taboo_code(e, s); continue; }
 				const uint32_t cx = lget(ctx, (uint32_t)q);
 				GGeoCtx g;
-				g.load(geo, cx);
+				g.load(geo, cx, T);
 				g.code<false>(e, T, s, 0);
 				geo = lset(geo, cx, g.packed());
 			}
@@ -408,7 +412,7 @@ GC_DI RecChunk fetch_recs(const uint64_t* rec, const uint8_t* pin, int dx, int d
 GC_DI void code_coefs(GEnc& e, const GTabs& T, uint32_t& geo, uint32_t gc, uint32_t mask, uint32_t cv, uint32_t cb)
 {
 	GGeoCtx g;
-	g.load(geo, gc);
+	g.load(geo, gc, T);
 	while (mask) {
 		const uint32_t i = (uint32_t)__builtin_ctz(mask);
 		mask &= mask - 1;
@@ -814,16 +818,16 @@ struct GBitD {                                          // CBitCodec::decode, bi
 	}
 };
 
-struct GGeoD {                                          // one CGeomCodec context in scalars
-	uint32_t freq, idx;
-	GC_DI void load(uint32_t arr, uint32_t c) { const uint32_t v = lget(arr, c); freq = v & 0xFFFFu; idx = v >> 16; }
+struct GGeoD {                                          // one CGeomCodec context in scalars (as GGeoCtx)
+	uint32_t freq, idx, k, s, thr;
+	GC_DI void params(const GTabs& T) { const uint32_t ks = lget(T.geo_ks, idx); k = ks & 0xFFu; s = ks >> 8; thr = lget(T.geo_thr, s); }
+	GC_DI void load(uint32_t arr, uint32_t c, const GTabs& T) { const uint32_t v = lget(arr, c); freq = v & 0xFFFFu; idx = v >> 16; params(T); }
 	GC_DI uint32_t packed() const { return freq | idx << 16; }
 	// SIGNED: magnitude - 1 then the raw sign (decoder.cpp GeoReg::decode_signed);
 	// else the plain geometric value (GeoM::decode).  lmax: the unary guard.
 	template <bool SIGNED>
 	GC_DI int decode(GDec& d, const GTabs& T, uint32_t lmax)
 	{
-		const uint32_t ks = lget(T.geo_ks, idx), k = ks & 0xFFu, s = ks >> 8;
 		const uint32_t f = freq;
 		uint32_t fr = freq, l = 0;
 		if (__builtin_expect(d.bit(f), 0)) {             // most runs are empty: fall through
@@ -842,11 +846,12 @@ struct GGeoD {                                          // one CGeomCodec contex
 			out = (int)l;
 		}
 		fr = (fr + ((4096u - fr) >> (3 + s))) & 0xFFFFu;
-		const uint32_t th = lget(T.geo_thr, s), t0 = th & 0xFFFFu, t1 = th >> 16;
+		const uint32_t t0 = thr & 0xFFFFu, t1 = thr >> 16;
 		if (__builtin_expect(((fr - t0) & 0xFFFFu) > t1 - t0, 0)) {
 			if (fr < t0) { if (idx < 24) idx++; }
 			else if (idx > 0) idx--;
 			if (idx >= 9) fr = 2048;
+			params(T);
 		}
 		freq = fr;
 		return out;
@@ -901,7 +906,7 @@ GC_DI void pred_dec(GDec& d, const GTabs& T, const GBandDesc& B, char* arena)
 						pred = left + u - upleft;
 					}
 					GGeoD g;
-					g.load(geo, ctx);
+					g.load(geo, ctx, T);
 					const int r = g.decode<false>(d, T, 1u << 20);
 					geo = lset(geo, ctx, g.packed());
 					v = trunc_c(is_int, pred + u2s(r));
@@ -1009,11 +1014,11 @@ GC_DI void tree_dec(GDec& d, const GTabs& T, const GBandDesc& B, const GBandDesc
 				if (high || k != 0) {
 					uint32_t sig = k != 16 ? d.enum_n(cnk, binom, k, 16, true) : 0xFFFFu;
 					GGeoD g;
-					g.load(geo, k - 1);
+					g.load(geo, k - 1, T);
 					while (sig) {
 						const uint32_t b = 31u - (uint32_t)__builtin_clz(sig);      // bit 15 = raster 0
 						sig &= ~(1u << b);
-						g_blk[ob + 15 - b] = trunc_c(is_int, g.decode<true>(d, T, lmax));
+						g_blk[ob + 15 - b] = g.decode<true>(d, T, lmax);   // stc truncates a short band's value
 					}
 					geo = lset(geo, k - 1, g.packed());
 				}
@@ -1028,11 +1033,11 @@ GC_DI void tree_dec(GDec& d, const GTabs& T, const GBandDesc& B, const GBandDesc
 					uint32_t sig = k != cnt ? d.enum_n(cnk, binom, k, cnt, false) : (1u << cnt) - 1;
 					const uint32_t gc = kKConv2[kKConv1[cnt]][k - 1];
 					GGeoD g;
-					g.load(geo, gc);
+					g.load(geo, gc, T);
 					for (uint32_t q = 0; q < cnt; q++) {
 						if (sig & (1u << (cnt - 1))) {
 							const uint32_t r = w == 4 ? q >> 2 : q / w, cc = q - r * w;
-							g_blk[ob + r * 4 + cc] = trunc_c(is_int, g.decode<true>(d, T, lmax));
+							g_blk[ob + r * 4 + cc] = g.decode<true>(d, T, lmax);
 						}
 						sig <<= 1;
 					}
