@@ -120,6 +120,12 @@ def default_n_host(a, threads):
     return a.n_host if a.n_host >= 0 else (50 if a.coder == "gpu" else 16) * threads
 
 
+def host_frames_room(a, threads):
+    """Host round trips a step has frames for: with --coder gpu and no --n-host
+    the split is balanced after the warmup (up to 64 per thread)."""
+    return 64 * threads if (a.n_host < 0 and a.coder == "gpu") else default_n_host(a, threads)
+
+
 def host_info():
     model = None
     try:
@@ -203,7 +209,7 @@ def workload_frames(a, rank, world, threads):
         W, H = 7680, 4320
         if getattr(a, "coder", "host") in ("hybrid", "gpu", "mix"):
             # two stream-coder launches in flight plus the host threads' round trips
-            n = a.frames or a.batch or 2 * a.pool + default_n_host(a, threads)
+            n = a.frames or a.batch or 2 * a.pool + host_frames_room(a, threads)
         else:
             n = a.frames or a.batch or 8 * threads
         return W, H, 1, [(rank * n + i, rank * n + i, None) for i in range(n)], "weak"
@@ -281,10 +287,14 @@ def main():
     hybrid = a.coder in ("hybrid", "gpu", "mix") and CH == 1 and b is not None
     gpu_dec = {"hybrid": 0, "gpu": 1, "mix": 2}.get(a.coder, 0)
     n_host = 0
+    nstep = nfr                                # frames coded per step
     if hybrid:
         n_host = min(nfr, default_n_host(a, threads))
+        # the stream coder's frames: two launches in flight (or the rest of --frames)
+        n_gpu = nfr - n_host if (a.frames or a.batch) else min(2 * a.pool, nfr - n_host)
+        nstep = n_host + n_gpu
         # stream capacity: 3 bits per pixel (a q9 C3 stream is 1.7), 16-byte multiple
-        b.cp_pool = min(a.pool, max(nfr - n_host, 1))
+        b.cp_pool = min(a.pool, max(n_gpu, 1))
         scap = (W * H * 3 // 8 + 65536) // 16 * 16
         b.hybrid_config(b.cp_pool, scap)
         # host buffers of the .ric files, cycled like the frames (frame k and
@@ -295,7 +305,9 @@ def main():
     def step():
         if b is not None:
             if hybrid:
-                b.roundtrip_hybrid(frames, outs, n_host, q=a.q, trans=a.trans, gpu_decode=gpu_dec, streams=sbufs)
+                m = n_host + n_gpu
+                b.roundtrip_hybrid(frames[:m], outs[:m], n_host, q=a.q, trans=a.trans, gpu_decode=gpu_dec,
+                                   streams=sbufs[:m])
             else:
                 b.roundtrip(frames, outs, q=a.q, trans=a.trans)
         if gather and a.workload == "C4":
@@ -322,7 +334,7 @@ def main():
             # (SURVEY.md §8(e)); rank 0 keeps them on the device.  With the
             # stream coder a step holds ~1800 frames per rank (13 GB of
             # streams): the distinct ones (--distinct, the rest repeat them) go
-            ng = min(nfr, a.distinct) if hybrid else nfr
+            ng = min(nstep, a.distinct) if hybrid else nfr
             streams = [b.stream(i) for i in range(ng)] if b is not None else []
             got = shard.gather_streams(streams, dist, device=cdev, to_host=False)
             if rank == 0:
@@ -334,9 +346,44 @@ def main():
         if rank == 0:
             print("[bench] %s %.1f s" % (what, time.perf_counter() - t_start), file=sys.stderr, flush=True)
 
+    # Host/GPU split (--coder gpu, no --n-host): the last warmup step measures a
+    # host round trip per thread and a stream-coder launch pair (encode +
+    # decode: the GPU side of a step), and the host threads then take as many
+    # round trips as fit in the GPU side's time, so neither side idles.
+    balance = None
+    auto = hybrid and gpu_dec == 1 and a.n_host < 0 and not (a.frames or a.batch) and a.warmup >= 2
+    t_warm = None
     for i in range(a.warmup):
+        if auto and i == a.warmup - 1:
+            b.prof_enable(True)
+            t_warm = time.perf_counter()
         step()
+        if t_warm is not None and i == a.warmup - 1:
+            t_warm = (time.perf_counter() - t_warm) * 1e3
         progress("warmup step %d/%d" % (i + 1, a.warmup))
+    if auto:
+        pw = b.prof_read()
+        if pw["host_enc"][1] and pw["gpu_enc"][2] and pw["gpu_dec"][2]:
+            t_host = (pw["host_enc"][0] + pw["host_dec"][0]) / pw["host_enc"][1]     # ms per round trip per thread
+            t_gpu = pw["gpu_enc"][0] / pw["gpu_enc"][2] + pw["gpu_dec"][0] / pw["gpu_dec"][2]
+            # a thread's wall time per round trip also holds its waits and copies:
+            # when the host side bounded the warmup step, that step's time per
+            # host frame; otherwise the coder time plus a margin
+            per_warm = n_host / threads
+            t_eff = t_warm / per_warm if t_warm > 1.03 * t_gpu else 1.08 * t_host
+            t_eff = max(t_eff, t_host)
+            per = max(1, min(int(t_gpu / t_eff), host_frames_room(a, threads) // threads))
+            if world > 1:                      # one split for every rank: the slowest rank's
+                t = torch.tensor([per], dtype=torch.float64, device=cdev)
+                dist.all_reduce(t, op=dist.ReduceOp.MIN)
+                per = int(t[0])
+            n_host = min(per * threads, nfr - n_gpu)
+            nstep = n_host + n_gpu
+            balance = {"host_round_trip_ms": round(t_host, 1), "host_wall_ms_per_frame": round(t_eff, 1),
+                       "gpu_launch_pair_ms": round(t_gpu, 1), "warmup_step_ms": round(t_warm, 1),
+                       "host_frames_per_thread": per}
+            progress("balance: host %.0f ms per round trip, GPU %.0f ms per launch pair -> %d host frames per thread"
+                     % (t_host, t_gpu, per))
     if b is not None:
         b.prof_enable(True)
 
@@ -369,7 +416,7 @@ def main():
             ok &= r0 == chk.encode_ric(host0, a.q, a.trans)
             ok &= bool(np.array_equal(outs[0].cpu().numpy(), chk.decode_ric(r0)[0]))
             notes.append("frame %d vs oracle port" % mine[0][0])
-            if hybrid and n_host < nfr:
+            if hybrid and n_host < nstep:
                 k = n_host                     # the first frame the GPU stream coder encoded
                 rk = b.stream(k)
                 ok &= rk == chk.encode_ric(frames[k].cpu().numpy(), a.q, a.trans)
@@ -429,6 +476,8 @@ def main():
     coder = None
     if hybrid:
         coder = {"streams_per_launch": b.cp_pool, "frames_host_round_trip": n_host}
+        if balance:
+            coder["balance"] = balance
         for k, name in (("gpu_enc", "encode"), ("gpu_dec", "decode")):
             if k in per_launch:
                 ms, fr, ln = prof[k]
@@ -469,7 +518,7 @@ def main():
         split = {"encode_mpix_s": round(mpx / te, 2), "decode_mpix_s": round(mpx / td, 2),
                  "note": "rank 0, %d frames in groups of %d, groups not pipelined" % (nfr, slots)}
 
-    total_px = sum_px = nfr * W * H
+    total_px = sum_px = nstep * W * H
     if world > 1:
         t = torch.tensor([total_px], dtype=torch.float64, device=cdev)
         dist.all_reduce(t)
@@ -501,12 +550,12 @@ def main():
         "vs_baseline": None,
         "dtype": "int16",
         "data": "synthetic (SURVEY.md §8(d) generator), resident in HBM",
-        "config": {"workload": wl, "frames_per_gpu_per_step": nfr, "frames_per_launch": slots,
+        "config": {"workload": wl, "frames_per_gpu_per_step": nstep, "frames_per_launch": slots,
                    "host_coder_threads_per_gpu": threads, "parallelism": "frames sharded over %d GPU(s)" % world,
                    "coder": ("GPU stream coder (one wave per stream, %d streams per launch): encode%s of %d of %d "
                              "frames; host threads: %s" % (b.cp_pool, {0: "", 1: " and decode", 2: " (and decode of the "
                                                                         "launches the host threads have no room for)"}[gpu_dec],
-                                                           nfr - n_host, nfr,
+                                                           nstep - n_host, nstep,
                                                            {0: "round trips of the rest and every decode",
                                                             1: "round trips of the rest",
                                                             2: "round trips of the rest and the decode of the other "
@@ -527,7 +576,7 @@ def main():
         "per_level_us_per_frame": {"fwd": [round(x * 1e3, 2) if x else None for x in fwd],
                                    "inv": [round(x * 1e3, 2) if x else None for x in inv]},
         "stage_ms_per_frame": {k: round(v, 4) for k, v in per_frame.items()},
-        "bytes_per_frame": int(np.mean([len(b.stream(i)) for i in range(nfr)])) if b is not None else None,
+        "bytes_per_frame": int(np.mean([len(b.stream(i)) for i in range(nstep)])) if b is not None else None,
     }
     if hs:
         out["host_serial"] = hs

@@ -234,6 +234,7 @@ struct ric_batch {
 		uint32_t* h_res = nullptr;                 // pinned mirror
 		hipStream_t st[2] = {nullptr, nullptr};    // coder stream of each half
 		hipEvent_t ev_fwd[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr};
+		hipEvent_t ev_enc[2] = {nullptr, nullptr};   // a half's encode (and its result words) done
 	} cp;
 
 	int nslot() const { return 2 * slots; }
@@ -577,6 +578,7 @@ void ric_batch_destroy(ric_batch* b)
 		for (int h = 0; h < 2; h++) {
 			if (c.ev_fwd[h]) (void)hipEventDestroy(c.ev_fwd[h]);
 			if (c.ev_done[h]) (void)hipEventDestroy(c.ev_done[h]);
+			if (c.ev_enc[h]) (void)hipEventDestroy(c.ev_enc[h]);
 			if (c.st[h]) (void)hipStreamDestroy(c.st[h]);
 		}
 	}
@@ -895,6 +897,7 @@ int ric_batch_hybrid_config(ric_batch* b, int pool_frames, size_t stream_cap)
 		if (!c.st[h]) BCHK(hipStreamCreateWithFlags(&c.st[h], hipStreamNonBlocking));
 		if (!c.ev_fwd[h]) BCHK(hipEventCreateWithFlags(&c.ev_fwd[h], hipEventDisableTiming));
 		if (!c.ev_done[h]) BCHK(hipEventCreateWithFlags(&c.ev_done[h], hipEventDisableTiming));
+		if (!c.ev_enc[h]) BCHK(hipEventCreateWithFlags(&c.ev_enc[h], hipEventDisableTiming));
 	}
 	return RIC_OK;
 }
@@ -985,6 +988,9 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 		auto sp = b->prof.begin(B_GENC, m, c.st[h]);
 		if (launch_gc_encode(c.d_args + h, m, c.st[h])) return bfail(hipGetLastError(), "k_gc_encode") ? RIC_E_HIP : RIC_E_HIP;
 		b->prof.end(sp);
+		BCHK(hipMemcpyAsync(c.h_res + res_enc(h), c.d_res + res_enc(h), sizeof(uint32_t) * 2 * c.n, hipMemcpyDeviceToHost,
+		                    c.st[h]));
+		BCHK(hipEventRecord(c.ev_enc[h], c.st[h]));
 		if (gpu_decode == 1) bgpu[j] = 1;
 		else if (gpu_decode == 2) {
 			// the host pool's backlog (frames to decode, round trips queued), in seconds of its threads
@@ -1005,18 +1011,41 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 				return bfail(hipGetLastError(), "k_gc_decode") ? RIC_E_HIP : RIC_E_HIP;
 			b->prof.end(sd);
 		}
-		BCHK(hipMemcpyAsync(c.h_res + res_enc(h), c.d_res + res_enc(h), sizeof(uint32_t) * 3 * c.n, hipMemcpyDeviceToHost,
-		                    c.st[h]));
+		if (bgpu[j])
+			BCHK(hipMemcpyAsync(c.h_res + res_dec(h), c.d_res + res_dec(h), sizeof(uint32_t) * c.n, hipMemcpyDeviceToHost,
+			                    c.st[h]));
 		BCHK(hipEventRecord(c.ev_done[h], c.st[h]));
 		copied[j].reset(bgpu[j] ? 0 : m);
 		return RIC_OK;
 	};
 	// batch j's coder launches are done: (host decode) its decode groups become
 	// ready; (gpu_decode) its frames go through the inverse levels right away
+	// A GPU-decoded batch's .ric files leave for the host as soon as its encode
+	// is done, from a thread of their own (the host buffers are pageable: the
+	// copies block their caller), while the batch decodes on the GPU.
+	std::vector<std::thread> copier(nbatch > 0 ? nbatch : 1);
+	std::vector<int> copy_rc(nbatch > 0 ? nbatch : 1, RIC_OK);
+	int enc_seen = 0;                                      // batches whose encode event was handled
+	auto copy_out = [&](int j) {
+		const int f0 = batch_f0(j), m = batch_m(j), h = j & 1;
+		const uint32_t* re = c.h_res + res_enc(h);
+		copier[j] = std::thread([=, &copy_rc, &c] {
+			int r = set_dev(b->device);
+			for (int k = 0; k < m && !r; k++) {
+				if (re[2 * k + 1] || re[2 * k] > cap[f0 + k]) break;   // harvest reports it
+				if (bfail(hipMemcpy(out[f0 + k], c.d_out + ((size_t)h * c.n + k) * c.ocap, re[2 * k], hipMemcpyDeviceToHost),
+				          "hipMemcpy stream"))
+					r = RIC_E_HIP;
+			}
+			copy_rc[j] = r;
+		});
+	};
 	auto harvest = [&](int j) -> int {
 		const int f0 = batch_f0(j), m = batch_m(j), h = j & 1;
 		const uint32_t* re = c.h_res + res_enc(h);
 		const uint32_t* rd = c.h_res + res_dec(h);
+		if (copier[j].joinable()) copier[j].join();
+		if (copy_rc[j]) return copy_rc[j];
 		for (int k = 0; k < m; k++) {
 			if (re[2 * k + 1] == 2) {
 				clear_status(b);
@@ -1051,9 +1080,6 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 			if (!r) r = gpu_pix_out(b, 0, gm, qs.data(), pix_out + f0 + g0, 1);
 			if (r) return r;
 		}
-		for (int k = 0; k < m; k++)
-			BCHK(hipMemcpyAsync(out[f0 + k], c.d_out + ((size_t)h * c.n + k) * c.ocap, len[f0 + k], hipMemcpyDeviceToHost,
-			                    b->st));
 		return RIC_OK;
 	};
 	struct Flight {
@@ -1128,8 +1154,20 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 	};
 	bool running[2] = {false, false};
 	while (rc == RIC_OK && (finished < nbatch || !ready_host.empty() || !ready_dec.empty() || !fl.empty())) {
+		// the oldest batch whose encode is still out: a GPU-decoded batch's
+		// streams start for the host
+		if (enc_seen < kicked) {
+			const hipError_t e = hipEventQuery(c.ev_enc[enc_seen & 1]);
+			if (e == hipSuccess) {
+				if (bgpu[enc_seen]) copy_out(enc_seen);
+				enc_seen++;
+			} else if (e != hipErrorNotReady) {
+				rc = bfail(e, "coder stream") ? RIC_E_HIP : RIC_E_HIP;
+				break;
+			}
+		}
 		// the oldest coder batch (batches finish in order: one per half, alternating)
-		if (finished < kicked) {
+		if (finished < kicked && enc_seen > finished) {
 			const int h = finished & 1;
 			const hipError_t e = hipEventQuery(c.ev_done[h]);
 			if (e == hipSuccess) {
@@ -1168,8 +1206,10 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 			std::this_thread::sleep_for(std::chrono::milliseconds(1));
 		}
 	}
-	// on an error: let queued tasks and the coder finish before returning
+	// on an error: let queued tasks, copies and the coder finish before returning
 	while (!fl.empty()) { fl.front().done.wait(); fl.pop_front(); }
+	for (auto& t : copier)
+		if (t.joinable()) t.join();
 	for (int h = 0; h < 2; h++)
 		if (c.st[h]) (void)hipStreamSynchronize(c.st[h]);
 	const bool ok = !bfail(hipStreamSynchronize(b->st), "hipStreamSynchronize");

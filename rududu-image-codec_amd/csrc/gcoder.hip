@@ -19,6 +19,7 @@
 // i.e. to the reference's tree<encode> / pred<encode> / CMuxCodec.
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <cstdlib>
 
 #include "ric_types.h"
 #include "symbols.h"
@@ -1124,17 +1125,33 @@ __global__ void __launch_bounds__(64) k_gc_decode(const GDecArgs* __restrict__ a
 }
 }  // namespace
 
+// LDS footprint of a coder wave.  RIC_GC_LDS=<bytes> pads each coder
+// workgroup's LDS allocation (static + dynamic) up to that size, which caps the
+// coder waves per CU at floor(160 KiB / bytes): a CU's four SIMDs then hold at
+// most one coder wave each instead of two stacking on one SIMD (the scalar
+// coder issues from one wave per SIMD slot).  0 / unset: no padding.
+static size_t gc_dyn_lds(const void* kernel)
+{
+	static const long want = [] { const char* e = getenv("RIC_GC_LDS"); return e ? atol(e) : 0L; }();
+	if (want <= 0) return 0;
+	hipFuncAttributes fa;
+	if (hipFuncGetAttributes(&fa, kernel) != hipSuccess) return 0;
+	return (size_t)want > fa.sharedSizeBytes ? (size_t)want - fa.sharedSizeBytes : 0;
+}
+
 int launch_gc_encode(const GEncArgs* dev_args, int nframes, hipStream_t st)
 {
 	if (nframes <= 0) return 0;
-	hipLaunchKernelGGL(k_gc_encode, dim3(nframes), dim3(64), 0, st, dev_args);
+	static const size_t dyn = gc_dyn_lds((const void*)k_gc_encode);
+	hipLaunchKernelGGL(k_gc_encode, dim3(nframes), dim3(64), dyn, st, dev_args);
 	return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int launch_gc_decode(const GDecArgs* dev_args, int nframes, hipStream_t st)
 {
 	if (nframes <= 0) return 0;
-	hipLaunchKernelGGL(k_gc_decode, dim3(nframes), dim3(64), 0, st, dev_args);
+	static const size_t dyn = gc_dyn_lds((const void*)k_gc_decode);
+	hipLaunchKernelGGL(k_gc_decode, dim3(nframes), dim3(64), dyn, st, dev_args);
 	return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
