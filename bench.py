@@ -86,7 +86,7 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="C3", choices=["C3", "C4", "C5"])
     ap.add_argument("--frames", type=int, default=0,
                     help="C3: frames per GPU per step (default 8 per host thread); C5: frames per step in total (64)")
@@ -105,6 +105,7 @@ def parse():
                          "mix = GPU stream encoder, each launch decoded by the host threads or the GPU stream decoder "
                          "(whichever has room)")
     ap.add_argument("--pool", type=int, default=512, help="hybrid / gpu: frames per GPU stream-coder launch")
+    ap.add_argument("--launches", type=int, default=2, help="hybrid / gpu: stream-coder launches per step")
     ap.add_argument("--distinct", type=int, default=128,
                     help="distinct frames resident in HBM (inputs, outputs) and host stream buffers; a longer step cycles them")
     ap.add_argument("--n-host", type=int, default=-1,
@@ -209,7 +210,7 @@ def workload_frames(a, rank, world, threads):
         W, H = 7680, 4320
         if getattr(a, "coder", "host") in ("hybrid", "gpu", "mix"):
             # two stream-coder launches in flight plus the host threads' round trips
-            n = a.frames or a.batch or 2 * a.pool + host_frames_room(a, threads)
+            n = a.frames or a.batch or getattr(a, "launches", 2) * a.pool + host_frames_room(a, threads)
         else:
             n = a.frames or a.batch or 8 * threads
         return W, H, 1, [(rank * n + i, rank * n + i, None) for i in range(n)], "weak"
@@ -291,7 +292,7 @@ def main():
     if hybrid:
         n_host = min(nfr, default_n_host(a, threads))
         # the stream coder's frames: two launches in flight (or the rest of --frames)
-        n_gpu = nfr - n_host if (a.frames or a.batch) else min(2 * a.pool, nfr - n_host)
+        n_gpu = nfr - n_host if (a.frames or a.batch) else min(a.launches * a.pool, nfr - n_host)
         nstep = n_host + n_gpu
         # stream capacity: 3 bits per pixel (a q9 C3 stream is 1.7), 16-byte multiple
         b.cp_pool = min(a.pool, max(n_gpu, 1))
@@ -366,13 +367,18 @@ def main():
         if pw["host_enc"][1] and pw["gpu_enc"][2] and pw["gpu_dec"][2]:
             t_host = (pw["host_enc"][0] + pw["host_dec"][0]) / pw["host_enc"][1]     # ms per round trip per thread
             t_gpu = pw["gpu_enc"][0] / pw["gpu_enc"][2] + pw["gpu_dec"][0] / pw["gpu_dec"][2]
-            # a thread's wall time per round trip also holds its waits and copies:
-            # when the host side bounded the warmup step, that step's time per
-            # host frame; otherwise the coder time plus a margin
+            # the warmup step's own timeline: when the host side (its last round
+            # trip group) and the GPU side (its last coder batch) finished; the
+            # host share is scaled so both end together (a little before the GPU)
             per_warm = n_host / threads
-            t_eff = t_warm / per_warm if t_warm > 1.03 * t_gpu else 1.08 * t_host
-            t_eff = max(t_eff, t_host)
-            per = max(1, min(int(t_gpu / t_eff), host_frames_room(a, threads) // threads))
+            th, tg = b.hybrid_times()
+            if th > 0 and tg > 0:
+                t_eff = th / per_warm                       # host wall ms per round trip per thread
+                per = int(per_warm * (tg - 150.0) / th)
+            else:
+                t_eff = 1.08 * t_host
+                per = int(t_gpu / t_eff)
+            per = max(1, min(per, host_frames_room(a, threads) // threads))
             if world > 1:                      # one split for every rank: the slowest rank's
                 t = torch.tensor([per], dtype=torch.float64, device=cdev)
                 dist.all_reduce(t, op=dist.ReduceOp.MIN)
@@ -381,6 +387,7 @@ def main():
             nstep = n_host + n_gpu
             balance = {"host_round_trip_ms": round(t_host, 1), "host_wall_ms_per_frame": round(t_eff, 1),
                        "gpu_launch_pair_ms": round(t_gpu, 1), "warmup_step_ms": round(t_warm, 1),
+                       "warmup_host_side_ms": round(th, 1), "warmup_gpu_side_ms": round(tg, 1),
                        "host_frames_per_thread": per}
             progress("balance: host %.0f ms per round trip, GPU %.0f ms per launch pair -> %d host frames per thread"
                      % (t_host, t_gpu, per))

@@ -194,6 +194,11 @@ int ric_batch_hybrid_config(ric_batch* b, int pool_frames, size_t stream_cap);
  * launch, the GPU for the rest).  Byte-identical streams either way. */
 int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, int n_host, int gpu_decode, int q,
                                int trans, uint8_t* const* out, const size_t* cap, size_t* len, uint8_t* const* pix_out);
+/* When each side of the last ric_batch_roundtrip_hybrid finished, in ms from
+ * its entry: the last host round-trip group, the last stream-coder batch (0
+ * for a side with no work).  For splitting frames between the two (no
+ * reference counterpart). */
+int ric_batch_hybrid_times(ric_batch* b, double* host_ms, double* gpu_ms);
 /* Stage timers of the batch (no reference counterpart): 0 pixel conversion
  * in, 1..8 forward level 0..7 (fused DWT + quantiser + records), 9 D2H of
  * bands + records, 10 host encode, 11 host decode, 12 H2D of the bands,

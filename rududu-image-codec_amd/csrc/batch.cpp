@@ -18,6 +18,8 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <functional>
@@ -201,6 +203,7 @@ struct BProf {
 
 struct ric_batch {
 	int device = 0, w = 0, h = 0, channels = 1, slots = 0;
+	double hyb_host_ms = 0, hyb_gpu_ms = 0;        // last hybrid call: when each side finished (ms from entry)
 	Pyramid P;
 	size_t astride = 0, hstride = 0, pstride = 0;   // bytes per slot: device arena, host mirror, coding planes
 	long pitch = 0;                                // coding plane row pitch (elements)
@@ -950,6 +953,15 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 		BCHK(hipMemcpy(c.d_args, c.args, sizeof(c.args), hipMemcpyHostToDevice));
 		BCHK(hipMemcpy(c.d_dargs, c.dargs, sizeof(c.dargs), hipMemcpyHostToDevice));
 	}
+	// RIC_HYBRID_TRACE=1: the step's timeline on stderr (kicks, encode ends,
+	// harvests, host groups, the end), ms from entry
+	static const bool trace = [] { const char* e = getenv("RIC_HYBRID_TRACE"); return e && atoi(e) > 0; }();
+	const double t_entry = now_ms();
+	auto tr = [&](const char* what, int j) {
+		if (trace) fprintf(stderr, "[hybrid] %9.1f ms %s %d\n", now_ms() - t_entry, what, j);
+	};
+	int host_groups_done = 0;
+	b->hyb_host_ms = b->hyb_gpu_ms = 0;
 	std::deque<HGroup> ready_host, ready_dec;
 	for (int f0 = 0; f0 < n_host; f0 += S) ready_host.push_back({f0, std::min(S, n_host - f0), false, 0, 0});
 	const int ng = n - n_host;
@@ -1005,6 +1017,7 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 			bgpu[j] = backlog_ms > enc_ms_est ? 1 : 0;
 		}
 		t_kick[j] = now_ms();
+		tr("kick", j);
 		if (bgpu[j]) {
 			auto sd = b->prof.begin(B_GDEC, m, c.st[h]);
 			if (launch_gc_decode(c.d_dargs + h, m, c.st[h]))
@@ -1145,6 +1158,10 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 		int r2 = RIC_OK;
 		if (r && r != RIC_E_STREAM) r2 = r;
 		stream_err |= r == RIC_E_STREAM;
+		if (!F.g.gpu) {
+			b->hyb_host_ms = now_ms() - t_entry;
+			if (++host_groups_done == 1 || host_groups_done == (n_host + S - 1) / S) tr("host group done", host_groups_done);
+		}
 		if (!r2) r2 = gpu_decode_plane(b, F.set, F.g.m, 0, qs.data(), trans);
 		if (!r2) r2 = gpu_pix_out(b, F.set, F.g.m, qs.data(), pix_out + F.g.f0, 1);
 		if (!r2) BCHK(hipEventRecord(F.ev, b->st));   // the set's mirrors are free once this passes
@@ -1159,6 +1176,7 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 		if (enc_seen < kicked) {
 			const hipError_t e = hipEventQuery(c.ev_enc[enc_seen & 1]);
 			if (e == hipSuccess) {
+				tr("encoded", enc_seen);
 				if (bgpu[enc_seen]) copy_out(enc_seen);
 				enc_seen++;
 			} else if (e != hipErrorNotReady) {
@@ -1172,6 +1190,8 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 			const hipError_t e = hipEventQuery(c.ev_done[h]);
 			if (e == hipSuccess) {
 				running[h] = false;
+				b->hyb_gpu_ms = now_ms() - t_entry;
+				tr("decoded", finished);
 				rc = harvest(finished);
 				finished++;
 				if (rc) break;
@@ -1213,6 +1233,7 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 	for (int h = 0; h < 2; h++)
 		if (c.st[h]) (void)hipStreamSynchronize(c.st[h]);
 	const bool ok = !bfail(hipStreamSynchronize(b->st), "hipStreamSynchronize");
+	tr("end", rc);
 	for (auto& e : evs) (void)hipEventDestroy(e);
 	if (rc == RIC_E_HIP) clear_status(b);
 	if (rc) return rc;
@@ -1261,3 +1282,13 @@ int ric_batch_prof_read(ric_batch* b, double* ms, long* frames, long* launches, 
 }
 
 }  // extern "C"
+
+// When each side of the last ric_batch_roundtrip_hybrid finished: its last
+// host round-trip group and its last stream-coder batch (ms from entry).
+int ric_batch_hybrid_times(ric_batch* b, double* host_ms, double* gpu_ms)
+{
+	if (!b || !host_ms || !gpu_ms) return RIC_E_ARG;
+	*host_ms = b->hyb_host_ms;
+	*gpu_ms = b->hyb_gpu_ms;
+	return RIC_OK;
+}

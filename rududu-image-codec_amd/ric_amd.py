@@ -91,6 +91,7 @@ def lib():
         "ric_batch_prof_enable": (_I, [_P, _I]),
         "ric_batch_encode_gpu": (_I, [_P, _P, _I, _I, _I, _P, ctypes.c_size_t, ctypes.c_size_t, _P]),
         "ric_batch_hybrid_config": (_I, [_P, _I, ctypes.c_size_t]),
+        "ric_batch_hybrid_times": (_I, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
         "ric_batch_decode_gpu": (_I, [_P, _P, ctypes.c_size_t, _P, _I, _P]),
         "ric_diag_gdec_dbg": (_I, [_P]),
         "ric_batch_roundtrip_hybrid": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
@@ -380,6 +381,12 @@ class Batch:
     def hybrid_config(self, pool_frames, stream_cap):
         """Pool of the GPU stream coder (ric_batch_hybrid_config)."""
         _chk(lib().ric_batch_hybrid_config(self.h, pool_frames, stream_cap), "ric_batch_hybrid_config")
+
+    def hybrid_times(self):
+        """(host side, GPU side) end of the last roundtrip_hybrid, ms from its start."""
+        hm, gm = ctypes.c_double(), ctypes.c_double()
+        _chk(lib().ric_batch_hybrid_times(self.h, ctypes.byref(hm), ctypes.byref(gm)), "ric_batch_hybrid_times")
+        return hm.value, gm.value
 
     def roundtrip_hybrid(self, frames, pix_out, n_host, q=9, trans=0, gpu_decode=False, streams=None):
         """ric_batch_roundtrip_hybrid: frames[:n_host] round trips on the host,
