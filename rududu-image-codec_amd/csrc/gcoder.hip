@@ -549,6 +549,7 @@ __global__ void __launch_bounds__(64) k_gc_encode(const GEncArgs* __restrict__ a
 // reads past what was staged (a pathological stream) is flagged.
 constexpr uint32_t kDRing = 4096;
 constexpr uint32_t kDAhead = 2048;     // bytes staged past the read position at each refill
+constexpr uint32_t kDMargin = 512;     // staged bytes kept ahead of a block / a unary run's bin
 __shared__ __attribute__((aligned(16))) uint8_t g_dring[kDRing];
 __shared__ int32_t g_blk[64 * 16];     // the current chunk's decoded blocks, 16 values each
 
@@ -572,9 +573,13 @@ struct GDec {
 	// big-endian: file byte wf + o is bits 56 - 8 o of win (the byte swap is one
 	// VALU op on the dword read from LDS)
 	GC_DI uint32_t rd_dword(uint32_t f) const { return __builtin_bswap32(*(const uint32_t*)(g_dring + (f & (kDRing - 1)))); }
+	// The window only moves inside what is staged: ensure() keeps at least
+	// kDMargin staged bytes ahead before every block (and LL value) and before
+	// every bin of a unary run, the one place a block can read without bound;
+	// outside runs a block reads < 256 bytes (16 values x (a bin's <= 4
+	// normalisation bytes + <= 25 raw bits), the tree bit, k, the enum code).
 	GC_DI void wadvance()
 	{
-		if (__builtin_expect(wf + 24 >= st_hi, 0)) stage_now();
 		win = (win << 32) | nxt;
 		wf += 4;
 		nxt = rd_dword(wf + 8);
@@ -620,6 +625,10 @@ struct GDec {
 	// that read past them
 	// (pend == st_hi: the next KiB is in flight.)  Staging only advances with
 	// the read position, so the ring always keeps the bytes just behind it.
+	GC_DI void ensure()
+	{
+		if (__builtin_expect(st_hi < p + 7 + kDMargin, 0)) stage_now();
+	}
 	GC_DI void refill()
 	{
 		if (st_hi >= p + 7 + kDAhead) return;
@@ -835,6 +844,7 @@ struct GGeoD {                                          // one CGeomCodec contex
 			do {
 				fr -= fr >> (3 + s);
 				if (++l > lmax) break;
+				d.ensure();
 			} while (d.bit(f));
 		}
 		int out;
@@ -892,6 +902,7 @@ GC_DI void pred_dec(GDec& d, const GTabs& T, const GBandDesc& B, char* arena)
 			for (int q = 0; q < nx; q++) {
 				const int x = x0 + q;
 				int v;
+				d.ensure();
 				if (j == 0 && x == 0) {
 					v = trunc_c(is_int, u2s((int)d.taboo()));
 				} else {
@@ -1001,6 +1012,7 @@ GC_DI void tree_dec(GDec& d, const GTabs& T, const GBandDesc& B, const GBandDesc
 		for (int j = 0; j < nj; j++) {
 			const uint32_t in = lget(info, (uint32_t)j);
 			const uint32_t ob = (uint32_t)j * 16;
+			d.ensure();
 			if ((in >> 5) & 1) {
 				if ((in >> 6) & 1) continue;                   // propagated
 				const uint32_t ctx = in & 31u;
