@@ -584,11 +584,9 @@ struct GDec {
 		wf += 4;
 		nxt = rd_dword(wf + 8);
 	}
-	GC_DI uint32_t byte(uint32_t x) const            // x + 7 in [wf, wf + 8)
-	{
-		const uint32_t b = (uint32_t)(win >> (56 - ((x + 7) - wf) * 8)) & 255u;
-		return (x < 2 || x >= n + 2) ? 0u : b;
-	}
+	// x + 7 in [wf, wf + 8).  The ring holds the virtual stream: the two bytes
+	// in front and everything past the payload are zeroed when staged.
+	GC_DI uint32_t byte(uint32_t x) const { return (uint32_t)(win >> (56 - ((x + 7) - wf) * 8)) & 255u; }
 	GC_DI uint32_t next()
 	{
 		const uint32_t b = byte(p);
@@ -601,6 +599,15 @@ struct GDec {
 		const uint32_t o = off + lane_id() * 16;
 		u32x4 v = {0, 0, 0, 0};
 		if (o + 16 <= flen) v = *gld((const u32x4*)(file + o));
+		// virtual bytes past the payload read as 0 (ric.cpp's zero padding):
+		// file bytes from n + 9 on
+		const uint32_t end = n + 9;
+		RIC_UNROLL
+		for (int i = 0; i < 4; i++) {
+			const uint32_t b = o + 4 * (uint32_t)i;
+			const uint32_t keep = end <= b ? 0u : (end - b >= 4 ? 4u : end - b);
+			v[i] &= keep >= 4 ? 0xFFFFFFFFu : (1u << (8 * keep)) - 1u;
+		}
 		return v;
 	}
 	GC_DI void put_kib(uint32_t off, const u32x4& v)
@@ -642,6 +649,7 @@ struct GDec {
 		if (flen > cap) flen = cap;
 		st_hi = 0;
 		for (uint32_t off = 0; off < 2 * 1024 + 1024; off += 1024) { put_kib(off, load_kib(off)); st_hi = off + 1024; }
+		g_dring[7 + (lane_id() & 1)] = 0;                // virtual bytes 0, 1 (file 7, 8: the header's tail)
 		pend = st_hi;
 		stage = load_kib(pend);
 		limit = npay + 2 + 65536 - 16;
@@ -680,22 +688,18 @@ struct GDec {
 	GC_DI void fill(uint32_t len)                        // fillBuffer, muxcodec.cpp:572-579
 	{
 		// the nb bytes fillBuffer reads one at a time, taken from the window at
-		// once when they all lie inside the payload (the window holds >= 5 bytes
-		// at the read position; nb <= 4)
+		// once (nb <= 4: len <= 26; the window holds >= 5 bytes at the read
+		// position; bytes past the payload are the ring's zeros).  One straight
+		// path, no byte loop: a corrupt stream that runs to the read limit stops
+		// there and is flagged, as next() does.
 		const uint32_t nb = (len - nbits + 7) >> 3;
-		if (__builtin_expect(p + nb <= n + 2 && nb <= 4, 1)) {
-			const uint32_t o = p + 7 - wf;
-			const uint32_t v = (uint32_t)((win << (8 * o)) >> (64 - 8 * nb));
-			buffer = (uint32_t)(((uint64_t)buffer << (8 * nb)) | v);
-			nbits += 8 * nb;
-			p += nb;
-			while (p + 7 >= wf + 4) wadvance();
-			return;
-		}
-		do {
-			nbits += 8;
-			buffer = (buffer << 8) | next();
-		} while (nbits < len);
+		const uint32_t o = p + 7 - wf;
+		const uint32_t v = (uint32_t)((win << (8 * o)) >> (64 - 8 * nb));
+		buffer = (uint32_t)(((uint64_t)buffer << (8 * nb)) | v);
+		nbits += 8 * nb;
+		p += nb;
+		if (__builtin_expect(p > limit, 0)) { p = limit; ovf |= 1; }
+		if (p + 7 >= wf + 4) wadvance();
 	}
 	GC_DI uint32_t bits(uint32_t len)                    // bitsDecode, muxcodec.h:233-239
 	{
