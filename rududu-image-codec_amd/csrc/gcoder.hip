@@ -43,6 +43,8 @@ template <typename T> GC_DI GAS T* gst(T* p) { return (GAS T*)p; }
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 GC_DI uint32_t lane_id() { return __lane_id(); }
+// a wave-uniform value kept in a VGPR (the compiler would give it an SGPR)
+GC_DI uint32_t to_vgpr(uint32_t x) { uint32_t r; asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "s"(x)); return r; }
 // lane arrays: element i of a per-wave array held in lane i of a VGPR
 GC_DI uint32_t lget(uint32_t a, uint32_t i) { return __builtin_amdgcn_readlane(a, i); }
 GC_DI uint32_t lset(uint32_t a, uint32_t i, uint32_t x) { return lane_id() == i ? x : a; }
@@ -554,14 +556,14 @@ __shared__ __attribute__((aligned(16))) uint8_t g_dring[kDRing];
 __shared__ int32_t g_blk[64 * 16];     // the current chunk's decoded blocks, 16 values each
 
 struct GDec {
-	const uint8_t* file;
-	uint32_t n;                        // payload bytes read (ric.cpp: at most W*H)
-	uint32_t flen;                     // file bytes that may be loaded
+	// Staging-only values, held in VGPRs (the lanes use them; the scalar walk
+	// never does): the file's address, the payload size n (ric.cpp: at most
+	// W*H), the file bytes that may be loaded.  SGPRs are the scarce resource.
+	uint32_t vfile_lo, vfile_hi, vn, vflen;
 	uint32_t range, low, code, nbits, buffer;
 	uint32_t p, limit;
 	uint32_t ovf;                      // 1: read past the end (RIC_E_STREAM), 2: ring overrun
 	uint32_t st_hi;                    // file bytes [.., st_hi) are in the ring
-	uint32_t pend;                     // file offset of the 1 KiB in flight in `stage`
 	u32x4 stage;
 	uint64_t win;                      // file bytes [wf, wf + 8)
 	uint32_t wf, nxt;
@@ -598,10 +600,10 @@ struct GDec {
 	{
 		const uint32_t o = off + lane_id() * 16;
 		u32x4 v = {0, 0, 0, 0};
-		if (o + 16 <= flen) v = *gld((const u32x4*)(file + o));
+		if (o + 16 <= vflen) v = *gld((const u32x4*)((((uint64_t)vfile_hi << 32) | vfile_lo) + o));
 		// virtual bytes past the payload read as 0 (ric.cpp's zero padding):
 		// file bytes from n + 9 on
-		const uint32_t end = n + 9;
+		const uint32_t end = vn + 9;
 		RIC_UNROLL
 		for (int i = 0; i < 4; i++) {
 			const uint32_t b = o + 4 * (uint32_t)i;
@@ -614,19 +616,18 @@ struct GDec {
 	{
 		*(u32x4*)(g_dring + ((off + lane_id() * 16) & (kDRing - 1))) = v;
 	}
-	// stage file bytes up to kDAhead past the read position (pend == st_hi: the
-	// next KiB is in flight in `stage`)
+	// stage file bytes up to kDAhead past the read position (the KiB at st_hi
+	// is in flight in `stage`)
 	GC_DI void stage_now()
 	{
-		put_kib(pend, stage);
-		st_hi = pend + 1024;
+		put_kib(st_hi, stage);
+		st_hi += 1024;
 		while (st_hi < p + 7 + kDAhead) {
 			const u32x4 v = load_kib(st_hi);
 			put_kib(st_hi, v);
 			st_hi += 1024;
 		}
-		pend = st_hi;
-		stage = load_kib(pend);
+		stage = load_kib(st_hi);
 	}
 	// between chunks: the bytes a chunk may read are staged; flags a chunk
 	// that read past them
@@ -644,14 +645,16 @@ struct GDec {
 	// f: the file, len its size, cap the bytes readable at f (a multiple of 16)
 	GC_DI void init(const uint8_t* f, uint32_t len, uint32_t cap, uint32_t npay)
 	{
-		file = f; n = npay;
-		flen = (len + 15) & ~15u;
-		if (flen > cap) flen = cap;
+		uint32_t fl = (len + 15) & ~15u;
+		if (fl > cap) fl = cap;
+		vfile_lo = to_vgpr((uint32_t)(uintptr_t)f);
+		vfile_hi = to_vgpr((uint32_t)((uintptr_t)f >> 32));
+		vn = to_vgpr(npay);
+		vflen = to_vgpr(fl);
 		st_hi = 0;
 		for (uint32_t off = 0; off < 2 * 1024 + 1024; off += 1024) { put_kib(off, load_kib(off)); st_hi = off + 1024; }
 		g_dring[7 + (lane_id() & 1)] = 0;                // virtual bytes 0, 1 (file 7, 8: the header's tail)
-		pend = st_hi;
-		stage = load_kib(pend);
+		stage = load_kib(st_hi);
 		limit = npay + 2 + 65536 - 16;
 		range = 1u << 16;
 		nbits = 0; buffer = 0; ovf = 0;
