@@ -364,13 +364,14 @@ def main():
         progress("warmup step %d/%d" % (i + 1, a.warmup))
     if auto:
         pw = b.prof_read()
+        per_warm = n_host // threads
+        per, t_host, t_gpu, t_eff, th, tg = per_warm, 0.0, 0.0, 0.0, 0.0, 0.0
         if pw["host_enc"][1] and pw["gpu_enc"][2] and pw["gpu_dec"][2]:
             t_host = (pw["host_enc"][0] + pw["host_dec"][0]) / pw["host_enc"][1]     # ms per round trip per thread
             t_gpu = pw["gpu_enc"][0] / pw["gpu_enc"][2] + pw["gpu_dec"][0] / pw["gpu_dec"][2]
             # the warmup step's own timeline: when the host side (its last round
             # trip group) and the GPU side (its last coder batch) finished; the
             # host share is scaled so both end together (a little before the GPU)
-            per_warm = n_host / threads
             th, tg = b.hybrid_times()
             if th > 0 and tg > 0:
                 t_eff = th / per_warm                       # host wall ms per round trip per thread
@@ -379,18 +380,18 @@ def main():
                 t_eff = 1.08 * t_host
                 per = int(t_gpu / t_eff)
             per = max(1, min(per, host_frames_room(a, threads) // threads))
-            if world > 1:                      # one split for every rank: the slowest rank's
-                t = torch.tensor([per], dtype=torch.float64, device=cdev)
-                dist.all_reduce(t, op=dist.ReduceOp.MIN)
-                per = int(t[0])
-            n_host = min(per * threads, nfr - n_gpu)
-            nstep = n_host + n_gpu
-            balance = {"host_round_trip_ms": round(t_host, 1), "host_wall_ms_per_frame": round(t_eff, 1),
-                       "gpu_launch_pair_ms": round(t_gpu, 1), "warmup_step_ms": round(t_warm, 1),
-                       "warmup_host_side_ms": round(th, 1), "warmup_gpu_side_ms": round(tg, 1),
-                       "host_frames_per_thread": per}
-            progress("balance: host %.0f ms per round trip, GPU %.0f ms per launch pair -> %d host frames per thread"
-                     % (t_host, t_gpu, per))
+        if world > 1:                          # one split for every rank: the slowest rank's
+            t = torch.tensor([per], dtype=torch.float64, device=cdev)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            per = int(t[0])
+        n_host = min(per * threads, nfr - n_gpu)
+        nstep = n_host + n_gpu
+        balance = {"host_round_trip_ms": round(t_host, 1), "host_wall_ms_per_frame": round(t_eff, 1),
+                   "gpu_launch_pair_ms": round(t_gpu, 1), "warmup_step_ms": round(t_warm, 1),
+                   "warmup_host_side_ms": round(th, 1), "warmup_gpu_side_ms": round(tg, 1),
+                   "host_frames_per_thread": per}
+        progress("balance: host side %.0f ms, GPU side %.0f ms in the last warmup step -> %d host frames per thread"
+                 % (th, tg, per))
     if b is not None:
         b.prof_enable(True)
 
