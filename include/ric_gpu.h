@@ -106,14 +106,34 @@ int ric_band_host(ric_wavelet* w, int index, void** ptr, int* pitch);
 
 /* ------------------------------------------------------------- ric_mux */
 /* CMuxCodec(unsigned char* pStream, unsigned short firstWord)
- * (src/lib/muxcodec.h:102): encoder writing at most cap bytes into buf. */
+ * (src/lib/muxcodec.h:102): encoder writing at most cap bytes into buf
+ * (cap SIZE_MAX: no bound, the reference's contract).  buf NULL is the
+ * reference's CMuxCodec(0, 0) (src/lib/rududucodec.cpp:36): no output until
+ * ric_mux_reinit_encoder gives it a buffer. */
 int ric_mux_create_encoder(ric_mux** out, uint8_t* buf, size_t cap, uint16_t first_word);
+/* CMuxCodec::initCoder(unsigned short firstWord, unsigned char* pStream)
+ * (src/lib/muxcodec.h:104, muxcodec.cpp:36-49): restart the coder (low =
+ * firstWord << 16, full range, empty bit buffer).  buf non-NULL: the output
+ * restarts at buf (cap bytes; SIZE_MAX: no bound); NULL keeps the output
+ * position, as in the reference.  Turns a decoder object into an encoder
+ * (the reference's one CMuxCodec serves both, src/lib/rududucodec.cpp:89,123). */
+int ric_mux_reinit_encoder(ric_mux* m, uint8_t* buf, size_t cap, uint16_t first_word);
+/* CMuxCodec::initDecoder(unsigned char* pStream) (src/lib/muxcodec.h:105,
+ * muxcodec.cpp:51-61): restart the decoder on buf (payload at buf + 2): len
+ * bytes copied and zero padded, or len 0 to read buf in place with no end
+ * (the reference's form; UNSAFE on untrusted input, see below).  buf NULL
+ * only resets the range and bit buffer, as in the reference. */
+int ric_mux_reinit_decoder(ric_mux* m, const uint8_t* buf, size_t len);
 /* CMuxCodec(unsigned char* pStream) (src/lib/muxcodec.h:103): decoder over
  * len bytes of buf (the reference reads its payload from buf + 2). */
 int ric_mux_create_decoder(ric_mux** out, const uint8_t* buf, size_t len);
 /* CMuxCodec(unsigned char* pStream) exactly (src/lib/muxcodec.h:103,
  * muxcodec.cpp:31-34): reads buf + 2 in place with no end, like the
- * reference (the caller's buffer must hold the stream). */
+ * reference (the caller's buffer must hold the stream).
+ * UNSAFE on untrusted input: a corrupt or truncated stream makes the decoder
+ * read past the caller's buffer, as the reference's does.  Kept for source
+ * compatibility only; untrusted streams go through ric_mux_create_decoder
+ * (bounded) -- every product path does. */
 int ric_mux_create_decoder_inplace(ric_mux** out, const uint8_t* buf);
 /* CMuxCodec::endCoding() (src/lib/muxcodec.h:106): *len_out = end - buf. */
 int ric_mux_end(ric_mux* m, size_t* len_out);
@@ -168,7 +188,8 @@ int ric_batch_roundtrip(ric_batch* b, const uint8_t* const* pix, int n, int q, i
 /* The whole CompressImage of n <= slots gray frames on the GPU, the serial
  * coder included (one wave per frame's stream): pix[i] device pixels; the
  * .ric file of frame i to out + i * ostride (DEVICE memory, cap <= ostride
- * bytes each), its size to len[i] (host).  Byte-identical to ric_batch_encode.
+ * bytes each; cap and ostride multiples of 16, else RIC_E_ARG), its size to
+ * len[i] (host).  Byte-identical to ric_batch_encode.
  * No reference counterpart (the reference's CompressImage is one stream on
  * one host thread). */
 int ric_batch_encode_gpu(ric_batch* b, const uint8_t* const* pix, int n, int q, int trans, uint8_t* out, size_t ostride,
@@ -178,8 +199,17 @@ int ric_batch_encode_gpu(ric_batch* b, const uint8_t* const* pix, int n, int q, 
  * (DEVICE memory, istride a multiple of 16), their sizes len[i]; pixels to
  * device pix_out[i].  RIC_E_STREAM as ric_batch_decode. */
 int ric_batch_decode_gpu(ric_batch* b, const uint8_t* in, size_t istride, const size_t* len, int n, uint8_t* const* pix_out);
-/* Diagnostics: the stream decoder dumps 8 words of coder state after the LL
- * and after each band (64 slots per frame) into dev_buf (null: off). */
+/* Diagnostics (no reference counterpart), process-wide: while dev_buf is set,
+ * every ric_batch_decode_gpu call of n frames writes into it (u32 words):
+ *   frame f, words [f*2048, f*2048 + 512): 8 words of coder state (range, low,
+ *     code, nbits, buffer, read position, overflow flags, 0xC0DE) after the LL
+ *     and after each band, 64 slots;
+ *   frame f, words [f*2048 + 1024, f*2048 + 2048): the first 1024 values of
+ *     the decoded LL, row-major;
+ *   frame 0's whole decoded pyramid from word n*2048 on (finest first, D H V,
+ *     then the LL; dimx*dimy words per band).
+ * Size dev_buf for n*2048 words plus the pyramid's sample count.  NULL: off.
+ * One caller at a time (the pointer is a process global). */
 int ric_diag_gdec_dbg(void* dev_buf);
 /* Hybrid round trip (gray): the serial encoder runs on the GPU (one wave per
  * stream, launches of `pool_frames` frames, each stream up to stream_cap

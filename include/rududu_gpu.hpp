@@ -34,6 +34,7 @@
 #pragma once
 
 #include <cstdint>
+#include <climits>
 #include <cstdlib>
 #include <cstring>
 #include <iostream>
@@ -72,15 +73,13 @@ constexpr bounded_t bounded{};
 class CMuxCodec {
 public:
 	// CMuxCodec(unsigned char* pStream, unsigned short firstWord): encoder
-	// (src/lib/muxcodec.h:102).  Like the reference it takes no capacity: it
-	// codes into its own buffer (address space reserved, touched as it fills)
-	// and endCoding() copies the stream to pStream -- the caller's buffer must
-	// hold it, as with the reference.
+	// (src/lib/muxcodec.h:102).  Like the reference it takes no capacity and
+	// writes pStream in place -- the caller's buffer must hold the stream, as
+	// with the reference.  CMuxCodec(0, 0) (src/lib/rududucodec.cpp:36) is a
+	// coder without a buffer until initCoder / initDecoder give it one.
 	CMuxCodec(unsigned char* pStream, unsigned short firstWord) : buf_(pStream)
 	{
-		own_.reset((unsigned char*)std::malloc(kOwnCap));
-		if (!own_) throw std::bad_alloc();
-		ric_check(ric_mux_create_encoder(&m_, own_.get(), kOwnCap, firstWord), "CMuxCodec(encoder)");
+		ric_check(ric_mux_create_encoder(&m_, pStream, pStream ? SIZE_MAX : 0, firstWord), "CMuxCodec(encoder)");
 	}
 	// the bounded encoder: writes pStream directly, at most capacity bytes
 	CMuxCodec(unsigned char* pStream, unsigned short firstWord, size_t capacity) : buf_(pStream)
@@ -102,22 +101,46 @@ public:
 	CMuxCodec(const CMuxCodec&) = delete;
 	CMuxCodec& operator=(const CMuxCodec&) = delete;
 
+	// CMuxCodec::initCoder(unsigned short firstWord, unsigned char* pStream)
+	// (src/lib/muxcodec.h:104): restart as an encoder; pStream 0 keeps the
+	// output position, as in the reference
+	void initCoder(unsigned short firstWord, unsigned char* pStream)
+	{
+		ric_check(ric_mux_reinit_encoder(m_, pStream, SIZE_MAX, firstWord), "initCoder");
+		if (pStream) buf_ = pStream;
+	}
+	// the bounded form: at most capacity bytes at pStream
+	void initCoder(unsigned short firstWord, unsigned char* pStream, size_t capacity)
+	{
+		ric_check(ric_mux_reinit_encoder(m_, pStream, capacity, firstWord), "initCoder");
+		if (pStream) buf_ = pStream;
+	}
+	// CMuxCodec::initDecoder(unsigned char* pStream) (src/lib/muxcodec.h:105):
+	// restart as a decoder reading pStream + 2 in place, like the reference
+	void initDecoder(const unsigned char* pStream)
+	{
+		ric_check(ric_mux_reinit_decoder(m_, pStream, 0), "initDecoder");
+		if (pStream) buf_ = const_cast<unsigned char*>(pStream);
+	}
+	// the bounded form: `length` bytes of pStream
+	void initDecoder(const unsigned char* pStream, size_t length, bounded_t)
+	{
+		ric_check(ric_mux_reinit_decoder(m_, pStream, length), "initDecoder");
+		if (pStream) buf_ = const_cast<unsigned char*>(pStream);
+	}
+
 	unsigned char* endCoding()
 	{
 		size_t n = 0;
 		ric_check(ric_mux_end(m_, &n), "endCoding");
-		if (own_) std::memcpy(buf_, own_.get(), n);
 		return buf_ + n;
 	}
 	unsigned int getSize() { return (unsigned int)ric_mux_size(m_); }
 	ric_mux* handle() { return m_; }
 
 private:
-	static constexpr size_t kOwnCap = (size_t)1 << 30;
-	struct Free { void operator()(unsigned char* p) const { std::free(p); } };
 	ric_mux* m_ = nullptr;
 	unsigned char* buf_;
-	std::unique_ptr<unsigned char, Free> own_;
 };
 
 // CBand::pBand: converts to a typed pointer into the band's host mirror

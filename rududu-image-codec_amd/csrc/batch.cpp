@@ -481,6 +481,15 @@ struct FirstErr {
 	}
 };
 
+// Two frames of one call must not share an output buffer: different threads
+// (host coders, the stream copier) write them concurrently.
+bool outputs_distinct(uint8_t* const* out, int n)
+{
+	std::vector<uint8_t*> v(out, out + n);
+	std::sort(v.begin(), v.end());
+	return std::adjacent_find(v.begin(), v.end()) == v.end();
+}
+
 int check_header(ric_batch* b, const uint8_t* ric, size_t len, int* q, int* trans)
 {
 	int w, h, ch;
@@ -664,6 +673,7 @@ int ric_batch_roundtrip(ric_batch* b, const uint8_t* const* pix, int n, int q, i
 	if (!b || !pix || !out || !cap || !len || !pix_out || n < 0 || q < 0 || q > 31 || trans < 0 || trans > 2)
 		return RIC_E_ARG;
 	if (n == 0) return RIC_OK;
+	if (!outputs_distinct(out, n)) return set_last_error("ric_batch_roundtrip: out[] buffers must be distinct"), RIC_E_ARG;
 	if (set_dev(b->device)) return RIC_E_HIP;
 	const int S = b->slots;
 	const int G = (n + S - 1) / S;
@@ -748,8 +758,10 @@ int ric_batch_roundtrip(ric_batch* b, const uint8_t* const* pix, int n, int q, i
 int ric_batch_encode_gpu(ric_batch* b, const uint8_t* const* pix, int n, int q, int trans, uint8_t* out, size_t ostride,
                          size_t cap, size_t* len)
 {
+	// the coder stores 16-byte chunks (gcoder.hip GEnc::flush_to): a capacity or
+	// stride off a multiple of 16 would drop the stream's last bytes unflagged
 	if (!b || !pix || !out || !len || n < 0 || n > b->slots || q < 0 || q > 31 || trans < 0 || trans > 2 || cap > ostride ||
-	    cap > 0xFFFFFFF0u)
+	    cap > 0xFFFFFFF0u || (cap & 15) || (ostride & 15))
 		return RIC_E_ARG;
 	if (b->channels != 1) return RIC_E_ARG;      // one plane per stream here; colour goes through ric_batch_encode
 	if (n == 0) return RIC_OK;
@@ -926,6 +938,8 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 	if (b->channels != 1) return RIC_E_ARG;
 	if (n_host < n && !b->cp.d_ab) return RIC_E_ARG;    // ric_batch_hybrid_config first
 	if (n == 0) return RIC_OK;
+	if (!outputs_distinct(out, n))
+		return set_last_error("ric_batch_roundtrip_hybrid: out[] buffers must be distinct"), RIC_E_ARG;
 	if (set_dev(b->device)) return RIC_E_HIP;
 	auto& c = b->cp;
 	Pyramid& P = b->P;

@@ -756,12 +756,32 @@ int ric_band_write(ric_wavelet* w, int index, const int32_t* in)
 
 int ric_mux_create_encoder(ric_mux** out, uint8_t* buf, size_t cap, uint16_t first_word)
 {
-	if (!out || !buf) return RIC_E_ARG;
+	if (!out) return RIC_E_ARG;
 	ric_mux* m = new ric_mux;
 	m->encoder = true;
 	m->buf = buf;
-	m->m.init_encoder(buf, cap, first_word);
+	// CMuxCodec(0, 0) (src/lib/rududucodec.cpp:36): no buffer until initCoder;
+	// coding before that is flagged (capacity 0) instead of writing anywhere
+	m->m.init_encoder(buf, buf ? cap : 0, first_word);
 	*out = m;
+	return RIC_OK;
+}
+
+int ric_mux_reinit_encoder(ric_mux* m, uint8_t* buf, size_t cap, uint16_t first_word)
+{
+	if (!m) return RIC_E_ARG;
+	m->encoder = true;
+	if (buf) m->buf = buf;
+	m->m.reinit_encoder(buf, cap, first_word);
+	return RIC_OK;
+}
+
+int ric_mux_reinit_decoder(ric_mux* m, const uint8_t* buf, size_t len)
+{
+	if (!m || (buf && len != 0 && len < 4)) return RIC_E_ARG;
+	m->encoder = false;
+	if (buf) m->buf = const_cast<uint8_t*>(buf);
+	m->m.reinit_decoder(buf, len);
 	return RIC_OK;
 }
 
@@ -788,6 +808,7 @@ int ric_mux_create_decoder_inplace(ric_mux** out, const uint8_t* buf)
 int ric_mux_end(ric_mux* m, size_t* len_out)
 {
 	if (!m || !m->encoder) return RIC_E_ARG;
+	if (!m->buf) return RIC_E_ARG;                 // CMuxCodec(0, 0) never given a buffer
 	uint8_t* e = m->m.end_coding();
 	if (len_out) *len_out = (size_t)(e - m->buf);
 	return m->m.overflow() ? RIC_E_CAPACITY : RIC_OK;

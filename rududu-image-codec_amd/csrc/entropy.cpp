@@ -77,10 +77,19 @@ constexpr size_t kDecPad = 1 << 16;
 }  // namespace
 
 // ================================================================= Mux
+namespace {
+// buf + cap, saturated at the top of the address space (cap SIZE_MAX: no bound)
+uint8_t* bound_of(uint8_t* buf, size_t cap)
+{
+	const uintptr_t b = (uintptr_t)buf;
+	return (uint8_t*)(cap > UINTPTR_MAX - b ? UINTPTR_MAX : b + cap);
+}
+}  // namespace
+
 void Mux::init_encoder(uint8_t* buf, size_t cap, uint16_t first_word)
 {
 	base_ = buf;
-	limit_ = buf + cap;
+	limit_ = bound_of(buf, cap);
 	low_ = (uint32_t)first_word << 16;
 	range_ = 1u << 16;
 	outcount_ = 0; nbits_ = 0; buffer_ = 0; reserved_ = nullptr; overflow_ = cap < 4;
@@ -137,6 +146,30 @@ void Mux::init_decoder_inplace(const uint8_t* buf)
 	init_ = base_ + 2; p_ = base_ + 2;
 	code_ = low_ = ((uint32_t)p_[0] << 8) | p_[1];
 	p_ += 2;
+}
+
+void Mux::reinit_encoder(uint8_t* buf, size_t cap, uint16_t first_word)
+{
+	if (buf) {
+		init_encoder(buf, cap, first_word);
+		return;
+	}
+	// no buffer: the state only (muxcodec.cpp:38-42), the output continues
+	low_ = (uint32_t)first_word << 16;
+	range_ = 1u << 16;
+	outcount_ = 0; nbits_ = 0; reserved_ = nullptr;
+	ebuf_ = 0; ebits_ = 0;
+}
+
+void Mux::reinit_decoder(const uint8_t* buf, size_t len)
+{
+	if (!buf) {                           // muxcodec.cpp:53-54
+		range_ = 1u << 16;
+		nbits_ = 0;
+		return;
+	}
+	if (len == 0) init_decoder_inplace(buf);
+	else init_decoder(buf, len);
 }
 
 Mux::~Mux() { free(owned_); }

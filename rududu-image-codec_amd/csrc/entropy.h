@@ -30,6 +30,16 @@ public:
 	// CMuxCodec(pStream), src/lib/muxcodec.cpp:31-34, 51-61): the caller's
 	// buffer must outlive it and hold the stream
 	void init_decoder_inplace(const uint8_t* buf);
+	// CMuxCodec::initCoder(firstWord, pStream) (src/lib/muxcodec.cpp:36-49):
+	// resets the coder state; a non-null buf also restarts the output there
+	// (cap bytes; SIZE_MAX: no bound, like the reference), a null buf keeps
+	// the current output position, as the reference does.
+	void reinit_encoder(uint8_t* buf, size_t cap, uint16_t first_word);
+	// CMuxCodec::initDecoder(pStream) (src/lib/muxcodec.cpp:51-61): resets the
+	// range and bit buffer; a non-null buf restarts the input there (len bytes
+	// copied with zero padding; len 0: read in place with no end, like the
+	// reference), a null buf keeps the read position.
+	void reinit_decoder(const uint8_t* buf, size_t len);
 	Mux() = default;
 	Mux(const Mux&) = delete;
 	Mux& operator=(const Mux&) = delete;

@@ -1129,7 +1129,7 @@ __global__ void __launch_bounds__(64) k_gc_decode(const GDecArgs* __restrict__ a
 	// status in bits 0-3; on a staging overrun, the read position (diagnostic)
 	if (a.dbg && f == 0) {                           // every band, the host harness's order (finest first, D H V, LL)
 		__threadfence();
-		size_t o = 2048;
+		size_t o = (size_t)gridDim.x * 2048;         // after every frame's 2048-word slot block
 		for (int k = 0; k <= a.nb; k++) {
 			// a.b is coarse -> fine V, H, D: band i of the harness order
 			const int lev = k / 3, ori = k % 3;          // harness: level lev, orientation D=0, H=1, V=2

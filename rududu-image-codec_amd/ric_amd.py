@@ -64,6 +64,8 @@ def lib():
         "ric_band_write": (_I, [_P, _I, _P]),
         "ric_band_host": (_I, [_P, _I, ctypes.POINTER(_P), ctypes.POINTER(_I)]),
         "ric_mux_create_decoder_inplace": (_I, [ctypes.POINTER(_P), _P]),
+        "ric_mux_reinit_encoder": (_I, [_P, _P, _S, ctypes.c_uint16]),
+        "ric_mux_reinit_decoder": (_I, [_P, _P, _S]),
         "ric_mux_create_encoder": (_I, [ctypes.POINTER(_P), _P, _S, ctypes.c_uint16]),
         "ric_mux_create_decoder": (_I, [ctypes.POINTER(_P), _P, _S]),
         "ric_mux_end": (_I, [_P, ctypes.POINTER(_S)]),
@@ -164,14 +166,31 @@ class MuxCodec:
     def __init__(self, buf, first_word=None, length=None):
         self._buf = buf
         h = _P()
-        if first_word is not None:       # encoder: CMuxCodec(pStream, firstWord)
-            _chk(lib().ric_mux_create_encoder(ctypes.byref(h), _ptr(buf), buf.nbytes, first_word), "CMuxCodec(enc)")
+        if first_word is not None:       # encoder: CMuxCodec(pStream, firstWord); buf None: CMuxCodec(0, 0)
+            _chk(lib().ric_mux_create_encoder(ctypes.byref(h), _ptr(buf), buf.nbytes if buf is not None else 0,
+                                              first_word), "CMuxCodec(enc)")
             self.encoder = True
         else:                            # decoder: CMuxCodec(pStream)
             n = buf.nbytes if length is None else length
             _chk(lib().ric_mux_create_decoder(ctypes.byref(h), _ptr(buf), n), "CMuxCodec(dec)")
             self.encoder = False
         self.h = h
+
+    def initCoder(self, first_word, buf):
+        """CMuxCodec::initCoder (src/lib/muxcodec.h:104); buf None keeps the output position."""
+        if buf is not None:
+            self._buf = buf
+        _chk(lib().ric_mux_reinit_encoder(self.h, _ptr(buf), buf.nbytes if buf is not None else 0, first_word),
+             "initCoder")
+        self.encoder = True
+
+    def initDecoder(self, buf, length=None):
+        """CMuxCodec::initDecoder (src/lib/muxcodec.h:105), bounded to `length` bytes of buf (all of it by default)."""
+        if buf is not None:
+            self._buf = buf
+        n = 0 if buf is None else (buf.nbytes if length is None else length)
+        _chk(lib().ric_mux_reinit_decoder(self.h, _ptr(buf), n), "initDecoder")
+        self.encoder = False
 
     def endCoding(self):
         n = _S()
@@ -363,17 +382,19 @@ class Batch:
             _chk(rc, "ric_batch_decode")
         return rc
 
-    def roundtrip(self, frames, pix_out, q=9, trans=0):
+    def roundtrip(self, frames, pix_out, q=9, trans=0, allow_stream_err=False):
         """Encode then decode every frame (device pixels in and out), groups
         pipelined; returns the .ric files' sizes and keeps the files in
-        self.streams(n)."""
+        self.streams(n).  RIC_E_STREAM (a decoder ran past its stream: only
+        the reference's own desynchronising geometries do that)
+        raises unless allow_stream_err."""
         n = len(frames)
         outs = self._out_bufs(n)
         caps = (ctypes.c_size_t * n)(*([self.cap] * n))
         lens = (ctypes.c_size_t * n)()
         self._streams = None
         rc = lib().ric_batch_roundtrip(self.h, _ptrs(frames), n, q, trans, _ptrs(outs), caps, lens, _ptrs(pix_out))
-        if rc not in (RIC_OK, RIC_E_STREAM):
+        if rc != RIC_OK and not (allow_stream_err and rc == RIC_E_STREAM):
             _chk(rc, "ric_batch_roundtrip")
         self._lens = [lens[i] for i in range(n)]
         return self._lens
@@ -388,11 +409,14 @@ class Batch:
         _chk(lib().ric_batch_hybrid_times(self.h, ctypes.byref(hm), ctypes.byref(gm)), "ric_batch_hybrid_times")
         return hm.value, gm.value
 
-    def roundtrip_hybrid(self, frames, pix_out, n_host, q=9, trans=0, gpu_decode=False, streams=None):
+    def roundtrip_hybrid(self, frames, pix_out, n_host, q=9, trans=0, gpu_decode=False, streams=None,
+                         allow_stream_err=False):
         """ric_batch_roundtrip_hybrid: frames[:n_host] round trips on the host,
         the rest encoded by the GPU stream coder and decoded by the GPU stream
         decoder (gpu_decode 1), on the host (0), or per launch by whichever
-        has room (2)."""
+        has room (2).  `streams`: one host buffer per frame (distinct: the
+        library rejects aliased ones).  RIC_E_STREAM raises unless
+        allow_stream_err."""
         n = len(frames)
         outs = streams if streams is not None else self._out_bufs(n)   # host buffers of the .ric files
         caps = (ctypes.c_size_t * n)(*[o.size for o in outs])
@@ -400,7 +424,7 @@ class Batch:
         self._streams = outs
         rc = lib().ric_batch_roundtrip_hybrid(self.h, _ptrs(frames), n, n_host, int(gpu_decode), q, trans, _ptrs(outs),
                                               caps, lens, _ptrs(pix_out))
-        if rc not in (RIC_OK, RIC_E_STREAM):
+        if rc != RIC_OK and not (allow_stream_err and rc == RIC_E_STREAM):
             _chk(rc, "ric_batch_roundtrip_hybrid")
         self._lens = [lens[i] for i in range(n)]
         return self._lens

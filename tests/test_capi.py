@@ -66,6 +66,28 @@ def test_mux_capacity_is_explicit():
     assert m.endCoding() <= 8
 
 
+def test_mux_reinit():
+    """CMuxCodec(0, 0) + initCoder / initDecoder (src/lib/muxcodec.h:102-105,
+    src/lib/rududucodec.cpp:36,89,123): one object, re-initialised per frame,
+    serving as encoder and decoder."""
+    m = ric_amd.MuxCodec(None, first_word=0)          # CMuxCodec(0, 0): no buffer yet
+    with pytest.raises(ric_amd.RicError):
+        m.endCoding()                                  # nothing to end into
+    outs = []
+    for k in range(3):
+        buf = np.full(64, 0xAA, np.uint8)
+        m.initCoder(0, buf)
+        assert m.getSize() == 2                        # pStream - pInitStream after initCoder
+        n = m.endCoding()
+        assert n == 4 and m.getSize() == 2                # the 4 final bytes land in the ring slots buf[0..3]
+        outs.append(buf[:n].tobytes())
+    assert outs[0] == outs[1] == outs[2]               # the state is fully reset per frame
+    m.initDecoder(np.frombuffer(outs[0], np.uint8).copy())
+    assert not m.encoder and m.getSize() == 2
+    m.initCoder(0, np.zeros(64, np.uint8))             # and back to an encoder
+    assert m.encoder
+
+
 def test_shim_compat_builds():
     """A caller in the reference's own call forms (CMuxCodec(pStream, 0),
     CMuxCodec(pStream), DBand/pLow members, (C*) pBand) compiles and links

@@ -146,3 +146,18 @@ def test_gpu_roundtrip_large_sha(ric, name):
     pix = torch.zeros((1, h, w), dtype=torch.uint8, device="cuda")
     b.decompress_gpu(out, ostride, lens, [pix])
     assert hashlib.sha256(pix.cpu().numpy().tobytes()).hexdigest() == e["decoded_sha256"]
+
+
+def test_gpu_encoder_rejects_unaligned_capacity(ric):
+    """The stream coder stores 16-byte chunks: a capacity or stride that is not
+    a multiple of 16 would drop a stream's tail unflagged, so it is refused."""
+    import ctypes
+    import torch
+    w, h = 64, 48
+    frame = torch.from_numpy(ric.synth(w, h, 1, 1)).cuda()
+    b = ric.Batch(w, h, 1, slots=1, threads=1)
+    out = torch.zeros(65536, dtype=torch.uint8, device="cuda")
+    lens = (ctypes.c_size_t * 1)()
+    for ostride, cap in ((8192, 8190), (8200, 8192), (8192, 8192)):
+        rc = ric.lib().ric_batch_encode_gpu(b.h, ric._ptrs([frame]), 1, 9, 0, out.data_ptr(), ostride, cap, lens)
+        assert rc == (ric.RIC_OK if (cap, ostride) == (8192, 8192) else ric.RIC_E_ARG), (ostride, cap)

@@ -1,0 +1,84 @@
+"""The reference video codec's coding loop (src/lib/rududucodec.cpp) on the GPU
+against the reference library itself (oracle/_ref, compiled from
+/root/reference/src/lib by oracle/Makefile).
+
+test_video_intra_*: tests/native/video_intra.cpp, ONE source built on the GPU
+drop-in (include/rududu_gpu.hpp) and against the reference's headers: the
+CMuxCodec(0, 0) + initCoder / initDecoder per frame, CWavelet2D(w, h, 3),
+Transform -> CodeBand -> TSUQi -> TransformI on CImage-style bordered planes
+with the video quants() table.  Streams and planes must be byte-identical."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+SHIM_BIN = os.path.join(HERE, "native", "video_intra")
+REF_BIN = os.path.join(REPO, "oracle", "_ref", "video_intra_ref")
+
+
+def _planes(w, h, n, seed):
+    """n frames of 3 int16 planes in the video codec's scale (Y << 4, Co/Cg << 3:
+    src/lib/image.cpp:113-117) from the synthetic generator, shifted per frame."""
+    import ric_amd
+    out = []
+    for f in range(n):
+        rgb = ric_amd.synth(w + 16, h + 16, 3, seed + f // 4)[:, (3 * f) % 16:(3 * f) % 16 + h, (5 * f) % 16:(5 * f) % 16 + w]
+        r, g, b = (rgb[i].astype(np.int32) for i in range(3))
+        co = r - b
+        y = b + (co >> 1)
+        cg = g - y
+        y = y + (cg >> 1) - 128
+        out += [(y << 4).astype(np.int16), (co << 3).astype(np.int16), (cg << 3).astype(np.int16)]
+    return np.stack(out)
+
+
+def _run(binary, w, h, q, n, planes, tmp):
+    src = os.path.join(tmp, "in.i16")
+    dst = os.path.join(tmp, os.path.basename(binary) + ".bin")
+    planes.astype(np.int16).tofile(src)
+    subprocess.run([binary, str(w), str(h), str(q), str(n), src, dst], check=True, timeout=120)
+    return open(dst, "rb").read()
+
+
+def _frames(blob, w, h, n):
+    """split video_intra's output into per-frame (stream, enc planes, dec planes, dec size)"""
+    out, o = [], 0
+    npl = 3 * w * h * 2
+    for _ in range(n):
+        size = int(np.frombuffer(blob, np.uint32, 1, o)[0])
+        o += 4
+        s = blob[o:o + size + 2]
+        o += size + 2
+        e = np.frombuffer(blob, np.int16, 3 * w * h, o).reshape(3, h, w)
+        o += npl
+        d = np.frombuffer(blob, np.int16, 3 * w * h, o).reshape(3, h, w)
+        o += npl
+        ds = int(np.frombuffer(blob, np.uint32, 1, o)[0])
+        o += 4
+        out.append((s, e, d, ds))
+    assert o == len(blob)
+    return out
+
+
+# q is CRududuCodec::quant: quants(q + 20) is the quantiser, so q down to -19
+# (quants(1) = 32) gives dense streams; testmotion.cpp uses 20 (quants(40) = 7132)
+@pytest.mark.parametrize("w,h,q,n", [(128, 96, -10, 3), (160, 120, -19, 2), (200, 72, 0, 2), (97, 61, -5, 2),
+                                     (352, 288, -15, 3), (64, 48, 20, 2)])
+def test_video_intra_matches_reference(ric, tmp_path, w, h, q, n):
+    if not os.path.exists(REF_BIN):
+        pytest.fail("oracle/_ref/video_intra_ref not built (make -C oracle with /root/reference present)")
+    planes = _planes(w, h, n, 300 + w)
+    got = _run(SHIM_BIN, w, h, q, n, planes, str(tmp_path))
+    want = _run(REF_BIN, w, h, q, n, planes, str(tmp_path))
+    gf, wf = _frames(got, w, h, n), _frames(want, w, h, n)
+    for k, (g, e) in enumerate(zip(gf, wf)):
+        assert g[0] == e[0], "frame %d stream" % k
+        assert np.array_equal(g[1], e[1]), "frame %d encoder reconstruction" % k
+        assert np.array_equal(g[2], e[2]), "frame %d decoder planes" % k
+        assert g[3] == e[3], "frame %d decoder getSize" % k
+    assert got == want
