@@ -271,6 +271,52 @@ uint32_t Mux::huff_decode(int high, int idx)
 	return sym;
 }
 
+uint32_t Mux::huff_decode_table(const HuffSym* t)
+{
+	const uint32_t code = (((buffer_ << 16) | ((uint32_t)p_[0] << 8) | p_[1]) >> nbits_) & 0xFFFF;
+	while (code < t->code) t++;                    // the last entry's code is 0
+	if (t->len > 16) { overflow_ = true; return 0; }   // a code the reference cannot read either
+	p_ -= (int)(nbits_ - t->len) >> 3;
+	if (p_ > limit_) { p_ = limit_; overflow_ = true; }
+	if (nbits_ < t->len) buffer_ = p_[-1];
+	nbits_ = (nbits_ - t->len) & 7;
+	return (t->value - (code >> (16 - t->len))) & 0xFF;
+}
+
+void Mux::golomb_lin_code(uint32_t nb, int k, int m)
+{
+	uint32_t l = 1;
+	while (nb >= (1u << (k + m))) {
+		l += 1u << m;
+		nb -= 1u << (k + m);
+		k++;
+	}
+	l += nb >> k;
+	nb &= (1u << k) - 1;
+	// l - 1 zeros then a one (the reference shifts them through its 32-bit
+	// buffer in pieces, muxcodec.cpp:479-490: only the bit order matters)
+	while (l > 32) { bits_code(0, 32); l -= 32; }
+	bits_code(1, l);
+	bits_code(nb, k);
+}
+
+uint32_t Mux::golomb_lin_decode(int k, int m)
+{
+	uint32_t l = 0;
+	// the zero run, one bit at a time: a byte is read exactly when the bit
+	// buffer runs dry, as in the reference's scan (muxcodec.cpp:499-506)
+	for (;;) {
+		if (bits_decode(1)) break;
+		if (++l > (1u << 20)) { overflow_ = true; return 0; }   // no valid stream has such a run
+	}
+	uint32_t nb = ((1u << (l >> m)) - 1) << k;
+	k += l >> m;
+	l &= (1u << m) - 1;
+	if (k > 24) { overflow_ = true; return 0; }
+	nb += (l << k) | bits_decode(k);
+	return nb;
+}
+
 void Mux::taboo_code(uint32_t nb)
 {
 	const uint32_t nt = 2;
@@ -770,6 +816,216 @@ void tree_dispatch(Mux& m, const BandView& b, const BandView& par, bool high, bo
 }
 
 }  // namespace
+
+// ====================================================== video motion vectors
+namespace {
+
+// CHuffCodec (src/lib/huffcodec.{h,cpp}) as the video codec builds it, with
+// no initial table (pInitTable 0): adaptive canonical Huffman over n symbols,
+// every symbol starting at frequency 8; the code is rebuilt when the
+// accumulated count reaches UPDATE_THRES, frequencies halving each time.
+// glibc's qsort (2.35) is a stable merge sort here; std::stable_sort matches it.
+class AdaptiveHuff {
+public:
+	AdaptiveHuff(bool enc, unsigned n) : enc_(enc), n_(n)
+	{
+		for (unsigned i = 0; i < n; i++) freq_[i] = 8;
+		update_code();
+	}
+	void code(Mux& m, unsigned sym)                     // huffcodec.h:80-87
+	{
+		if (count_ >= kThres) update_code();
+		m.bits_code(sym_[sym].code, sym_[sym].len);
+		freq_[sym] = (uint16_t)(freq_[sym] + step_);
+		count_ += step_;
+	}
+	unsigned decode(Mux& m)                             // huffcodec.h:89-97
+	{
+		if (count_ >= kThres) update_code();
+		const unsigned sym = lut_[m.huff_decode_table(sym_)];
+		freq_[sym] = (uint16_t)(freq_[sym] + step_);
+		count_ += step_;
+		return sym;
+	}
+
+private:
+	static constexpr unsigned kStepMin = 128, kStepMax = 2048, kThres = 1u << 14;   // huffcodec.h:32-34
+	bool enc_;
+	unsigned n_, count_ = 0, step_ = kStepMax;
+	uint16_t freq_[256];
+	HuffSym sym_[256];
+	uint8_t lut_[256];
+
+	// make_len (huffcodec.cpp:83-125): Moffat-Katajainen in place, weights in .code
+	static void make_len(HuffSym* s, int n)
+	{
+		int root = n - 1, leaf = n - 3, next, nodes_left, nb_nodes, depth;
+		s[n - 1].code = (uint16_t)(s[n - 1].code + s[n - 2].code);
+		for (int i = n - 2; i > 0; i--) {
+			if (leaf < 0 || s[root].code < s[leaf].code) {
+				s[i].code = s[root].code;
+				s[root--].code = (uint16_t)i;
+			} else
+				s[i].code = s[leaf--].code;
+			if (leaf < 0 || (root > i && s[root].code < s[leaf].code)) {
+				s[i].code = (uint16_t)(s[i].code + s[root].code);
+				s[root--].code = (uint16_t)i;
+			} else
+				s[i].code = (uint16_t)(s[i].code + s[leaf--].code);
+		}
+		s[1].code = 0;
+		for (int i = 2; i < n; i++) s[i].code = (uint16_t)(s[s[i].code].code + 1);
+		nodes_left = 1;
+		nb_nodes = depth = 0;
+		root = 1;
+		next = 0;
+		while (nodes_left > 0) {
+			while (root < n && s[root].code == depth) { nb_nodes++; root++; }
+			while (nodes_left > nb_nodes) { s[next++].len = (uint8_t)depth; nodes_left--; }
+			nodes_left = 2 * nb_nodes;
+			depth++;
+			nb_nodes = 0;
+		}
+	}
+	// make_codes (huffcodec.cpp:149-160): canonical codes, longest (last) = 0
+	static void make_codes(HuffSym* s, int n)
+	{
+		unsigned bits = s[n - 1].len, code = 0;
+		s[n - 1].code = 0;
+		for (int i = n - 2; i >= 0; i--) {
+			code >>= bits - s[i].len;
+			bits = s[i].len;
+			code++;
+			s[i].code = (uint16_t)code;
+		}
+	}
+	// enc2dec (huffcodec.cpp:191-211): one entry per length + the symbol LUT
+	static void enc2dec(const HuffSym* s, HuffSym* out, uint8_t* lut, int n)
+	{
+		unsigned bits = s[0].len, cnt = 0;
+		for (int i = 1; i < n; i++) {
+			if (s[i].len != bits) {
+				bits = s[i].len;
+				out[cnt].code = (uint16_t)(s[i - 1].code << (16 - s[i - 1].len));
+				out[cnt].len = s[i - 1].len;
+				out[cnt++].value = (uint8_t)(s[i - 1].code + i - 1);
+			}
+		}
+		out[cnt].code = (uint16_t)(s[n - 1].code << (16 - s[n - 1].len));
+		out[cnt].len = s[n - 1].len;
+		out[cnt++].value = (uint8_t)(s[n - 1].code + n - 1);
+		for (int i = 0; i < n; i++) lut[i] = s[i].value;
+	}
+	// update_code (huffcodec.cpp:213-236)
+	void update_code()
+	{
+		HuffSym s[256];
+		for (unsigned i = 0; i < n_; i++) {
+			s[i].code = freq_[i];
+			s[i].value = (uint8_t)i;
+			s[i].len = 0;
+			freq_[i] = (uint16_t)((freq_[i] + 1) >> 1);
+		}
+		std::stable_sort(s, s + n_, [](const HuffSym& a, const HuffSym& b) { return a.code > b.code; });   // comp_freq
+		make_len(s, (int)n_);
+		make_codes(s, (int)n_);
+		if (enc_) {
+			std::stable_sort(s, s + n_, [](const HuffSym& a, const HuffSym& b) { return a.value < b.value; });  // comp_sym
+			memcpy(sym_, s, sizeof(HuffSym) * n_);
+		} else {
+			enc2dec(s, sym_, lut_, (int)n_);
+		}
+		count_ = 0;
+		step_ >>= 1;
+		step_ = std::max(step_, kStepMin);
+	}
+};
+
+constexpr uint32_t kMvIntra = 0x80008000u;           // MV_INTRA, obmc.h:37
+
+inline int mv_x(uint32_t v) { return (int16_t)(v & 0xFFFF); }
+inline int mv_y(uint32_t v) { return (int16_t)(v >> 16); }
+inline uint32_t mv_make(int x, int y) { return (uint32_t)(uint16_t)x | ((uint32_t)(uint16_t)y << 16); }
+// median (src/lib/utils.h:64-77) on short
+inline int med3(int a, int b, int c)
+{
+	if (b < a) std::swap(a, b);
+	if (c <= a) return a;
+	if (c <= b) return c;
+	return b;
+}
+
+// the MV predictor of block (i, j) (obmc.cpp:358-367): the left vector on the
+// first row, the one above on the first and last columns, else the median of
+// left, above, above-right (ILP32 indexing: pCurMV[i - dimX] is the row above)
+inline uint32_t mv_pred(const uint32_t* row, int i, int j, int dimx)
+{
+	if (j == 0) return i != 0 ? row[i - 1] : 0u;
+	if (i == 0 || i == dimx - 1) return row[i - dimx];
+	const uint32_t l = row[i - 1], u = row[i - dimx], ur = row[i - dimx + 1];
+	return mv_make(med3(mv_x(l), mv_x(u), mv_x(ur)), med3(mv_y(l), mv_y(u), mv_y(ur)));
+}
+
+}  // namespace
+
+void mv_encode(Mux& m, const uint32_t* mv, int dimx, int dimy)
+{
+	BitModel intra, zero;                             // CBitCodec intraCodec, zeroCodec (obmc.cpp:347)
+	intra.init();
+	zero.init();
+	AdaptiveHuff huff_x(true, 128), huff_y(true, 128), huff(true, 255);
+	for (int j = 0; j < dimy; j++) {
+		const uint32_t* row = mv + (size_t)j * dimx;
+		for (int i = 0; i < dimx; i++) {
+			if (row[i] == kMvIntra) { intra.code(m, 1, 0); continue; }
+			intra.code(m, 0, 0);
+			const uint32_t p = mv_pred(row, i, j, dimx);
+			if (mv_x(row[i]) == mv_x(p) && mv_y(row[i]) == mv_y(p)) { zero.code(m, 0, 0); continue; }
+			zero.code(m, 1, 0);
+			const int x = s2u(mv_x(row[i]) - mv_x(p)), y = s2u(mv_y(row[i]) - mv_y(p));
+			huff.code(m, (unsigned)((std::min(x, 15) | (std::min(y, 15) << 4)) - 1));
+			if (x >= 15) {
+				huff_x.code(m, (unsigned)std::min(x - 15, 127));
+				if (x >= 127 + 15) m.golomb_lin_code((uint32_t)(x - 127 - 15), 5, 0);
+			}
+			if (y >= 15) {
+				huff_y.code(m, (unsigned)std::min(y - 15, 127));
+				if (y >= 127 + 15) m.golomb_lin_code((uint32_t)(y - 127 - 15), 5, 0);
+			}
+		}
+	}
+}
+
+void mv_decode(Mux& m, uint32_t* mv, int dimx, int dimy)
+{
+	BitModel intra, zero;
+	intra.init();
+	zero.init();
+	AdaptiveHuff huff_x(false, 128), huff_y(false, 128), huff(false, 255);
+	for (int j = 0; j < dimy; j++) {
+		uint32_t* row = mv + (size_t)j * dimx;
+		for (int i = 0; i < dimx; i++) {
+			if (intra.decode(m, 0)) { row[i] = kMvIntra; continue; }
+			const uint32_t p = mv_pred(row, i, j, dimx);
+			if (zero.decode(m, 0)) {
+				const int tmp = (int)huff.decode(m) + 1;
+				int x = tmp & 0xF, y = tmp >> 4;
+				if (x == 15) {
+					x += (int)huff_x.decode(m);
+					if (x == 127 + 15) x += (int)m.golomb_lin_decode(5, 0);
+				}
+				const int nx = u2s(x) + mv_x(p);
+				if (y == 15) {
+					y += (int)huff_y.decode(m);
+					if (y == 127 + 15) y += (int)m.golomb_lin_decode(5, 0);
+				}
+				row[i] = mv_make(nx, u2s(y) + mv_y(p));
+			} else {
+				row[i] = p;
+			}
+		}
+	}
+}
 
 void pred_encode(Mux& m, const BandView& b)
 {

@@ -15,6 +15,13 @@
 
 namespace ric {
 
+// sHuffSym (src/lib/muxcodec.h:42-46): a Huffman table entry
+struct HuffSym {
+	uint16_t code;
+	uint8_t len;
+	uint8_t value;
+};
+
 // ------------------------------------------------------------------ mux
 class Mux {
 public:
@@ -84,6 +91,11 @@ public:
 	}
 	// canonical-table Huffman decode (huffDecode, muxcodec.h:241-276)
 	uint32_t huff_decode(int table_is_high, int idx);
+	// huffDecode(const sHuffSym*) (muxcodec.h:242-253): one entry per code
+	// length, codes left-aligned to 16 bits, longest last (code 0)
+	uint32_t huff_decode_table(const HuffSym* table);
+	void golomb_lin_code(uint32_t nb, int k, int m);          // muxcodec.cpp:466-493
+	uint32_t golomb_lin_decode(int k, int m);                 // muxcodec.cpp:495-514
 
 	void taboo_code(uint32_t nb);           // muxcodec.cpp:210-240 (n = 2)
 	uint32_t taboo_decode();                // muxcodec.cpp:242-280
@@ -182,6 +194,11 @@ void tree_encode_state(const BandView& b, const BandView& par, bool has_child);
 // Register-resident decoder of one band (decoder.cpp), same semantics as
 // tree_decode.
 void tree_decode_fast(Mux& m, const BandView& b, const BandView& par, bool high, bool has_child);
+// The video codec's motion-vector field (COBMC::encode / decode,
+// src/lib/obmc.cpp:344-440): dimx x dimy vectors, x in the low 16 bits, y in
+// the high 16 (sMotionVector, obmc.h:29-35), MV_INTRA = 0x80008000.
+void mv_encode(Mux& m, const uint32_t* mv, int dimx, int dimy);
+void mv_decode(Mux& m, uint32_t* mv, int dimx, int dimy);
 // Encoder over GPU block records (symbols.h), coder state in registers
 // (encoder.cpp): rec / pin in raster block order; pin == nullptr for a band
 // without a parent (the coarsest level).

@@ -209,4 +209,25 @@ long hc_decode_states(const uint8_t* ric, long len, int w, int h, uint32_t* st_o
 	}
 	return k;
 }
+
+// the video codec's motion-vector coder (COBMC::decode, obmc.cpp:393-440) on
+// a stream (payload at buf + 2): the vectors it decodes first; returns the
+// decoder's read position (bytes from buf + 2)
+long hc_mv_decode(const uint8_t* buf, long len, int dimx, int dimy, uint32_t* mv)
+{
+	Mux m;
+	m.init_decoder(buf, (size_t)len);
+	mv_decode(m, mv, dimx, dimy);
+	return (long)m.size();
+}
+// COBMC::encode (obmc.cpp:344-391) alone into a fresh coder (firstWord 0),
+// then endCoding: the bytes written (from out)
+long hc_mv_encode(const uint32_t* mv, int dimx, int dimy, uint8_t* out, long cap)
+{
+	Mux m;
+	m.init_encoder(out, (size_t)cap, 0);
+	mv_encode(m, mv, dimx, dimy);
+	uint8_t* e = m.end_coding();
+	return m.overflow() ? -1 : (long)(e - out);
+}
 }
