@@ -244,6 +244,49 @@ int ric_batch_diag_gpu(ric_batch* b, const uint8_t* const* pix, int n, int q, in
 int ric_batch_prof_enable(ric_batch* b, int on);
 int ric_batch_prof_read(ric_batch* b, double* ms, long* frames, long* launches, int n);
 
+/* ----------------------------------------------------------- ric_video */
+/* The reference video codec, CRududuCodec (src/lib/rududucodec.{h,cpp}):
+ * key frames every 10 frames, the others predicted by EPZS motion search
+ * (COBME, src/lib/obme.cpp) and OBMC (COBMC, src/lib/obmc.cpp) from the
+ * previous reconstruction at quarter pel (CImageBuffer::calc_sub), the
+ * residual through a 3-level 9/7 wavelet closed loop, motion vectors and
+ * bands in one CMuxCodec stream per frame.  Frames stay in HBM; the search,
+ * interpolation, OBMC and wavelet stages are HIP kernels, the two serial
+ * coders run on the host.  One change from the reference: TransformI gets
+ * each plane's end pointer (rududucodec.cpp:74,83 pass the start, which
+ * writes outside the image: DESIGN.md §9). */
+typedef struct ric_video ric_video;
+/* CRududuCodec(cmode mode, int width, int height, int component)
+ * (src/lib/rududucodec.h:35, rududucodec.cpp:32-48); encoder 1 = encode,
+ * 0 = decode; component must be 3 (CImage::inputSGI writes Y, Co, Cg). */
+int ric_video_create(ric_video** out, int encoder, int w, int h, int component, int device);
+/* CRududuCodec::~CRududuCodec (rududucodec.cpp:51-56) */
+void ric_video_destroy(ric_video* v);
+/* the public member CRududuCodec::quant (rududucodec.h:33): the quantiser is
+ * quants(quant + 20), the RD lambda quants(quant + 12) (rududucodec.cpp:58-71);
+ * -12 <= quant <= 30 (the table's defined range) */
+int ric_video_set_quant(ric_video* v, int quant);
+/* CRududuCodec::encode(unsigned char* pImage, int stride, unsigned char*
+ * pBuffer, CImage** outImage) (rududucodec.cpp:87-119).  pix: 3 planes R, G,
+ * B of h rows x stride bytes, bottom row first (CImage::inputSGI), on the host
+ * or the device (pix_on_device).  The stream goes to the host buffer buf (cap
+ * bytes; the reference has no bound); *size = the reference's return value,
+ * endCoding() - pBuffer - 2 (the stream is *size + 2 bytes). */
+int ric_video_encode(ric_video* v, const uint8_t* pix, int stride, int pix_on_device, uint8_t* buf, size_t cap,
+                     int* size);
+/* CRududuCodec::decode(unsigned char* pBuffer, CImage** outImage)
+ * (rududucodec.cpp:121-141): buf holds the len bytes of one frame's stream;
+ * *size = codec.getSize().  RIC_E_STREAM when the decoder ran past len. */
+int ric_video_decode(ric_video* v, const uint8_t* buf, size_t len, int* size);
+/* *outImage of the last encode / decode: its planes Y, Co, Cg as int16,
+ * 3 x h x w (border 0), or with the 15-sample border, 3 x (h + 30) x (w + 30)
+ * (border 1), to host or device memory (on_device). */
+int ric_video_output(ric_video* v, int16_t* planes, int border, int on_device);
+/* the motion field after the last encode / decode: (w >> 3) x (h >> 3)
+ * vectors in quarter pel, x in the low 16 bits, y in the high 16, MV_INTRA =
+ * 0x80008000 (COBMC::pMV, obmc.h:29-57) */
+int ric_video_motion(ric_video* v, uint32_t* mv);
+
 /* .ric header fields (src/ric/ric.cpp:114-121, 187-200) */
 int ric_read_header(const uint8_t* ric, size_t len, int* w, int* h, int* channels, int* q, int* trans);
 /* src/ric/ric.cpp:42-49 */

@@ -16,6 +16,7 @@
 #include "ric_image.h"
 #include "entropy.h"
 #include "codec_params.h"
+#include "wavelet_api.h"
 
 using namespace ric;
 
@@ -475,6 +476,45 @@ int ensure_img(ric_wavelet* w)
 }
 
 }  // namespace
+
+namespace ric {
+namespace wapi {
+
+hipStream_t stream(ric_wavelet* w) { return w->st; }
+
+int encode_plane(ric_wavelet* w, Mux& m, int16_t* plane, long stride, int trans, int quant, int lambda, int dq)
+{
+	if (set_dev(w->device)) return RIC_E_HIP;
+	w->pend = false;
+	int rc = encode_gpu(w, plane, stride, trans, quant, lambda);     // Transform + buildTree + records
+	if (!rc) rc = code_band_host(w, m, true, true);                 // CodeBand's serial half + its band state
+	if (!rc && m.overflow()) rc = RIC_E_CAPACITY;
+	if (!rc) rc = tsuqi(w, dq);
+	if (!rc) rc = inverse(w, plane, stride, trans);
+	return rc;
+}
+
+int decode_plane(ric_wavelet* w, Mux& m, int16_t* plane, long stride, int trans, int dq)
+{
+	if (set_dev(w->device)) return RIC_E_HIP;
+	w->pend = false;
+	return decode_inverse_pipelined(w, m, plane, stride, trans, dq);
+}
+
+bool ll1(ric_wavelet* w, const int16_t** p, long* pitch, int* dx, int* dy)
+{
+	if (w->P.nlev < 2) return false;
+	const Band& B = w->P.L[0].b[BL];
+	if (B.is_int) return false;
+	*p = (const int16_t*)(w->d_arena + B.off);
+	*pitch = B.pitch;
+	*dx = B.dx;
+	*dy = B.dy;
+	return true;
+}
+
+}  // namespace wapi
+}  // namespace ric
 
 extern "C" {
 

@@ -99,6 +99,13 @@ def lib():
         "ric_batch_roundtrip_hybrid": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
         "ric_batch_diag_gpu": (_I, [_P, _P, _I, _I, _I, _I, _P]),
         "ric_batch_prof_read": (_I, [_P, _P, _P, _P, _I]),
+        "ric_video_create": (_I, [ctypes.POINTER(_P), _I, _I, _I, _I, _I]),
+        "ric_video_destroy": (None, [_P]),
+        "ric_video_set_quant": (_I, [_P, _I]),
+        "ric_video_encode": (_I, [_P, _P, _I, _I, _P, _S, ctypes.POINTER(_I)]),
+        "ric_video_decode": (_I, [_P, _P, _S, ctypes.POINTER(_I)]),
+        "ric_video_output": (_I, [_P, _P, _I, _I]),
+        "ric_video_motion": (_I, [_P, _P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -515,3 +522,65 @@ class Codec:
         if rc not in (RIC_OK, RIC_E_STREAM):
             _chk(rc, "DecompressImage")
         return rc
+
+
+class VideoCodec:
+    """CRududuCodec (src/lib/rududucodec.{h,cpp}): the reference's video codec
+    on the GPU.  encoder=True is CRududuCodec(encode, ...), else decode.
+    Frames are (3, h, w) uint8 arrays of planes R, G, B with the bottom row
+    first (CImage::inputSGI), host numpy or device tensors."""
+
+    def __init__(self, encoder, w, h, component=3, device=0):
+        hd = _P()
+        _chk(lib().ric_video_create(ctypes.byref(hd), int(bool(encoder)), w, h, component, device), "CRududuCodec")
+        self.h = hd
+        self.w, self.hgt = w, h
+        self._quant = 0
+        self._buf = np.zeros(w * h * 3 * 4 + 65536, np.uint8)
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.ric_video_destroy(self.h)
+            self.h = None
+
+    @property
+    def quant(self):
+        return self._quant
+
+    @quant.setter
+    def quant(self, q):
+        _chk(lib().ric_video_set_quant(self.h, q), "CRududuCodec::quant")
+        self._quant = q
+
+    def encode(self, frame, stride=None, on_device=None):
+        """CRududuCodec::encode: returns the frame's stream (size + 2 bytes)."""
+        dev = on_device if on_device is not None else not isinstance(frame, np.ndarray)
+        if not dev:
+            frame = np.ascontiguousarray(frame, np.uint8)
+        size = _I()
+        _chk(lib().ric_video_encode(self.h, _ptr(frame), stride or self.w, int(dev), self._buf.ctypes.data,
+                                    self._buf.nbytes, ctypes.byref(size)), "CRududuCodec::encode")
+        return self._buf[:size.value + 2].tobytes()
+
+    def decode(self, stream):
+        """CRududuCodec::decode: returns getSize()."""
+        b = np.frombuffer(stream, np.uint8)
+        size = _I()
+        rc = lib().ric_video_decode(self.h, b.ctypes.data, len(stream), ctypes.byref(size))
+        if rc != RIC_OK:
+            _chk(rc, "CRududuCodec::decode")
+        return size.value
+
+    def output(self, border=False):
+        """*outImage of the last call: int16 planes Y, Co, Cg (3, h, w), or with
+        the 15-sample border (3, h + 30, w + 30)."""
+        b = 15 if border else 0
+        out = np.zeros((3, self.hgt + 2 * b, self.w + 2 * b), np.int16)
+        _chk(lib().ric_video_output(self.h, out.ctypes.data, int(bool(border)), 0), "outImage")
+        return out
+
+    def motion(self):
+        """the motion field (h >> 3, w >> 3), uint32 (x low, y high; MV_INTRA 0x80008000)"""
+        out = np.zeros((self.hgt >> 3, self.w >> 3), np.uint32)
+        _chk(lib().ric_video_motion(self.h, out.ctypes.data), "motion field")
+        return out

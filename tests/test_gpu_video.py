@@ -10,8 +10,12 @@ with the video quants() table.  Streams and planes must be byte-identical."""
 import os
 import subprocess
 
+import json
+
 import numpy as np
 import pytest
+
+import video_seq
 
 pytestmark = pytest.mark.gpu
 
@@ -82,3 +86,49 @@ def test_video_intra_matches_reference(ric, tmp_path, w, h, q, n):
         assert np.array_equal(g[2], e[2]), "frame %d decoder planes" % k
         assert g[3] == e[3], "frame %d decoder getSize" % k
     assert got == want
+
+
+GV = json.load(open(os.path.join(HERE, "golden", "video.json")))
+
+
+def _first_diff(a, b):
+    d = np.argwhere(a != b)
+    return None if d.size == 0 else (tuple(int(x) for x in d[0]), int(a[tuple(d[0])]), int(b[tuple(d[0])]), len(d))
+
+
+def _check_sequence(ric, w, h, q, n, seed, tmp_path):
+    """CRududuCodec on the GPU vs the reference's classes (oracle/_ref/ricvid_ref),
+    frame by frame: stream bytes, encoder output image (with its border: the
+    next frame's quarter-pel pass reads it), motion field, decoder output."""
+    if not os.path.exists(video_seq.REF_BIN):
+        pytest.fail("oracle/_ref/ricvid_ref not built (make -C oracle with /root/reference present)")
+    seq = video_seq.sequence(w, h, n, seed)
+    want = video_seq.ref_run(seq, q, tmp_path)
+    enc = ric.VideoCodec(True, w, h)
+    dec = ric.VideoCodec(False, w, h)
+    enc.quant = q
+    dec.quant = q
+    B = video_seq.BORDER
+    for k in range(n):
+        e = want[k]
+        s = enc.encode(seq[k])
+        assert np.array_equal(enc.motion(), e["mv"]), "frame %d motion field: %s" % (k, _first_diff(enc.motion(), e["mv"]))
+        bo = enc.output(border=True)
+        assert np.array_equal(bo[:, B:B + h, B:B + w], e["enc"]), \
+            "frame %d encoder image: %s" % (k, _first_diff(bo[:, B:B + h, B:B + w], e["enc"]))
+        assert np.array_equal(bo, e["bordered"]), "frame %d encoder image border: %s" % (k, _first_diff(bo, e["bordered"]))
+        assert len(s) == e["size"] + 2 and s == e["stream"], "frame %d stream (%d vs %d bytes)" % (k, len(s), e["size"] + 2)
+        assert dec.decode(s) == e["dsize"], "frame %d decoder getSize" % k
+        assert np.array_equal(dec.output(), e["dec"]), "frame %d decoder image: %s" % (k, _first_diff(dec.output(), e["dec"]))
+
+
+@pytest.mark.parametrize("cfg", GV["sequences"], ids=lambda c: "%dx%d_q%d" % (c["w"], c["h"], c["q"]))
+def test_video_golden_sequences(ric, cfg, tmp_path):
+    _check_sequence(ric, cfg["w"], cfg["h"], cfg["q"], cfg["frames"], cfg["seed"], tmp_path)
+
+
+@pytest.mark.parametrize("w,h,q,n,seed", [(68, 44, 4, 3, 11), (333, 141, -12, 3, 12), (1280, 720, 20, 3, 13)])
+def test_video_sequences(ric, w, h, q, n, seed, tmp_path):
+    """odd and non-multiple-of-8 sizes (the OBMC grid does not cover the
+    frame), the finest quantiser, and testmotion.cpp's 1280x720 at quant 20"""
+    _check_sequence(ric, w, h, q, n, seed, tmp_path)
