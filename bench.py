@@ -216,9 +216,11 @@ def cpu_baseline(W, H, q, trans, threads, per_thread=2):
                       "value = the best throughput point (%d threads)"
                       % (W, H, q, ", ".join("%d frames on %d threads (%.1f s)" % (p["frames"], p["threads"], p["wall_s"])
                                             for p in points), best["threads"]),
-            "headline_cores": "%d threads: %s" % (best["threads"], "this GPU's CPU share (OMP_NUM_THREADS)"
-                                                  if best["threads"] == threads else
-                                                  "the node's per-GPU share of its cores (nproc / 8)"),
+            "headline_cores": "%d threads: %s%s" % (best["threads"], "this GPU's CPU share (OMP_NUM_THREADS)"
+                                                    if best["threads"] == threads else
+                                                    "the node's per-GPU share of its cores (nproc / 8)",
+                                                    "; the process's cgroup CPU quota is %s CPUs" % hi["cgroup_cpu_quota"]
+                                                    if hi["cgroup_cpu_quota"] else ""),
             "latency_1core": lat, "throughput_points": points, "host": hi}
 
 

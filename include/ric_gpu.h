@@ -276,7 +276,9 @@ int ric_video_encode(ric_video* v, const uint8_t* pix, int stride, int pix_on_de
                      int* size);
 /* CRududuCodec::decode(unsigned char* pBuffer, CImage** outImage)
  * (rududucodec.cpp:121-141): buf holds the len bytes of one frame's stream;
- * *size = codec.getSize().  RIC_E_STREAM when the decoder ran past len. */
+ * *size = codec.getSize().  RIC_E_STREAM when the decoder ran past len.
+ * len 0 reads buf in place with no end, as the reference does (UNSAFE on
+ * untrusted input, see ric_mux_create_decoder_inplace). */
 int ric_video_decode(ric_video* v, const uint8_t* buf, size_t len, int* size);
 /* *outImage of the last encode / decode: its planes Y, Co, Cg as int16,
  * 3 x h x w (border 0), or with the 15-sample border, 3 x (h + 30) x (w + 30)

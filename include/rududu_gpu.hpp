@@ -13,6 +13,8 @@
 //                       DimX..type, pParent/pChild, pBand, Mean/TSUQ/TSUQi/
 //                       Add/Clear/GetBand
 //   rududu::trans / cmode / band_t  (src/lib/utils.h:27-28, band.h:35)
+//   rududu::CRududuCodec (src/lib/rududucodec.h:31-55) and the CImage caller
+//                       container (src/lib/image.h:30-66): the video codec
 //
 // What differs, and why:
 //   * the pyramid lives in GPU memory.  CBand::pBand converts (C-style cast,
@@ -36,7 +38,9 @@
 #include <cstdint>
 #include <climits>
 #include <cstdlib>
+#include <cmath>
 #include <cstring>
+#include <utility>
 #include <iostream>
 #include <memory>
 #include <stdexcept>
@@ -416,6 +420,183 @@ private:
 	}
 	ric_wavelet* w_ = nullptr;
 	int level_ = 0;
+};
+
+// CImage (src/lib/image.h:30-66): the caller's image container, host planes in
+// the reference's layout -- dimXAlign = (x + 2 BORDER + Align - 1) & -Align
+// samples per row, BORDER rows and columns of border, planes back to back
+// (image.cpp:56-68).  The codec's own images live in HBM (ric_video); the
+// CImage a CRududuCodec call hands back is a host copy of its output image,
+// border included.  The pixel helpers are the reference's caller-side
+// conversions (image.cpp:70-278).
+#ifndef BORDER
+#define BORDER 15
+#endif
+class CImage {
+public:
+	unsigned int dimX = 0, dimY = 0, dimXAlign = 0;
+	int component = 0;
+	short* pImage[3] = {nullptr, nullptr, nullptr};
+
+	CImage(unsigned int x, unsigned int y, int cmpnt, int Align) : dimX(x), dimY(y), component(cmpnt) { init(Align); }
+	CImage(CImage* pImg, int Align) : dimX(pImg->dimX), dimY(pImg->dimY), component(pImg->component) { init(Align); }
+
+	// image.cpp:96-123: planes R, G, B (stride bytes per row, bottom row
+	// first) -> Y, Co, Cg; 8-bit input is scaled (Y << 4, Co / Cg << 3)
+	template <class input_t> void inputSGI(input_t* pIn, int stride, short offset)
+	{
+		const long ps = (long)stride * dimY;
+		for (unsigned int j = 0; j < dimY; j++) {
+			const input_t* R = pIn + (long)(dimY - 1 - j) * stride;
+			const input_t* G = R + ps;
+			const input_t* B = G + ps;
+			short *Y = pImage[0] + (long)j * dimXAlign, *Co = pImage[1] + (long)j * dimXAlign,
+			      *Cg = pImage[2] + (long)j * dimXAlign;
+			for (unsigned int i = 0; i < dimX; i++) {
+				Co[i] = (short)(R[i] - B[i]);
+				Y[i] = (short)(B[i] + (Co[i] >> 1));
+				Cg[i] = (short)(G[i] - Y[i]);
+				Y[i] = (short)(Y[i] + (Cg[i] >> 1) + offset);
+				if (sizeof(input_t) == 1) {
+					Y[i] = (short)(Y[i] * 16);
+					Co[i] = (short)(Co[i] * 8);
+					Cg[i] = (short)(Cg[i] * 8);
+				}
+			}
+		}
+	}
+	// image.cpp:148-185 (reads one sample right of / below odd-sized images)
+	template <class output_t, bool i420> void outputYV12(output_t* pOut, int stride, short offset)
+	{
+		output_t* Yo = pOut;
+		output_t* Vo = Yo + (long)stride * dimY;
+		output_t* Uo = Vo + (((long)stride * dimY) >> 2);
+		const int shift = 12 - (int)sizeof(output_t) * 8;
+		if (sizeof(output_t) == 1) offset = (short)(offset * 16);
+		else if (sizeof(output_t) == 2) offset = (short)(offset >> 4);
+		if (i420) std::swap(Uo, Vo);
+		const long S = dimXAlign;
+		for (unsigned int j = 0; j < dimY; j += 2) {
+			const short *Y = pImage[0] + j * S, *Co = pImage[1] + j * S, *Cg = pImage[2] + j * S;
+			for (unsigned int i = 0; i < dimX; i += 2) {
+				auto luma = [&](long k) {
+					return (output_t)(((440 * (Y[k] - offset) + 82 * Co[k] + 76 * Cg[k] + (1 << (8 + shift))) >> (9 + shift)) + 16);
+				};
+				Yo[i] = luma(i);
+				Yo[i + 1] = luma(i + 1);
+				Yo[i + stride] = luma(i + S);
+				Yo[i + stride + 1] = luma(i + S + 1);
+				const int co = Co[i] + Co[i + 1] + Co[i + S] + Co[i + S + 1];
+				const int cg = Cg[i] + Cg[i + 1] + Cg[i + S] + Cg[i + S + 1];
+				Uo[i >> 1] = (output_t)(((-150 * co - 148 * cg + (1 << (9 + shift))) >> (10 + shift)) + 128);
+				Vo[i >> 1] = (output_t)(((130 * co - 188 * cg + (1 << (9 + shift))) >> (10 + shift)) + 128);
+			}
+			Yo += stride * 2;
+			Vo += stride >> 1;
+			Uo += stride >> 1;
+		}
+	}
+	// image.cpp:216-246
+	CImage& operator-=(const CImage& In) { return addsub(In, -1); }
+	CImage& operator+=(const CImage& In) { return addsub(In, 1); }
+	// image.cpp:248-265: per component 10 log10(4096^2 / MSE)
+	void psnr(const CImage& In, float* ret)
+	{
+		for (int c = 0; c < component; c++) {
+			long long sum = 0;
+			for (unsigned int j = 0; j < dimY; j++)
+				for (unsigned int i = 0; i < dimX; i++) {
+					const int t = In.pImage[c][(long)j * In.dimXAlign + i] - pImage[c][(long)j * dimXAlign + i];
+					sum += t * t;
+				}
+			ret[c] = (float)(10. * (std::log((double)(1 << 24)) - std::log((double)sum / (dimX * dimY))) / std::log(10.));
+		}
+	}
+	// image.cpp:267-278
+	void copy(const CImage& In)
+	{
+		for (int c = 0; c < component; c++)
+			for (unsigned int j = 0; j < dimY; j++)
+				std::memcpy(pImage[c] + (long)j * dimXAlign, In.pImage[c] + (long)j * In.dimXAlign, sizeof(short) * dimX);
+	}
+	// this image's planes with their border from `bordered` (3 x (dimY + 30)
+	// x (dimX + 30) int16, ric_video_output with border)
+	void load_bordered(const int16_t* bordered)
+	{
+		const unsigned int bw = dimX + 2 * BORDER, bh = dimY + 2 * BORDER;
+		for (int c = 0; c < component; c++)
+			for (unsigned int r = 0; r < bh; r++)
+				std::memcpy(pImage[c] + ((long)r - BORDER) * dimXAlign - BORDER, bordered + ((size_t)c * bh + r) * bw,
+				            sizeof(short) * bw);
+	}
+
+private:
+	std::vector<short> data_;
+	void init(int Align)
+	{
+		dimXAlign = (dimX + 2 * BORDER + Align - 1) & -Align;
+		const size_t plane = (size_t)dimXAlign * (dimY + 2 * BORDER);
+		data_.assign(plane * component + Align, 0);
+		for (int c = 0; c < component && c < 3; c++) pImage[c] = data_.data() + c * plane + BORDER * dimXAlign + BORDER;
+	}
+	CImage& addsub(const CImage& In, int sign)
+	{
+		for (int c = 0; c < component; c++)
+			for (unsigned int j = 0; j < dimY; j++)
+				for (unsigned int i = 0; i < dimX; i++) {
+					short& o = pImage[c][(long)j * dimXAlign + i];
+					o = (short)(o + sign * In.pImage[c][(long)j * In.dimXAlign + i]);
+				}
+		return *this;
+	}
+};
+
+// CRududuCodec (src/lib/rududucodec.h:31-55): the video codec over ric_video.
+// encode / decode keep the reference's signatures and return values; the
+// CImage* handed back is a host copy of the codec's output image (valid until
+// the next call).  Like the reference, encode writes pBuffer with no bound and
+// decode reads it in place.
+class CRududuCodec {
+public:
+	int quant = 0;
+	CRududuCodec(cmode mode, int width, int height, int component, int device = 0)
+		: out_(width, height, component, ALIGN), bordered_((size_t)3 * (width + 2 * BORDER) * (height + 2 * BORDER))
+	{
+		ric_check(ric_video_create(&v_, mode == rududu::encode ? 1 : 0, width, height, component, device), "CRududuCodec");
+	}
+	~CRududuCodec() { ric_video_destroy(v_); }
+	CRududuCodec(const CRududuCodec&) = delete;
+	CRududuCodec& operator=(const CRududuCodec&) = delete;
+
+	int encode(unsigned char* pImage, int stride, unsigned char* pBuffer, CImage** outImage)
+	{
+		ric_check(ric_video_set_quant(v_, quant), "CRududuCodec::quant");
+		int size = 0;
+		ric_check(ric_video_encode(v_, pImage, stride, 0, pBuffer, SIZE_MAX, &size), "CRududuCodec::encode");
+		if (outImage) *outImage = sync_out();
+		return size;
+	}
+	int decode(unsigned char* pBuffer, CImage** outImage)
+	{
+		ric_check(ric_video_set_quant(v_, quant), "CRududuCodec::quant");
+		int size = 0;
+		const int rc = ric_video_decode(v_, pBuffer, 0, &size);
+		if (rc != RIC_OK && rc != RIC_E_STREAM) ric_check(rc, "CRududuCodec::decode");
+		if (outImage) *outImage = sync_out();
+		return size;
+	}
+	ric_video* handle() { return v_; }
+
+private:
+	ric_video* v_ = nullptr;
+	CImage out_;
+	std::vector<int16_t> bordered_;
+	CImage* sync_out()
+	{
+		ric_check(ric_video_output(v_, bordered_.data(), 1, 0), "outImage");
+		out_.load_bordered(bordered_.data());
+		return &out_;
+	}
 };
 
 }  // namespace rududu

@@ -38,7 +38,9 @@
 //              u32 decode()'s return, the decoder's output image, the
 //              encoder's motion vectors ((W >> 3) x (H >> 3) u32), and the
 //              bordered planes of the encoder's output image (3 x (H + 30) x
-//              (W + 30) int16, rows and columns -15 .. +14 past the edges)
+//              (W + 30) int16, rows and columns -15 .. +14 past the edges),
+//              and that image as CImage::outputYV12<char, false>(pOut, W,
+//              -128) writes it (W * H * 3 / 2 bytes, testmotion.cpp:62)
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -285,6 +287,11 @@ int main(int argc, char** argv)
 		put_planes(fo, dout, W, H, 0);
 		fwrite(enc.mvs(), 4, (size_t)(W >> 3) * (H >> 3), fo);
 		put_planes(fo, eout, W, H, 15);
+		// CImage::outputYV12<char, false>(pOut, W, -128) of the encoder's
+		// image, as testmotion.cpp:62 writes it (image.cpp:148-185)
+		std::vector<char> yv((size_t)W * H * 3 / 2 + 16, 0);
+		eout->outputYV12<char, false>(yv.data(), W, -128);
+		fwrite(yv.data(), 1, (size_t)W * H * 3 / 2, fo);
 	}
 	fclose(fo);
 	fclose(fi);

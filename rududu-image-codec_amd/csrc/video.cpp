@@ -333,7 +333,7 @@ int ric_video_encode(ric_video* v, const uint8_t* pix, int stride, int pix_on_de
 
 int ric_video_decode(ric_video* v, const uint8_t* buf, size_t len, int* size)
 {
-	if (!v || !buf || !size || len < 4) return RIC_E_ARG;
+	if (!v || !buf || !size || (len != 0 && len < 4)) return RIC_E_ARG;
 	if (vfail(hipSetDevice(v->device), "hipSetDevice")) return RIC_E_HIP;
 	const VidGeom& g = v->g;
 	v->mux.reinit_decoder(buf, len);                       // codec.initDecoder(pBuffer) (:123)

@@ -41,6 +41,14 @@ def _planes(w, h, n, seed):
     return np.stack(out)
 
 
+def _byte_diff(a, b):
+    """where two byte strings first differ (pytest's own diff of MB-sized
+    bytes takes minutes)"""
+    n = min(len(a), len(b))
+    d = np.nonzero(np.frombuffer(a[:n], np.uint8) != np.frombuffer(b[:n], np.uint8))[0]
+    return "lengths %d vs %d, first difference at %s" % (len(a), len(b), int(d[0]) if d.size else n)
+
+
 def _run(binary, w, h, q, n, planes, tmp):
     src = os.path.join(tmp, "in.i16")
     dst = os.path.join(tmp, os.path.basename(binary) + ".bin")
@@ -69,10 +77,12 @@ def _frames(blob, w, h, n):
     return out
 
 
-# q is CRududuCodec::quant: quants(q + 20) is the quantiser, so q down to -19
-# (quants(1) = 32) gives dense streams; testmotion.cpp uses 20 (quants(40) = 7132)
-@pytest.mark.parametrize("w,h,q,n", [(128, 96, -10, 3), (160, 120, -19, 2), (200, 72, 0, 2), (97, 61, -5, 2),
-                                     (352, 288, -15, 3), (64, 48, 20, 2)])
+# q is CRududuCodec::quant: quants(q + 20) is the quantiser and quants(q + 12)
+# the RD lambda, so q >= -12 (below, quants reads its table at a negative
+# index: undefined in the reference); q = -12 gives the densest streams
+# (quants(8) = 84), testmotion.cpp uses 20 (quants(40) = 7132)
+@pytest.mark.parametrize("w,h,q,n", [(128, 96, -10, 3), (160, 120, -12, 2), (200, 72, 0, 2), (97, 61, -5, 2),
+                                     (352, 288, -11, 3), (64, 48, 20, 2)])
 def test_video_intra_matches_reference(ric, tmp_path, w, h, q, n):
     if not os.path.exists(REF_BIN):
         pytest.fail("oracle/_ref/video_intra_ref not built (make -C oracle with /root/reference present)")
@@ -81,11 +91,11 @@ def test_video_intra_matches_reference(ric, tmp_path, w, h, q, n):
     want = _run(REF_BIN, w, h, q, n, planes, str(tmp_path))
     gf, wf = _frames(got, w, h, n), _frames(want, w, h, n)
     for k, (g, e) in enumerate(zip(gf, wf)):
-        assert g[0] == e[0], "frame %d stream" % k
+        assert g[0] == e[0], "frame %d stream: %s" % (k, _byte_diff(g[0], e[0]))
         assert np.array_equal(g[1], e[1]), "frame %d encoder reconstruction" % k
         assert np.array_equal(g[2], e[2]), "frame %d decoder planes" % k
         assert g[3] == e[3], "frame %d decoder getSize" % k
-    assert got == want
+    assert got == want, _byte_diff(got, want)
 
 
 GV = json.load(open(os.path.join(HERE, "golden", "video.json")))
@@ -117,7 +127,7 @@ def _check_sequence(ric, w, h, q, n, seed, tmp_path):
         assert np.array_equal(bo[:, B:B + h, B:B + w], e["enc"]), \
             "frame %d encoder image: %s" % (k, _first_diff(bo[:, B:B + h, B:B + w], e["enc"]))
         assert np.array_equal(bo, e["bordered"]), "frame %d encoder image border: %s" % (k, _first_diff(bo, e["bordered"]))
-        assert len(s) == e["size"] + 2 and s == e["stream"], "frame %d stream (%d vs %d bytes)" % (k, len(s), e["size"] + 2)
+        assert s == e["stream"], "frame %d stream: %s" % (k, _byte_diff(s, e["stream"]))
         assert dec.decode(s) == e["dsize"], "frame %d decoder getSize" % k
         assert np.array_equal(dec.output(), e["dec"]), "frame %d decoder image: %s" % (k, _first_diff(dec.output(), e["dec"]))
 
@@ -132,3 +142,42 @@ def test_video_sequences(ric, w, h, q, n, seed, tmp_path):
     """odd and non-multiple-of-8 sizes (the OBMC grid does not cover the
     frame), the finest quantiser, and testmotion.cpp's 1280x720 at quant 20"""
     _check_sequence(ric, w, h, q, n, seed, tmp_path)
+
+
+COMPAT_BIN = os.path.join(HERE, "native", "video_compat")
+
+
+@pytest.mark.parametrize("w,h,q,n,seed", [(128, 96, -5, 12, 5), (176, 144, 20, 4, 21)])
+def test_video_compat_caller(ric, w, h, q, n, seed, tmp_path):
+    """tests/native/video_compat.cpp -- testmotion.cpp's calls (CRududuCodec
+    encode / decode, quant, CImage::psnr, outputYV12<char, false>) over the
+    GPU drop-in: the same streams, sizes and YV12 output as the reference."""
+    seq = video_seq.sequence(w, h, n, seed)
+    want = video_seq.ref_run(seq, q, tmp_path)
+    src = os.path.join(str(tmp_path), "compat.rgb")
+    dst = os.path.join(str(tmp_path), "compat.bin")
+    np.ascontiguousarray(seq).tofile(src)
+    subprocess.run([COMPAT_BIN, str(w), str(h), str(q), str(n), src, dst], check=True, timeout=300)
+    blob, o = open(dst, "rb").read(), 0
+    for k in range(n):
+        size = int(np.frombuffer(blob, np.uint32, 1, o)[0]); o += 4
+        stream = blob[o:o + size + 2]; o += size + 2
+        dsize = int(np.frombuffer(blob, np.uint32, 1, o)[0]); o += 4
+        yv = blob[o:o + w * h * 3 // 2]; o += w * h * 3 // 2
+        psnr = np.frombuffer(blob, np.float32, 6, o).reshape(2, 3); o += 24
+        e = want[k]
+        assert size == e["size"] and stream == e["stream"], "frame %d stream: %s" % (k, _byte_diff(stream, e["stream"]))
+        assert dsize == e["dsize"], "frame %d decode() return" % k
+        assert yv == e["yv12"], "frame %d outputYV12: %s" % (k, _byte_diff(yv, e["yv12"]))
+        # CImage::psnr (src/lib/image.cpp:248-265) of the origin against both outputs
+        r, g_, b = (seq[k][i].astype(np.int32) for i in range(3))
+        co = r - b
+        y = b + (co >> 1)
+        cg = g_ - y
+        y = y + (cg >> 1) - 128
+        origin = np.stack([y * 16, co * 8, cg * 8])[:, ::-1, :]       # inputSGI: bottom row first
+        for side, planes in ((0, e["enc"]), (1, e["dec"])):
+            mse = ((planes.astype(np.int64) - origin) ** 2).reshape(3, -1).sum(1) / (w * h)
+            ref_psnr = (10.0 * (np.log(float(1 << 24)) - np.log(mse)) / np.log(10.0)).astype(np.float32)
+            np.testing.assert_allclose(psnr[side], ref_psnr, rtol=1e-6)
+    assert o == len(blob)

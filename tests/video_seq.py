@@ -28,7 +28,7 @@ def sequence(w, h, n, seed=0, dx=3, dy=2, margin=64):
 
 
 def parse(blob, w, h, n):
-    """ricvid_ref's output: per frame dict(size, stream, enc, dsize, dec, mv, bordered)"""
+    """ricvid_ref's output: per frame dict(size, stream, enc, dsize, dec, mv, bordered, yv12)"""
     frames, o = [], 0
     npl = 3 * w * h
     nb = 3 * (h + 2 * BORDER) * (w + 2 * BORDER)
@@ -41,7 +41,8 @@ def parse(blob, w, h, n):
         dec = np.frombuffer(blob, np.int16, npl, o).reshape(3, h, w); o += 2 * npl
         mv = np.frombuffer(blob, np.uint32, nmv, o).reshape(h >> 3, w >> 3); o += 4 * nmv
         bord = np.frombuffer(blob, np.int16, nb, o).reshape(3, h + 2 * BORDER, w + 2 * BORDER); o += 2 * nb
-        frames.append(dict(size=size, stream=stream, enc=enc, dsize=dsize, dec=dec, mv=mv, bordered=bord))
+        yv12 = blob[o:o + w * h * 3 // 2]; o += w * h * 3 // 2
+        frames.append(dict(size=size, stream=stream, enc=enc, dsize=dsize, dec=dec, mv=mv, bordered=bord, yv12=yv12))
     assert o == len(blob), (o, len(blob))
     return frames
 
