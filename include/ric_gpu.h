@@ -282,7 +282,8 @@ int ric_video_encode(ric_video* v, const uint8_t* pix, int stride, int pix_on_de
 int ric_video_decode(ric_video* v, const uint8_t* buf, size_t len, int* size);
 /* *outImage of the last encode / decode: its planes Y, Co, Cg as int16,
  * 3 x h x w (border 0), or with the 15-sample border, 3 x (h + 30) x (w + 30)
- * (border 1), to host or device memory (on_device). */
+ * (border 1), to host or device memory (on_device).  Diagnostics: border 2
+ * copies the OBMC prediction (predImage) instead, with its border. */
 int ric_video_output(ric_video* v, int16_t* planes, int border, int on_device);
 /* the motion field after the last encode / decode: (w >> 3) x (h >> 3)
  * vectors in quarter pel, x in the low 16 bits, y in the high 16, MV_INTRA =

@@ -176,6 +176,7 @@ public:
 	void encodeImage(CImage* pImage)
 	{
 		const int S = align_of(pImage);
+		dump(pImage, "res");
 		for (int c = 0; c < 3; c++) {
 			wavelet->Transform(plane(pImage, c), S, TRANSFORM);
 			wavelet->CodeBand(&codec, quants(quant + 20), quants(quant + 12));
@@ -203,6 +204,7 @@ public:
 			obme->EPZS(images);
 			obme->encode(&codec);
 			obme->apply_mv(images, *predImage);
+			dump(predImage, "pred");
 			*images[0][0] -= *predImage;
 			encodeImage(images[0][0]);
 			*images[0][0] += *predImage;
@@ -212,6 +214,7 @@ public:
 		}
 		key_count++;
 		if (key_count == 10) key_count = 0;
+		frame++;
 		*outImage = images[0][0];
 		images.remove(1);
 		return codec.endCoding() - pBuffer - 2;
@@ -234,6 +237,22 @@ public:
 		return codec.getSize();
 	}
 	const sMotionVector* mvs() const { return obmc->*Member<MvField>::ptr; }
+	// diagnostics: RICVID_DUMP=<dir> writes every frame's residual planes (the
+	// encoder's image as encodeImage receives it) and prediction, bordered
+	int frame = 0;
+	void dump(CImage* im, const char* what)
+	{
+		const char* dir = getenv("RICVID_DUMP");
+		if (!dir) return;
+		char path[4096];
+		snprintf(path, sizeof path, "%s/%s_f%d.i16", dir, what, frame);
+		FILE* f = fopen(path, "wb");
+		if (!f) return;
+		const int S = align_of(im);
+		for (int c = 0; c < 3; c++)
+			for (int y = -15; y < h + 15; y++) fwrite(plane(im, c) + (long)y * S - 15, 2, w + 30, f);
+		fclose(f);
+	}
 
 private:
 	CImageBuffer images;
@@ -289,7 +308,8 @@ int main(int argc, char** argv)
 		put_planes(fo, eout, W, H, 15);
 		// CImage::outputYV12<char, false>(pOut, W, -128) of the encoder's
 		// image, as testmotion.cpp:62 writes it (image.cpp:148-185)
-		std::vector<char> yv((size_t)W * H * 3 / 2 + 16, 0);
+		// (odd sizes: outputYV12 writes a little past W * H * 3 / 2)
+		std::vector<char> yv((size_t)W * H * 3 / 2 + 4 * (size_t)W + 64, 0);
 		eout->outputYV12<char, false>(yv.data(), W, -128);
 		fwrite(yv.data(), 1, (size_t)W * H * 3 / 2, fo);
 	}

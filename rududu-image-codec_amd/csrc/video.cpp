@@ -365,13 +365,14 @@ int ric_video_decode(ric_video* v, const uint8_t* buf, size_t len, int* size)
 int ric_video_output(ric_video* v, int16_t* planes, int border, int on_device)
 {
 	if (!v || !planes) return RIC_E_ARG;
-	if (v->out_id < 0) return RIC_E_ARG;
+	if (v->out_id < 0 && border != 2) return RIC_E_ARG;
 	if (vfail(hipSetDevice(v->device), "hipSetDevice")) return RIC_E_HIP;
 	const VidGeom& g = v->g;
 	const int b = border ? kVidBorder : 0;
 	const int ow = g.w + 2 * b, oh = g.h + 2 * b;
+	const int16_t* base = border == 2 ? v->pred_img() : v->img(v->out_id);
 	for (int c = 0; c < 3; c++) {
-		const int16_t* src = v->img(v->out_id) + c * g.P - (long)b * g.S - b;
+		const int16_t* src = base + c * g.P - (long)b * g.S - b;
 		VCHK(hipMemcpy2DAsync(planes + (size_t)c * ow * oh, (size_t)ow * 2, src, (size_t)g.S * 2, (size_t)ow * 2, oh,
 		                      on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, v->st));
 	}

@@ -579,6 +579,12 @@ class VideoCodec:
         _chk(lib().ric_video_output(self.h, out.ctypes.data, int(bool(border)), 0), "outImage")
         return out
 
+    def prediction(self):
+        """diagnostics: the OBMC prediction image (predImage) with its border"""
+        out = np.zeros((3, self.hgt + 30, self.w + 30), np.int16)
+        _chk(lib().ric_video_output(self.h, out.ctypes.data, 2, 0), "predImage")
+        return out
+
     def motion(self):
         """the motion field (h >> 3, w >> 3), uint32 (x low, y high; MV_INTRA 0x80008000)"""
         out = np.zeros((self.hgt >> 3, self.w >> 3), np.uint32)
