@@ -205,3 +205,17 @@ def gray_plane(pix, q):
     """Level shift of src/ric/ric.cpp:144-148 for one gray plane."""
     p = pix.astype(np.int32) - 128
     return (p << 4 if q else p).astype(np.int16)
+
+
+def full_range_plane(w, h, seed, kind):
+    """int16 planes that push the 9/7 lifting past 16 bits: the mult08 of a
+    sum runs in int in the reference (the template deduces C = int,
+    src/lib/wavelet2d.cpp:336), so a restatement that wraps the sum differs"""
+    rng = np.random.default_rng(seed)
+    if kind == "uniform":
+        return rng.integers(-32768, 32768, (h, w)).astype(np.int16)
+    if kind == "alt":                                   # extreme alternating pattern
+        y, x = np.mgrid[0:h, 0:w]
+        return np.where(((x + y) % 2) == 0, 32767, -32768).astype(np.int16)
+    y, x = np.mgrid[0:h, 0:w]                           # large smooth ramp + noise
+    return np.clip(30000 * np.sin(x / 7.0) * np.cos(y / 5.0) + rng.normal(0, 3000, (h, w)), -32768, 32767).astype(np.int16)

@@ -35,7 +35,10 @@ static inline int bitlen(uint32_t v) { int r = 0; while (v) { r++; v >>= 1; } re
 static inline int TR(int sh, int v) { return sh ? (int)(int16_t)v : v; }
 static inline uint32_t UC(int sh, int v) { return sh ? (uint32_t)(uint16_t)v : (uint32_t)v; }
 
-/* CWavelet2D::mult08, src/lib/wavelet2d.cpp:307-318 (all on C) */
+/* CWavelet2D::mult08, src/lib/wavelet2d.cpp:307-318.  It is a template on
+ * its argument's type: mult08(i[1]) runs on C (short truncations), but the
+ * calls on a sum, mult08(i[1] + i[3]), deduce C = int -- the sum is not
+ * truncated and the steps run in int (sh 0 here). */
 static inline int mult08(int sh, int a)
 {
 	a = TR(sh, a);
@@ -63,7 +66,7 @@ static void line97(int sh, int32_t* x, long st, int len)
 	if (!(len & 1)) X(last) = TR(sh, X(last) - (X(last - 1) >> 3));
 	/* P2 on even samples */
 	X(0) = TR(sh, X(0) + 2 * mult08(sh, X(1)));
-	for (n = 2; n < last; n += 2) X(n) = TR(sh, X(n) + mult08(sh, X(n - 1) + X(n + 1)));
+	for (n = 2; n < last; n += 2) X(n) = TR(sh, X(n) + mult08(0, X(n - 1) + X(n + 1)));
 	if (len & 1) X(last) = TR(sh, X(last) + 2 * mult08(sh, X(last - 1)));
 	/* U2 on odd samples */
 	for (n = 1; n < last; n += 2) { t = TR(sh, X(n - 1) + X(n + 1)); X(n) = TR(sh, X(n) + ((t >> 1) - (t >> 5))); }
@@ -77,7 +80,7 @@ static void line97i(int sh, int32_t* x, long st, int len)
 	for (n = 1; n < last; n += 2) { t = TR(sh, X(n - 1) + X(n + 1)); X(n) = TR(sh, X(n) - ((t >> 1) - (t >> 5))); }
 	if (!(len & 1)) X(last) = TR(sh, X(last) - (X(last - 1) - (X(last - 1) >> 4)));
 	X(0) = TR(sh, X(0) - 2 * mult08(sh, X(1)));
-	for (n = 2; n < last; n += 2) X(n) = TR(sh, X(n) - mult08(sh, X(n - 1) + X(n + 1)));
+	for (n = 2; n < last; n += 2) X(n) = TR(sh, X(n) - mult08(0, X(n - 1) + X(n + 1)));
 	if (len & 1) X(last) = TR(sh, X(last) - 2 * mult08(sh, X(last - 1)));
 	for (n = 1; n < last; n += 2) X(n) = TR(sh, X(n) + ((X(n - 1) + X(n + 1)) >> 4));
 	if (!(len & 1)) X(last) = TR(sh, X(last) + (X(last - 1) >> 3));

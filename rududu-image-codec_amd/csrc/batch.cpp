@@ -294,7 +294,8 @@ int gpu_encode_plane(ric_batch* b, int set, int n, int p, const uint8_t* const* 
 		fused[l] = mode != FQ_NONE;
 		auto sp = b->prof.begin(B_FWD + std::min(l, 7), n, b->st);
 		if (mode == FQ_PACKED) {
-			if (launch_fwdq_level_z(P, l, fr, vec8, vec16, qp, b->zf[set][l], b->st)) return RIC_E_HIP;
+			// the batch's planes are 8-bit pixels after the level shift (in8)
+			if (launch_fwdq_level_z(P, l, fr, vec8, vec16, qp, b->zf[set][l], b->st, 1)) return RIC_E_HIP;
 		} else if (mode == FQ_GENERIC) {
 			const bool coarsest = l + 1 == P.nlev;
 			int llQ = 0, lliQ = 0, llT0 = 0;

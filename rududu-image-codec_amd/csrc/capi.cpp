@@ -250,7 +250,9 @@ int quantize_gpu(ric_wavelet* w, int quant, int lambda)
 // Transform + the GPU half of CodeBand in one pass over the pyramid: every 9/7
 // short level runs the fused forward+quantiser (dwt.hip k_fwdq), the others the
 // separate forward level, quantiser and record kernels.
-int encode_gpu(ric_wavelet* w, const int16_t* dimg, long stride, int trans, int quant, int lambda)
+// in8: dimg holds 8-bit pixels after the ric level shift (the codec's own
+// planes), so level 0 may take the plain packed mult08 (ric_kernels.h)
+int encode_gpu(ric_wavelet* w, const int16_t* dimg, long stride, int trans, int quant, int lambda, bool in8 = false)
 {
 	Pyramid& P = w->P;
 	bool fused[kMaxLevels] = {};
@@ -274,7 +276,7 @@ int encode_gpu(ric_wavelet* w, const int16_t* dimg, long stride, int trans, int 
 		fused[l] = mode != FQ_NONE;
 		if (l == 0) w->prof.begin(S_FWD0, w->st);
 		if (mode == FQ_PACKED) {
-			launch_fwdq_level(P, l, src, sp, vec8, vec16, qp, w->d_arena, w->st);
+			launch_fwdq_level(P, l, src, sp, vec8, vec16, qp, w->d_arena, w->st, in8 ? 1 : 0);
 		} else if (mode == FQ_GENERIC) {
 			const bool coarsest = l + 1 == P.nlev;
 			int llQ = 0, lliQ = 0, llT0 = 0;
@@ -941,7 +943,7 @@ int ric_codec_encode(ric_codec* c, const uint8_t* pix, int on_device, int q, int
 				HIPCHK(hipGetLastError());
 			}
 			int rc = encode_gpu(w, c->d_planes + p * plane, c->pitch, trans,
-			                    q ? ric_quants(q + 20 + boost) : 0, q ? ric_quants(q + 13 + boost) : 0);
+			                    q ? ric_quants(q + 20 + boost) : 0, q ? ric_quants(q + 13 + boost) : 0, true);
 			if (rc) return rc;
 			// the copy runs inside the section too: its blit kernels would
 			// otherwise share the CUs with another codec's level kernels

@@ -338,6 +338,26 @@ __device__ __forceinline__ v2s mult08p(v2s a)     // CWavelet2D::mult08 on short
 	a = a + (a >> 4);
 	return a + (a >> 8);
 }
+// CWavelet2D::mult08 on a SUM: the template deduces C = int (mult08(i[1] +
+// i[3]), src/lib/wavelet2d.cpp:336, 344, 353, 372, 381, 443, 548, ...), so the
+// sum keeps its 17th bit and the steps run in int; only mult08 of a single
+// element runs on short.  mult08p of the 16-bit wrapped sum s' = s - 65536 w
+// is exact in 16 bits (no step wraps for |s'| <= 32768) and equals the int
+// result minus 52428 w (every step divides the wrap exactly: 65536 / 4,
+// 49152 / 16, 52224 / 256), so a wrapped add is corrected by +-52428.
+__device__ __forceinline__ v2s mult08x(v2s a, v2s b)
+{
+	const v2s s = a + b;
+	const uint32_t ov = ~(as_u32(a) ^ as_u32(b)) & (as_u32(a) ^ as_u32(s));   // sign bits: the add wrapped
+	const v2s m = as_v2(ov) >> 15;                                          // -1 where it did
+	const v2s sg = a >> 15;                                                  // -1: wrapped downwards
+	const v2s c = (as_v2(0xCCCCCCCCu) ^ sg) - sg;                            // +52428 / -52428 (mod 2^16)
+	return mult08p(s) + as_v2(as_u32(c) & as_u32(m));
+}
+// X: the exact form; !X: the plain 16-bit sum, for a level whose input range
+// keeps every such sum within 16 bits (level 0 of 8-bit pixels: |x| <= 2048
+// bounds the argument by 12902, the l1 norm of its linear map times 2048)
+template <bool X> __device__ __forceinline__ v2s m08s(v2s a, v2s b) { return X ? mult08x(a, b) : mult08p(a + b); }
 __device__ __forceinline__ v2s mul3(v2s a) { return a + a + a; }
 
 // per-lane boundary masks (16-bit halves) for the row steps
@@ -388,10 +408,8 @@ __device__ __forceinline__ void row_fwd97p(PRow& r, const EdgeMasks& m)
 	if (EDGE) a = sel(m.oR, E >> 3, a);
 	O = O - a;
 	OL = left_odd(O);                                       // P2 (even)
-	v2s arg = OL + O;
-	if (EDGE) arg = sel(m.eAny, sel(m.eL, O, OL), arg);
-	v2s mm = mult08p(arg);
-	if (EDGE) mm = sel(m.eAny, mm + mm, mm);
+	v2s mm = mult08x(OL, O);
+	if (EDGE) { v2s me = mult08p(sel(m.eL, O, OL)); mm = sel(m.eAny, me + me, mm); }
 	E = E + mm;
 	ER = right_even(E);                                     // U2 (odd)
 	t = E + ER;
@@ -412,10 +430,8 @@ __device__ __forceinline__ void row_inv97p(PRow& r, const EdgeMasks& m)
 	if (EDGE) d = sel(m.oR, E - (E >> 4), d);
 	O = O - d;
 	v2s OL = left_odd(O);                                   // P2^-1 (even)
-	v2s arg = OL + O;
-	if (EDGE) arg = sel(m.eAny, sel(m.eL, O, OL), arg);
-	v2s mm = mult08p(arg);
-	if (EDGE) mm = sel(m.eAny, mm + mm, mm);
+	v2s mm = mult08x(OL, O);
+	if (EDGE) { v2s me = mult08p(sel(m.eL, O, OL)); mm = sel(m.eAny, me + me, mm); }
 	E = E - mm;
 	ER = right_even(E);                                     // U1^-1 (odd)
 	v2s a = avg16(E, ER);
@@ -446,10 +462,11 @@ __device__ __forceinline__ void row_fwd97p2(PRow& r, PRow& q, const EdgeMasks& m
 	if (EDGE) { a = sel(m.oR, E >> 3, a); b = sel(m.oR, F >> 3, b); }
 	O = O - a; P = P - b;
 	OL = left_odd(O); PL = left_odd(P);                     // P2 (even)
-	v2s arg = OL + O, arg2 = PL + P;
-	if (EDGE) { arg = sel(m.eAny, sel(m.eL, O, OL), arg); arg2 = sel(m.eAny, sel(m.eL, P, PL), arg2); }
-	v2s mm = mult08p(arg), mm2 = mult08p(arg2);
-	if (EDGE) { mm = sel(m.eAny, mm + mm, mm); mm2 = sel(m.eAny, mm2 + mm2, mm2); }
+	v2s mm = mult08x(OL, O), mm2 = mult08x(PL, P);
+	if (EDGE) {
+		v2s me = mult08p(sel(m.eL, O, OL)), me2 = mult08p(sel(m.eL, P, PL));
+		mm = sel(m.eAny, me + me, mm); mm2 = sel(m.eAny, me2 + me2, mm2);
+	}
 	E = E + mm; F = F + mm2;
 	ER = right_even(E); FR = right_even(F);                 // U2 (odd)
 	t = E + ER; u = F + FR;
@@ -469,10 +486,11 @@ __device__ __forceinline__ void row_inv97p2(PRow& r, PRow& q, const EdgeMasks& m
 	if (EDGE) { d = sel(m.oR, E - (E >> 4), d); d2 = sel(m.oR, F - (F >> 4), d2); }
 	O = O - d; P = P - d2;
 	v2s OL = left_odd(O), PL = left_odd(P);                 // P2^-1 (even)
-	v2s arg = OL + O, arg2 = PL + P;
-	if (EDGE) { arg = sel(m.eAny, sel(m.eL, O, OL), arg); arg2 = sel(m.eAny, sel(m.eL, P, PL), arg2); }
-	v2s mm = mult08p(arg), mm2 = mult08p(arg2);
-	if (EDGE) { mm = sel(m.eAny, mm + mm, mm); mm2 = sel(m.eAny, mm2 + mm2, mm2); }
+	v2s mm = mult08x(OL, O), mm2 = mult08x(PL, P);
+	if (EDGE) {
+		v2s me = mult08p(sel(m.eL, O, OL)), me2 = mult08p(sel(m.eL, P, PL));
+		mm = sel(m.eAny, me + me, mm); mm2 = sel(m.eAny, me2 + me2, mm2);
+	}
 	E = E - mm; F = F - mm2;
 	ER = right_even(E); FR = right_even(F);                 // U1^-1 (odd)
 	v2s a = avg16(E, ER), b = avg16(F, FR);
@@ -598,7 +616,7 @@ __device__ __forceinline__ void fwd_seg(const FwdArgs<TI, TO>& a, int x, int lan
 				else { FOR4 { int t = tr<SH>(w3[j] + w5[j]); w4[j] = tr<SH>(w4[j] - (t + (t >> 1))); } }
 				if (FAST || e >= 1) { FOR4 w3[j] = tr<SH>(w3[j] - ((w2[j] + w4[j]) >> 4)); }
 				if (!FAST && e == 2) { FOR4 w2[j] = tr<SH>(w2[j] + 2 * mult08<SH>(w3[j])); }
-				else if (FAST || e >= 4) { FOR4 w2[j] = tr<SH>(w2[j] + mult08<SH>(w1[j] + w3[j])); }
+				else if (FAST || e >= 4) { FOR4 w2[j] = tr<SH>(w2[j] + mult08<false>(w1[j] + w3[j])); }
 				if (FAST || e >= 4) { FOR4 { int t = tr<SH>(w0[j] + w2[j]); w1[j] = tr<SH>(w1[j] + ((t >> 1) - (t >> 5))); } }
 			} else {
 				// P at e, U at e-1 (src/lib/wavelet2d.cpp:654-668)
@@ -615,7 +633,7 @@ __device__ __forceinline__ void fwd_seg(const FwdArgs<TI, TO>& a, int x, int lan
 			if (!(H & 1)) {
 				if constexpr (TRANS == CDF97) {      // src/lib/wavelet2d.cpp:476-491
 					FOR4 w3[j] = tr<SH>(w3[j] - (w2[j] >> 3));
-					FOR4 w2[j] = tr<SH>(w2[j] + mult08<SH>(w1[j] + w3[j]));
+					FOR4 w2[j] = tr<SH>(w2[j] + mult08<false>(w1[j] + w3[j]));
 					FOR4 { int t = tr<SH>(w0[j] + w2[j]); w1[j] = tr<SH>(w1[j] + ((t >> 1) - (t >> 5))); }
 					FOR4 w3[j] = tr<SH>(w3[j] + (w2[j] - (w2[j] >> 4)));
 				} else {                              // src/lib/wavelet2d.cpp:685-691
@@ -736,7 +754,7 @@ __device__ __forceinline__ void fwd97p_seg(const FwdArgs<int16_t, int16_t>& a, i
 			v2s me = mult08p(w3.e), mo = mult08p(w3.o);
 			w2.e += me + me; w2.o += mo + mo;
 		} else if (FAST || e >= 4) {
-			w2.e += mult08p(w1.e + w3.e); w2.o += mult08p(w1.o + w3.o);
+			w2.e += mult08x(w1.e, w3.e); w2.o += mult08x(w1.o, w3.o);
 		}
 		if (FAST || e >= 4) {
 			v2s te = w0.e + w2.e, to = w0.o + w2.o;
@@ -750,7 +768,7 @@ __device__ __forceinline__ void fwd97p_seg(const FwdArgs<int16_t, int16_t>& a, i
 	if (!FAST && y0 + S + 4 >= H) {
 		if (!(H & 1)) {                              // src/lib/wavelet2d.cpp:476-491
 			w3.e -= w2.e >> 3; w3.o -= w2.o >> 3;
-			w2.e += mult08p(w1.e + w3.e); w2.o += mult08p(w1.o + w3.o);
+			w2.e += mult08x(w1.e, w3.e); w2.o += mult08x(w1.o, w3.o);
 			v2s te = w0.e + w2.e, to = w0.o + w2.o;
 			w1.e += (te >> 1) - (te >> 5); w1.o += (to >> 1) - (to >> 5);
 			w3.e += w2.e - (w2.e >> 4); w3.o += w2.o - (w2.o >> 4);
@@ -833,6 +851,7 @@ struct FqArgs {
 	int level;
 	int* err;                          // device error word (ring hand-off timeout), or null
 	int fault;                         // fault injection (ric_diag_fault): force a ring timeout
+	int in8;                           // the level's input is 8-bit pixels (|x| <= 2048): plain 16-bit mult08 sums
 };
 
 struct PRow8 { v2s q[4]; };            // (c0,c2) (c4,c6) | (c1,c3) (c5,c7)
@@ -860,6 +879,7 @@ __device__ __forceinline__ void right_even8(const PRow8& r, v2s& r0, v2s& r1)
 }
 
 // TransLine97 (src/lib/wavelet2d.cpp:320-359) on two interior rows at once
+template <bool X>
 __device__ __forceinline__ void row_fwd97p8x2(PRow8& r, PRow8& s)
 {
 	v2s a0, a1, b0, b1, t;
@@ -872,8 +892,8 @@ __device__ __forceinline__ void row_fwd97p8x2(PRow8& r, PRow8& s)
 	r.q[2] -= avg16(r.q[0], a0); s.q[2] -= avg16(s.q[0], b0);
 	r.q[3] -= avg16(r.q[1], a1); s.q[3] -= avg16(s.q[1], b1);
 	left_odd8(r, a0, a1); left_odd8(s, b0, b1);                   // P2 (even)
-	r.q[0] += mult08p(a0 + r.q[2]); s.q[0] += mult08p(b0 + s.q[2]);
-	r.q[1] += mult08p(a1 + r.q[3]); s.q[1] += mult08p(b1 + s.q[3]);
+	r.q[0] += m08s<X>(a0, r.q[2]); s.q[0] += m08s<X>(b0, s.q[2]);
+	r.q[1] += m08s<X>(a1, r.q[3]); s.q[1] += m08s<X>(b1, s.q[3]);
 	right_even8(r, a0, a1); right_even8(s, b0, b1);               // U2 (odd)
 	t = r.q[0] + a0; r.q[2] += (t >> 1) - (t >> 5);
 	t = s.q[0] + b0; s.q[2] += (t >> 1) - (t >> 5);
@@ -996,6 +1016,7 @@ struct FqBorder {
 // TransLine97 with the left/right boundary formulas (src/lib/wavelet2d.cpp:
 // 326-358: x0 -= 3 x1 at column 0, 2 mult08 at column 0 for P2, the odd last
 // column from its left neighbour only), two rows at once
+template <bool X>
 __device__ __forceinline__ void row_fwd97p8x2_edge(PRow8& r, PRow8& s, const FqBorder& m)
 {
 	v2s a0, a1, b0, b1, t, u;
@@ -1009,9 +1030,9 @@ __device__ __forceinline__ void row_fwd97p8x2_edge(PRow8& r, PRow8& s, const FqB
 	r.q[3] -= sel(m.oR3, r.q[1] >> 3, avg16(r.q[1], a1));
 	s.q[3] -= sel(m.oR3, s.q[1] >> 3, avg16(s.q[1], b1));
 	left_odd8(r, a0, a1); left_odd8(s, b0, b1);                   // P2 (even)
-	t = mult08p(sel(m.eL0, r.q[2], a0 + r.q[2])); r.q[0] += sel(m.eL0, t + t, t);
-	u = mult08p(sel(m.eL0, s.q[2], b0 + s.q[2])); s.q[0] += sel(m.eL0, u + u, u);
-	r.q[1] += mult08p(a1 + r.q[3]); s.q[1] += mult08p(b1 + s.q[3]);
+	t = mult08p(r.q[2]); r.q[0] += sel(m.eL0, t + t, m08s<X>(a0, r.q[2]));
+	u = mult08p(s.q[2]); s.q[0] += sel(m.eL0, u + u, m08s<X>(b0, s.q[2]));
+	r.q[1] += m08s<X>(a1, r.q[3]); s.q[1] += m08s<X>(b1, s.q[3]);
 	right_even8(r, a0, a1); right_even8(s, b0, b1);               // U2 (odd)
 	t = r.q[0] + a0; r.q[2] += (t >> 1) - (t >> 5);
 	u = s.q[0] + b0; s.q[2] += (u >> 1) - (u >> 5);
@@ -1078,7 +1099,7 @@ struct NoStage {
 
 // stage(): called once the prologue row loads are in flight (k_fwdq_pc
 // stages the format tables there, so their latency overlaps the loads')
-template <bool EDGE, bool PC = false, typename Stage = NoStage>
+template <bool EDGE, bool PC = false, bool X = true, typename Stage = NoStage>
 __device__ __forceinline__ void fq_seg(const FqArgs& a, const int (*thr)[16], const uint32_t (*tpk)[17 * 8],
                                        const FqTables& F, int x, int lane, int y0, int kx, const FqBorder& m, int S,
                                        uint2 (*pcbuf)[3][4][kLanes] = nullptr, int dbg = 0, uint64_t* tr = nullptr,
@@ -1174,8 +1195,8 @@ __device__ __forceinline__ void fq_seg(const FqArgs& a, const int (*thr)[16], co
 			load_next(rg[2 * k]);
 			load_next(rg[2 * k + 1]);
 			if (EDGE && e < 0) continue;                 // above the image (top segment)
-			if (EDGE) row_fwd97p8x2_edge(w4, w5, m);
-			else row_fwd97p8x2(w4, w5);
+			if (EDGE) row_fwd97p8x2_edge<X>(w4, w5, m);
+			else row_fwd97p8x2<X>(w4, w5);
 			// P1 at e, U1 at e-1, P2 at e-2, U2 at e-3 (src/lib/wavelet2d.cpp:425-454)
 			if (EDGE && e == 0) {
 #pragma unroll
@@ -1193,7 +1214,7 @@ __device__ __forceinline__ void fq_seg(const FqArgs& a, const int (*thr)[16], co
 				for (int q = 0; q < 4; q++) { v2s t = mult08p(w3.q[q]); w2.q[q] += t + t; }
 			} else if (!EDGE || e >= 4) {
 #pragma unroll
-				for (int q = 0; q < 4; q++) w2.q[q] += mult08p(w1.q[q] + w3.q[q]);
+				for (int q = 0; q < 4; q++) w2.q[q] += m08s<X>(w1.q[q], w3.q[q]);
 			}
 			if (!EDGE || e >= 4) {
 #pragma unroll
@@ -1207,7 +1228,7 @@ __device__ __forceinline__ void fq_seg(const FqArgs& a, const int (*thr)[16], co
 #pragma unroll
 			for (int q = 0; q < 4; q++) {
 				w3.q[q] -= w2.q[q] >> 3;
-				w2.q[q] += mult08p(w1.q[q] + w3.q[q]);
+				w2.q[q] += m08s<X>(w1.q[q], w3.q[q]);
 				const v2s t = w0.q[q] + w2.q[q];
 				w1.q[q] += (t >> 1) - (t >> 5);
 				w3.q[q] += w2.q[q] - (w2.q[q] >> 4);
@@ -1378,7 +1399,7 @@ constexpr int kWgTraceMax = 8192;
 // producers on distinct SIMDs by HW_ID made no measurable difference, and a
 // role known before the first barrier lets the producer issue its prologue
 // row loads before the workgroup stages the format tables.
-template <bool ASYNC>
+template <bool ASYNC, bool X = true>
 __device__ __forceinline__ void fwdq_pc_body(const FqArgs& a, int S, int dbg)
 {
 	__shared__ int s_thres[3][16];
@@ -1429,10 +1450,10 @@ __device__ __forceinline__ void fwdq_pc_body(const FqArgs& a, int S, int dbg)
 			m.eL0 = x == 0 ? 0x0000FFFFu : 0u;
 			m.oR3 = x + 7 == a.W - 1 ? 0xFFFF0000u : 0u;
 			m.ld = x >= 0 && x < a.W;
-			fq_seg<true, true>(a, s_thres, s_tpk, s_F, x, lane, y0, kx, m, S, s_buf, dbg, wgt ? wgt + 8 : nullptr, stage,
+			fq_seg<true, true, X>(a, s_thres, s_tpk, s_F, x, lane, y0, kx, m, S, s_buf, dbg, wgt ? wgt + 8 : nullptr, stage,
 			                   ASYNC ? s_ring : nullptr);
 		} else {
-			fq_seg<false, true>(a, s_thres, s_tpk, s_F, x, lane, y0, kx, m, S, s_buf, dbg, wgt ? wgt + 8 : nullptr, stage,
+			fq_seg<false, true, X>(a, s_thres, s_tpk, s_F, x, lane, y0, kx, m, S, s_buf, dbg, wgt ? wgt + 8 : nullptr, stage,
 			                    ASYNC ? s_ring : nullptr);
 		}
 	} else {
@@ -1466,12 +1487,13 @@ __device__ __forceinline__ void fwdq_pc_body(const FqArgs& a, int S, int dbg)
 // One frame (arguments by value), or a batch of frames: blockIdx.z = frame,
 // per-frame arguments from a device array (their pointers differ), so the
 // levels of many frames run as one grid.
-template <bool ASYNC>
-__global__ void __launch_bounds__(256, 4) k_fwdq_pc(FqArgs a, int S, int dbg) { fwdq_pc_body<ASYNC>(a, S, dbg); }
-template <bool ASYNC>
+// X: exact mult08 sums (m08s); !X only for 8-bit-pixel input (FqArgs::in8)
+template <bool ASYNC, bool X>
+__global__ void __launch_bounds__(256, 4) k_fwdq_pc(FqArgs a, int S, int dbg) { fwdq_pc_body<ASYNC, X>(a, S, dbg); }
+template <bool ASYNC, bool X>
 __global__ void __launch_bounds__(256, 4) k_fwdq_pc_z(const FqArgs* __restrict__ az, int S, int dbg)
 {
-	fwdq_pc_body<ASYNC>(az[blockIdx.z], S, dbg);
+	fwdq_pc_body<ASYNC, X>(az[blockIdx.z], S, dbg);
 }
 
 // ------------------------------------ two-producer fused level (k_fwdq_pc2)
@@ -1564,7 +1586,7 @@ __device__ __forceinline__ void fq2_producer(const FqArgs& a, int x, int lane, i
 				v2s me = mult08p(w3.e), mo = mult08p(w3.o);
 				w2.e += me + me; w2.o += mo + mo;
 			} else if (!EDGE || e >= 4) {
-				w2.e += mult08p(w1.e + w3.e); w2.o += mult08p(w1.o + w3.o);
+				w2.e += mult08x(w1.e, w3.e); w2.o += mult08x(w1.o, w3.o);
 			}
 			if (!EDGE || e >= 4) {
 				v2s te = w0.e + w2.e, to = w0.o + w2.o;
@@ -1576,7 +1598,7 @@ __device__ __forceinline__ void fq2_producer(const FqArgs& a, int x, int lane, i
 		if (EDGE && last && mb.bottom) {
 			// even H: the window holds rows H-4 .. H-1 (src/lib/wavelet2d.cpp:476-491)
 			w3.e -= w2.e >> 3; w3.o -= w2.o >> 3;
-			w2.e += mult08p(w1.e + w3.e); w2.o += mult08p(w1.o + w3.o);
+			w2.e += mult08x(w1.e, w3.e); w2.o += mult08x(w1.o, w3.o);
 			v2s te = w0.e + w2.e, to = w0.o + w2.o;
 			w1.e += (te >> 1) - (te >> 5); w1.o += (to >> 1) - (to >> 5);
 			w3.e += w2.e - (w2.e >> 4); w3.o += w2.o - (w2.o >> 4);
@@ -1764,8 +1786,9 @@ void fq_launch_pc(FqArgs& a, hipStream_t st)
 		static const int async = [] { const char* e = getenv("RIC_FQ_ASYNC"); return e ? atoi(e) : 1; }();
 		const dim3 grid = onewg ? dim3(1, 1) : dim3(nstrip, a.nseg);
 		if (onewg) dbg |= 4;
-		if (async) hipLaunchKernelGGL(k_fwdq_pc<true>, grid, dim3(256), 0, st, a, S, dbg & ~128);
-		else hipLaunchKernelGGL(k_fwdq_pc<false>, grid, dim3(256), 0, st, a, S, dbg);
+		if (async && a.in8) hipLaunchKernelGGL((k_fwdq_pc<true, false>), grid, dim3(256), 0, st, a, S, dbg & ~128);
+		else if (async) hipLaunchKernelGGL((k_fwdq_pc<true, true>), grid, dim3(256), 0, st, a, S, dbg & ~128);
+		else hipLaunchKernelGGL((k_fwdq_pc<false, true>), grid, dim3(256), 0, st, a, S, dbg);
 	}
 }
 
@@ -2137,7 +2160,7 @@ __device__ __forceinline__ void inv_seg(const InvArgs<TB, TL, TO>& a, int x, int
 				// (src/lib/wavelet2d.cpp:512-561)
 				if (FAST || e >= 2) { FOR4 { int t = tr<SH>(w3[j] + w5[j]); w4[j] = tr<SH>(w4[j] - ((t >> 1) - (t >> 5))); } }
 				if (!FAST && e == 2) { FOR4 w3[j] = tr<SH>(w3[j] - 2 * mult08<SH>(w4[j])); }
-				else if (FAST || e >= 4) { FOR4 w3[j] = tr<SH>(w3[j] - mult08<SH>(w2[j] + w4[j])); }
+				else if (FAST || e >= 4) { FOR4 w3[j] = tr<SH>(w3[j] - mult08<false>(w2[j] + w4[j])); }
 				if (FAST || e >= 4) { FOR4 w2[j] = tr<SH>(w2[j] + ((w1[j] + w3[j]) >> 4)); }
 				if (!FAST && e == 4) { FOR4 w1[j] = tr<SH>(w1[j] + w2[j] * 3); }
 				else if (FAST || e >= 6) { FOR4 { int t = tr<SH>(w0[j] + w2[j]); w1[j] = tr<SH>(w1[j] + (t + (t >> 1))); } }
@@ -2155,7 +2178,7 @@ __device__ __forceinline__ void inv_seg(const InvArgs<TB, TL, TO>& a, int x, int
 			if (!(H & 1)) {                      // rows H-5 .. H-1
 				if constexpr (TRANS == CDF97) {  // src/lib/wavelet2d.cpp:572-587
 					FOR4 w4[j] = tr<SH>(w4[j] - (w3[j] - (w3[j] >> 4)));
-					FOR4 w3[j] = tr<SH>(w3[j] - mult08<SH>(w2[j] + w4[j]));
+					FOR4 w3[j] = tr<SH>(w3[j] - mult08<false>(w2[j] + w4[j]));
 					FOR4 w2[j] = tr<SH>(w2[j] + ((w1[j] + w3[j]) >> 4));
 					FOR4 w4[j] = tr<SH>(w4[j] + (w3[j] >> 3));
 					if (H == 4) { FOR4 w1[j] = tr<SH>(w1[j] + w2[j] * 3); }
@@ -2304,7 +2327,7 @@ __device__ __forceinline__ void inv97p_seg(const InvArgs<int16_t, int16_t, int16
 			v2s me = mult08p(w4.e), mo = mult08p(w4.o);
 			w3.e -= me + me; w3.o -= mo + mo;
 		} else if (FAST || e >= 4) {
-			w3.e -= mult08p(w2.e + w4.e); w3.o -= mult08p(w2.o + w4.o);
+			w3.e -= mult08x(w2.e, w4.e); w3.o -= mult08x(w2.o, w4.o);
 		}
 		if (FAST || e >= 4) { w2.e += avg16(w1.e, w3.e); w2.o += avg16(w1.o, w3.o); }
 		if (!FAST && e == 4) { w1.e += mul3(w2.e); w1.o += mul3(w2.o); }
@@ -2336,7 +2359,7 @@ __device__ __forceinline__ void inv97p_seg(const InvArgs<int16_t, int16_t, int16
 	if (!FAST && y0 + S + 4 >= H) {
 		if (!(H & 1)) {                              // src/lib/wavelet2d.cpp:572-587
 			w4.e -= w3.e - (w3.e >> 4); w4.o -= w3.o - (w3.o >> 4);
-			w3.e -= mult08p(w2.e + w4.e); w3.o -= mult08p(w2.o + w4.o);
+			w3.e -= mult08x(w2.e, w4.e); w3.o -= mult08x(w2.o, w4.o);
 			w2.e += avg16(w1.e, w3.e); w2.o += avg16(w1.o, w3.o);
 			w4.e += w3.e >> 3; w4.o += w3.o >> 3;
 			if (H == 4) { w1.e += mul3(w2.e); w1.o += mul3(w2.o); }
@@ -2565,10 +2588,11 @@ FqArgs fq_args(const Pyramid& P, int l, const void* src, long sp, int vec8, int 
 }  // namespace
 
 void launch_fwdq_level(const Pyramid& P, int l, const void* src, long sp, int vec8, int vec16, const QuantParams& qp,
-                       char* arena, hipStream_t st)
+                       char* arena, hipStream_t st, int in8)
 {
 	const Level& L = P.L[l];
 	FqArgs a = fq_args(P, l, src, sp, vec8, vec16, qp, arena, false);
+	a.in8 = in8 && l == 0;
 	if (fq_pc()) { fq_launch_pc(a, st); return; }
 	const int S = fq_seg_rows(L.h);
 	if (S == 32) fq_launch_s<32>(a, st);
@@ -2650,7 +2674,7 @@ int pc_seg_rows_z(int W, int H, int nz, int level)
 }  // namespace
 
 int launch_fwdq_level_z(const Pyramid& P, int l, const ZFrames& fr, int vec8, int vec16, const QuantParams& qp,
-                        ZArgs& z, hipStream_t st)
+                        ZArgs& z, hipStream_t st, int in8)
 {
 	const Level& L = P.L[l];
 	const int S = pc_seg_rows_z(L.w, L.h, fr.nz, l);
@@ -2665,7 +2689,8 @@ int launch_fwdq_level_z(const Pyramid& P, int l, const ZFrames& fr, int vec8, in
 	// the one-producer form on level 0 (VALU-bound), two producers above (see
 	// fq_launch_pc); knob RIC_FQZ_PC1 = the last level on one producer
 	static const int pc1 = [] { const char* e = getenv("RIC_FQZ_PC1"); return e ? atoi(e) : 0; }();
-	if (l <= pc1) hipLaunchKernelGGL(k_fwdq_pc_z<true>, grid, dim3(256), 0, st, d, S, 0);
+	if (l <= pc1 && l == 0 && in8) hipLaunchKernelGGL((k_fwdq_pc_z<true, false>), grid, dim3(256), 0, st, d, S, 0);
+	else if (l <= pc1) hipLaunchKernelGGL((k_fwdq_pc_z<true, true>), grid, dim3(256), 0, st, d, S, 0);
 	else hipLaunchKernelGGL(k_fwdq_pc2_z<true>, grid, dim3(320), 0, st, d, S, 0);
 	return 0;
 }

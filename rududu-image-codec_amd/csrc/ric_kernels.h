@@ -20,8 +20,12 @@ struct QuantParams;
 // separate forward / quantiser / record kernels (5/3, Haar).
 enum { FQ_NONE = 0, FQ_PACKED = 1, FQ_GENERIC = 2 };
 int fwdq_mode(const Level& L, int trans, const QuantParams& qp, int vec16);
+// in8: the level-0 input is 8-bit pixels after the ric level shift (|x| <=
+// 2048), which bounds every mult08 sum to 16 bits and allows the plain packed
+// form at level 0; any other input (the API's Transform, the video residual)
+// takes the exact form (dwt.hip mult08x).
 void launch_fwdq_level(const Pyramid& P, int l, const void* src, long sp, int vec8, int vec16, const QuantParams& qp,
-                       char* arena, hipStream_t st);
+                       char* arena, hipStream_t st, int in8 = 0);
 // Generic fused forward level + quantiser + records (dwt.hip k_fwdq_gen) for
 // any 9/7 level (int bands, odd sizes); ll_on: also CBand::TSUQ on the level's
 // LL (the coarsest level), with its iQ and dead zone T0.
@@ -76,7 +80,7 @@ void zargs_free(ZArgs& z);
 // launch_inv_level; 0 or -1 (HIP error).  The inverse takes 4 TSUQi factors
 // per frame (q + 4 f), or none.
 int launch_fwdq_level_z(const Pyramid& P, int l, const ZFrames& fr, int vec8, int vec16, const QuantParams& qp,
-                        ZArgs& z, hipStream_t st);
+                        ZArgs& z, hipStream_t st, int in8 = 0);
 int launch_fwdq_gen_level_z(const Pyramid& P, int l, const ZFrames& fr, int vec8, const QuantParams& qp, int ll_on,
                             int ll_iQ, int ll_T0, ZArgs& z, hipStream_t st);
 int launch_inv_level_z(const Level& L, const Band& lls, const ZFrames& fr, int out_is_int, int trans, const int* q,

@@ -243,3 +243,40 @@ def test_device_resident_buffers(ric, port):
     c.decompress(r, pix_out=out)
     torch.cuda.synchronize()
     assert np.array_equal(out.cpu().numpy(), port.decode_ric(r)[0])
+
+
+@pytest.mark.parametrize("kind", ["uniform", "alt", "ramp"])
+@pytest.mark.parametrize("w,h", [(64, 48), (96, 64), (129, 77), (256, 128)])
+@pytest.mark.parametrize("t", [0, 1])
+def test_full_range_planes(ric, port, kind, w, h, t):
+    """Planes whose 9/7 lifting sums leave 16 bits (the video residual, any
+    API caller): mult08 of a sum runs in int in the reference
+    (src/lib/wavelet2d.cpp:336 deduces C = int), so every kernel takes the
+    exact form (dwt.hip mult08x).  Forward (unfused k_fwd and the fused
+    packed/generic kernels), buildTree and the closed loop's inverse."""
+    pl = O.full_range_plane(w, h, w * h, kind)
+    for L, lc in [(3, 0), (5, 1)]:
+        W = ric.Wavelet2D(w, h, L, lc)
+        W.SetWeight(t)
+        W.Transform(pl, w, t)
+        for a, b in zip(W.bands(), port.bands(pl, L, lc, t, 0)):
+            assert np.array_equal(a, b), ("stage 0", L, lc)
+        W = ric.Wavelet2D(w, h, L, lc)
+        W.SetWeight(t)
+        W.TransformQuantize(pl, w, t, 96, 36)
+        for a, b in zip(W.bands(), port.bands(pl, L, lc, t, 1, 96, 36)):
+            assert np.array_equal(a, b), ("stage 1", L, lc)
+        exp_plane, exp_bands = port.closed_loop(pl, L, lc, t, 84, 0, 84)
+        W = ric.Wavelet2D(w, h, L, lc)
+        W.SetWeight(t)
+        W.Transform(pl, w, t)
+        buf = np.zeros(w * h * 8 + 4096, np.uint8)
+        m = ric.MuxCodec(buf, first_word=0)
+        W.CodeBand(m, 84, 0)
+        m.endCoding()
+        W.TSUQi(84)
+        for a, b in zip(W.bands(), exp_bands):
+            assert np.array_equal(a, b), ("closed loop bands", L, lc)
+        out = np.zeros((h, w), np.int16)
+        W.TransformI(out, w, t)
+        assert np.array_equal(out, exp_plane), ("closed loop plane", L, lc)

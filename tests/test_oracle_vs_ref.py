@@ -87,3 +87,19 @@ def test_stats_restatement(w, h, t):
     wts = O.set_weight(n, t)
     for i, b in enumerate(bands):
         assert O.band_variance(b, wts[i]) == out[i], i
+
+
+@pytest.mark.parametrize("kind", ["uniform", "alt", "ramp"])
+@pytest.mark.parametrize("w,h", [(64, 48), (129, 77), (96, 64)])
+@pytest.mark.parametrize("t", [0, 1])
+def test_full_range_planes(kind, w, h, t):
+    """forward band dumps (stages 0-2) and the closed loop on planes whose
+    lifting sums leave the 16-bit range"""
+    pl = O.full_range_plane(w, h, w * h, kind)
+    for L, lc in [(3, 0), (5, 1)]:
+        for stage in (0, 1, 2):
+            for x, y in zip(O.port().bands(pl, L, lc, t, stage, 96, 36), REF.bands(pl, L, lc, t, stage, 96, 36)):
+                assert np.array_equal(x, y), (L, lc, stage)
+        a, ab = O.port().closed_loop(pl, L, lc, t, 84, 0, 84)
+        b, bb = REF.closed_loop(pl, L, lc, t, 84, 0, 84)
+        assert np.array_equal(a, b), (L, lc)
