@@ -24,6 +24,7 @@ import argparse
 import csv
 import json
 import os
+import re
 import sys
 import time
 
@@ -47,9 +48,10 @@ def kstats(path, w, h, frames, inter):
     out = {}
     for row in csv.DictReader(open(path)):
         name = row.get("Name") or row.get("KernelName") or ""
-        short = name.split("(")[0].split("<")[0].strip()
-        if not short.startswith("k_vid"):
+        mk = re.search(r"k_vid_\w+", name)
+        if not mk:
             continue
+        short = mk.group(0)
         calls = int(row["Calls"])
         avg_ns = float(row["AverageNs"])
         rec = {"calls": calls, "avg_us": round(avg_ns / 1e3, 2), "total_ms": round(calls * avg_ns / 1e6, 3)}
@@ -63,6 +65,29 @@ def kstats(path, w, h, frames, inter):
     return out
 
 
+def pmc(fetch_csv, write_csv):
+    """HBM bytes per launch from the FETCH_SIZE / WRITE_SIZE passes (KiB per
+    dispatch; MI355X_MICROARCH.md: on gfx950 FETCH_SIZE counts half the bytes
+    of a wide coalesced read, so the read side is doubled; the raw value is
+    kept; Infinity-Cache hits are counted, not excluded)."""
+    acc = {}
+    for path, key in ((fetch_csv, "FETCH_SIZE"), (write_csv, "WRITE_SIZE")):
+        for r in csv.DictReader(open(path)):
+            if r.get("Counter_Name") != key:
+                continue
+            mk = re.search(r"k_vid_\w+", r["Kernel_Name"])
+            if not mk:
+                continue
+            short = mk.group(0)
+            acc.setdefault(short, {}).setdefault(key, []).append(float(r["Counter_Value"]) * 1024)
+    out = {}
+    for k, d in acc.items():
+        f = float(np.mean(d.get("FETCH_SIZE", [0])))
+        w = float(np.mean(d.get("WRITE_SIZE", [0])))
+        out[k] = {"traffic_bytes": int(2 * f + w), "fetch_raw_bytes": int(f), "write_bytes": int(w)}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--w", type=int, default=1920)
@@ -70,10 +95,17 @@ def main():
     ap.add_argument("--frames", type=int, default=30)
     ap.add_argument("--q", type=int, default=20)
     ap.add_argument("--kstats", default=None)
+    ap.add_argument("--pmc", nargs=2, default=None, metavar=("FETCH_CSV", "WRITE_CSV"),
+                    help="counter_collection.csv of the FETCH_SIZE and WRITE_SIZE passes")
     a = ap.parse_args()
     inter = a.frames - (a.frames + 9) // 10
     if a.kstats:
-        print(json.dumps({"w": a.w, "h": a.h, "frames": a.frames, "kernels": kstats(a.kstats, a.w, a.h, a.frames, inter)}))
+        ks = kstats(a.kstats, a.w, a.h, a.frames, inter)
+        if a.pmc:
+            for k, t in pmc(a.pmc[0], a.pmc[1]).items():
+                if k in ks:
+                    ks[k].update(t)
+        print(json.dumps({"w": a.w, "h": a.h, "frames": a.frames, "kernels": ks}))
         return
     import torch
     import ric_amd
