@@ -41,6 +41,7 @@
 //              (W + 30) int16, rows and columns -15 .. +14 past the edges),
 //              and that image as CImage::outputYV12<char, false>(pOut, W,
 //              -128) writes it (W * H * 3 / 2 bytes, testmotion.cpp:62)
+#include <chrono>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -287,11 +288,17 @@ int main(int argc, char** argv)
 	dec.quant = Q;
 	const size_t fsz = (size_t)W * H * 3;
 	std::vector<unsigned char> frame(fsz), buf(fsz * 4 + 4096), dbuf(fsz * 4 + 4096);
+	// RICVID_TIME set: the encode and decode calls' wall time on stderr (the
+	// video bench's CPU baseline, scripts/video_bench.py)
+	const bool timed = getenv("RICVID_TIME") != nullptr;
+	double t_enc = 0, t_dec = 0;
 	for (int k = 0; k < N; k++) {
 		if (fread(frame.data(), 1, fsz, fi) != fsz) return 3;
 		std::fill(buf.begin(), buf.end(), 0);
 		CImage* out = 0;
+		auto t0 = std::chrono::steady_clock::now();
 		const int size = enc.encode(frame.data(), W, buf.data(), &out);
+		t_enc += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 		const uint32_t s32 = (uint32_t)size;
 		fwrite(&s32, 4, 1, fo);
 		fwrite(buf.data(), 1, size + 2, fo);
@@ -301,7 +308,9 @@ int main(int argc, char** argv)
 		std::fill(dbuf.begin(), dbuf.end(), 0);
 		memcpy(dbuf.data(), buf.data(), size + 2);
 		CImage* dout = 0;
+		t0 = std::chrono::steady_clock::now();
 		const uint32_t d32 = (uint32_t)dec.decode(dbuf.data(), &dout);
+		t_dec += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 		fwrite(&d32, 4, 1, fo);
 		put_planes(fo, dout, W, H, 0);
 		fwrite(enc.mvs(), 4, (size_t)(W >> 3) * (H >> 3), fo);
@@ -315,5 +324,6 @@ int main(int argc, char** argv)
 	}
 	fclose(fo);
 	fclose(fi);
+	if (timed) fprintf(stderr, "{\"frames\": %d, \"encode_s\": %.6f, \"decode_s\": %.6f}\n", N, t_enc, t_dec);
 	return 0;
 }

@@ -57,10 +57,12 @@ int launch_vid_extend(const VidGeom& g, const VidSubs& s, int n, hipStream_t st)
 // raster order (a wavefront over the block rows: block (i, j) needs (i - 1, j)
 // and (i + 1, j - 1)), then the quarter-pel refinement of every block.
 // mv: the motion field, read (the previous frame's vectors are predictors)
-// and rewritten; dist: scratch (u16 per block); prog: scratch (int per block
-// row, zeroed here); status: set non-zero if a wait gave up.
+// and rewritten; dist: scratch (u16 per block); gran: the rows' hand-off
+// granules (u64 per block, {vector, epoch}: zeroed once at allocation, never
+// reset); epoch: this search's tag, non-zero and different from the previous
+// search's; status: set non-zero if a wait gave up.
 int launch_vid_epzs(const VidGeom& g, const int16_t* cur, const VidSubs& ref, uint32_t* mv, uint16_t* dist,
-                    int* prog, uint32_t* status, hipStream_t st);
+                    uint64_t* gran, uint32_t epoch, uint32_t* status, hipStream_t st);
 // COBMC::apply_mv (obmc.cpp:278-332) into pred, reference frame `ref`
 int launch_vid_obmc(const VidGeom& g, const uint32_t* mv, const VidSubs& ref, int16_t* pred, hipStream_t st);
 // the samples CWavelet2D::TransformI (given the plane's end pointer) leaves

@@ -131,16 +131,24 @@ struct EpzsArgs {
 	VidSubs ref;                 // reference frame's quarter-pel planes (plane 0 used)
 	uint32_t* mv;
 	uint16_t* dist;
-	int* prog;
+	uint64_t* gran;              // per block {vector, epoch} hand-off granules
 	uint32_t* status;
+	uint32_t epoch;
 	int w, h, S, bx, by;
 };
 
+// sum over the 64 lanes, returned to every lane (uniform): DPP adds within
+// each 16-lane row, then row_bcast15 / row_bcast31 carry the row sums into
+// lane 63, read back with readlane -- no LDS round trips
 __device__ __forceinline__ int wave_sum(int v)
 {
-#pragma unroll
-	for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-	return v;
+	v += __builtin_amdgcn_update_dpp(0, v, 0xb1, 0xf, 0xf, false);    // quad_perm [1,0,3,2]
+	v += __builtin_amdgcn_update_dpp(0, v, 0x4e, 0xf, 0xf, false);    // quad_perm [2,3,0,1]
+	v += __builtin_amdgcn_update_dpp(0, v, 0x141, 0xf, 0xf, false);   // row_half_mirror
+	v += __builtin_amdgcn_update_dpp(0, v, 0x140, 0xf, 0xf, false);   // row_mirror
+	v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);   // row_bcast15 into rows 1, 3
+	v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);   // row_bcast31 into rows 2, 3
+	return __builtin_amdgcn_readlane(v, 63);
 }
 
 // one lane's sample of the 8x8 block at (px, py) after CHECK_MV's clamp
@@ -157,31 +165,48 @@ __device__ __forceinline__ int sad_of(int diff) { return min(wave_sum(diff), 655
 
 constexpr int kUp = 1, kDown = 2, kLeft = 4, kRight = 8;   // utils.h:30-35
 
+// the row above's granule k of this search (an sc1 load: it bypasses the
+// CU's L1, and the 8 bytes arrive whole), polled until its tag is this
+// search's; false once the wait gives up (~2 s) or another row has
+__device__ __forceinline__ bool await_granule(const EpzsArgs& a, const uint64_t* g, uint32_t* out, int lane)
+{
+	for (long spins = 0;; spins++) {
+		const uint64_t v = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		if ((uint32_t)(v >> 32) == a.epoch) {
+			*out = (uint32_t)v;
+			return true;
+		}
+		__builtin_amdgcn_s_sleep(1);
+		if ((spins & 255) == 255 &&
+		    (spins > (1l << 24) || __hip_atomic_load(a.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)) {
+			if (lane == 0) __hip_atomic_store(a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			return false;
+		}
+	}
+}
+
 // COBME::EPZS(CImageBuffer&) first loop (obme.cpp:185-222): one wave per block
-// row, blocks left to right; block (i, j) waits for row j - 1 to have done
-// block i + 1 (its above-right predictor).  Rows publish their progress with
-// release stores; a wait that gives up (~2 s) raises *status and ends the wave
-// (every wave reaches an exit).  The previous frame's vector of the block is
-// read before this frame's overwrites it.
+// row, blocks left to right; block (i, j) needs row j - 1's vectors i and
+// i + 1 (its above and above-right predictors).  Each block's vector is handed
+// to the row below as one data-tagged granule {vector, epoch}: an 8-byte sc1
+// store the reader polls with sc1 loads (MI355X_MICROARCH.md, handoff-1to1) --
+// no release / acquire fences, which would write back and invalidate caches
+// per block.  A wait that gives up raises *status and ends the wave (every
+// wave reaches an exit).  The previous frame's vector of the block is read
+// before this frame's overwrites it.
 __global__ __launch_bounds__(64) void k_vid_epzs_full(EpzsArgs a)
 {
 	const int j = blockIdx.x, lane = threadIdx.x;
 	const int16_t* ref = a.ref.p[0];
 	uint32_t* row = a.mv + (long)j * a.bx;
-	const uint32_t* above = row - a.bx;
-	uint32_t left = 0;
+	const uint64_t* gabove = a.gran + (long)(j - 1) * a.bx;
+	uint64_t* grow = a.gran + (long)j * a.bx;
+	uint32_t left = 0, u = 0, ur = 0;
+	if (j > 0 && !await_granule(a, gabove, &ur, lane)) return;
 	for (int i = 0; i < a.bx; i++) {
 		if (j > 0) {
-			const int need = min(i + 2, a.bx);
-			long spins = 0;
-			while (__hip_atomic_load(a.prog + j - 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < need) {
-				__builtin_amdgcn_s_sleep(4);
-				if (++spins > (1l << 24) ||
-				    __hip_atomic_load(a.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
-					if (lane == 0) __hip_atomic_store(a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-					return;
-				}
-			}
+			u = ur;                                         // above[i], received last block
+			if (i + 1 < a.bx && !await_granule(a, gabove + i + 1, &ur, lane)) return;
 		}
 		const int cx = 8 * i, cy = 8 * j;
 		const int cur = a.cur[(long)(cy + (lane >> 3)) * a.S + cx + (lane & 7)];
@@ -194,9 +219,8 @@ __global__ __launch_bounds__(64) void k_vid_epzs_full(EpzsArgs a)
 		if (j == 0) {
 			if (i != 0) cand[0] = left;
 		} else if (i == 0 || i == a.bx - 1) {
-			cand[0] = above[i];
+			cand[0] = u;
 		} else {
-			const uint32_t u = above[i], ur = above[i + 1];
 			int mx0 = mvx(left), mx1 = mvx(u), mx2 = mvx(ur), my0 = mvy(left), my1 = mvy(u), my2 = mvy(ur);
 			// median (utils.h:64-77)
 			auto med = [](int p, int q, int r) {
@@ -253,9 +277,9 @@ __global__ __launch_bounds__(64) void k_vid_epzs_full(EpzsArgs a)
 			}
 		}
 		if (lane == 0) {
+			__hip_atomic_store(grow + i, ((uint64_t)a.epoch << 32) | best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 			row[i] = best;
 			a.dist[(long)j * a.bx + i] = (uint16_t)bd;
-			__hip_atomic_store(a.prog + j, i + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 		}
 		left = best;
 	}
@@ -422,13 +446,13 @@ int launch_vid_extend(const VidGeom& g, const VidSubs& s, int n, hipStream_t st)
 	return launched();
 }
 
-int launch_vid_epzs(const VidGeom& g, const int16_t* cur, const VidSubs& ref, uint32_t* mv, uint16_t* dist, int* prog,
-                    uint32_t* status, hipStream_t st)
+int launch_vid_epzs(const VidGeom& g, const int16_t* cur, const VidSubs& ref, uint32_t* mv, uint16_t* dist,
+                    uint64_t* gran, uint32_t epoch, uint32_t* status, hipStream_t st)
 {
 	if (g.bx < 1 || g.by < 1) return 0;
-	if (hipMemsetAsync(prog, 0, sizeof(int) * g.by, st) != hipSuccess) return -1;
+	if (epoch == 0) return -1;
 	EpzsArgs a;
-	a.cur = cur; a.ref = ref; a.mv = mv; a.dist = dist; a.prog = prog; a.status = status;
+	a.cur = cur; a.ref = ref; a.mv = mv; a.dist = dist; a.gran = gran; a.epoch = epoch; a.status = status;
 	a.w = g.w; a.h = g.h; a.S = g.S; a.bx = g.bx; a.by = g.by;
 	hipLaunchKernelGGL(k_vid_epzs_full, dim3(g.by), dim3(64), 0, st, a);
 	if (launched()) return -1;

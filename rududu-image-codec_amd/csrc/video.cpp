@@ -80,7 +80,8 @@ struct ric_video {
 	int16_t* pred = nullptr;                   // predImage (its allocation start)
 	uint32_t* d_mv = nullptr;                  // the motion field (COBMC::pMV), persistent
 	uint16_t* d_dist = nullptr;
-	int* d_prog = nullptr;
+	uint64_t* d_gran = nullptr;                // EPZS hand-off granules (motion.h)
+	uint32_t epoch = 0;                        // the last EPZS search's tag
 	uint32_t* d_status = nullptr;
 	uint8_t* d_rgb = nullptr;
 	size_t rgb_cap = 0;
@@ -234,7 +235,8 @@ int ric_video_create(ric_video** out, int encoder, int w, int h, int component, 
 	if (v->alloc_image(&first) || v->alloc_image(&v->pred) ||
 	    vfail(hipMalloc(&v->d_mv, sizeof(uint32_t) * (nb + 1)), "hipMalloc") ||
 	    vfail(hipMalloc(&v->d_dist, sizeof(uint16_t) * (nb + 1)), "hipMalloc") ||
-	    vfail(hipMalloc(&v->d_prog, sizeof(int) * (v->g.by + 1)), "hipMalloc") ||
+	    vfail(hipMalloc(&v->d_gran, sizeof(uint64_t) * (nb + 1)), "hipMalloc") ||
+	    vfail(hipMemsetAsync(v->d_gran, 0, sizeof(uint64_t) * (nb + 1), v->st), "hipMemset") ||
 	    vfail(hipMalloc(&v->d_status, sizeof(uint32_t)), "hipMalloc") ||
 	    vfail(hipMemsetAsync(v->d_mv, 0, sizeof(uint32_t) * (nb + 1), v->st), "hipMemset") ||   // COBMC: memset 0 (obmc.cpp:44-45)
 	    vfail(hipMemsetAsync(v->d_status, 0, sizeof(uint32_t), v->st), "hipMemset") ||
@@ -258,7 +260,7 @@ void ric_video_destroy(ric_video* v)
 	if (v->pred) (void)hipFree(v->pred);
 	if (v->d_mv) (void)hipFree(v->d_mv);
 	if (v->d_dist) (void)hipFree(v->d_dist);
-	if (v->d_prog) (void)hipFree(v->d_prog);
+	if (v->d_gran) (void)hipFree(v->d_gran);
 	if (v->d_status) (void)hipFree(v->d_status);
 	if (v->d_rgb) (void)hipFree(v->d_rgb);
 	if (v->wav) ric_wavelet_destroy(v->wav);
@@ -300,7 +302,11 @@ int ric_video_encode(ric_video* v, const uint8_t* pix, int stride, int pix_on_de
 		rc = v->calc_sub(1);
 		if (rc) return rc;
 		const VidSubs ref = v->subs(1);
-		if (launch_vid_epzs(g, v->img(cur), ref, v->d_mv, v->d_dist, v->d_prog, v->d_status, v->st))
+		if (++v->epoch == 0) {                             // tags wrapped: clear the granules
+			VCHK(hipMemsetAsync(v->d_gran, 0, sizeof(uint64_t) * v->mv.size(), v->st));
+			v->epoch = 1;
+		}
+		if (launch_vid_epzs(g, v->img(cur), ref, v->d_mv, v->d_dist, v->d_gran, v->epoch, v->d_status, v->st))
 			return vfail(hipGetLastError(), "k_vid_epzs"), RIC_E_HIP;
 		VCHK(hipMemcpyAsync(v->mv.data(), v->d_mv, sizeof(uint32_t) * v->mv.size(), hipMemcpyDeviceToHost, v->st));
 		rc = v->sync_status();

@@ -88,12 +88,34 @@ def pmc(fetch_csv, write_csv):
     return out
 
 
+def cpu_baseline(seq, q):
+    """the reference video codec (oracle/_ref/ricvid_ref: its classes compiled
+    from the reference sources, -O2, single-threaded as the reference is) on
+    the first frames of the same sequence, encode and decode timed apart"""
+    import subprocess
+    import tempfile
+    import video_seq
+    if not os.path.exists(video_seq.REF_BIN):
+        return None
+    n, _, h, w = seq.shape
+    with tempfile.TemporaryDirectory() as d:
+        src = os.path.join(d, "seq.rgb")
+        np.ascontiguousarray(seq).tofile(src)
+        r = subprocess.run([video_seq.REF_BIN, str(w), str(h), str(q), str(n), src, "/dev/null"],
+                           env=dict(os.environ, RICVID_TIME="1"), capture_output=True, text=True, timeout=600, check=True)
+    t = json.loads(r.stderr.strip().splitlines()[-1])
+    return {"kind": "reference", "cores": 1, "frames": n, "encode_fps": round(n / t["encode_s"], 3),
+            "decode_fps": round(n / t["decode_s"], 3), "sample": "the first %d frames of the same sequence" % n}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--w", type=int, default=1920)
     ap.add_argument("--h", type=int, default=1080)
     ap.add_argument("--frames", type=int, default=30)
     ap.add_argument("--q", type=int, default=20)
+    ap.add_argument("--cpu-frames", type=int, default=10,
+                    help="frames of the same sequence through oracle/_ref/ricvid_ref (0: skip)")
     ap.add_argument("--kstats", default=None)
     ap.add_argument("--pmc", nargs=2, default=None, metavar=("FETCH_CSV", "WRITE_CSV"),
                     help="counter_collection.csv of the FETCH_SIZE and WRITE_SIZE passes")
@@ -133,7 +155,8 @@ def main():
         dec.decode(s)
     td = time.perf_counter() - t0
     mpx = a.w * a.h / 1e6
-    print(json.dumps({"workload": "video: CRududuCodec %dx%d RGB, quant %d, %d frames (key every 10)"
+    cpu = cpu_baseline(seq[:a.cpu_frames], a.q) if a.cpu_frames > 0 else None
+    print(json.dumps({"cpu_baseline": cpu,"workload": "video: CRududuCodec %dx%d RGB, quant %d, %d frames (key every 10)"
                                   % (a.w, a.h, a.q, a.frames),
                       "encode_fps": round(a.frames / te, 2), "decode_fps": round(a.frames / td, 2),
                       "encode_ms_per_frame": round(te / a.frames * 1e3, 2), "decode_ms_per_frame": round(td / a.frames * 1e3, 2),
