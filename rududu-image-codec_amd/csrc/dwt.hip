@@ -2689,7 +2689,11 @@ int launch_fwdq_level_z(const Pyramid& P, int l, const ZFrames& fr, int vec8, in
 	// the one-producer form on level 0 (VALU-bound), two producers above (see
 	// fq_launch_pc); knob RIC_FQZ_PC1 = the last level on one producer
 	static const int pc1 = [] { const char* e = getenv("RIC_FQZ_PC1"); return e ? atoi(e) : 0; }();
-	if (l <= pc1 && l == 0 && in8) hipLaunchKernelGGL((k_fwdq_pc_z<true, false>), grid, dim3(256), 0, st, d, S, 0);
+	// knob RIC_FQZ_ASYNC=0: the double-buffered hand-off (20 KiB of LDS per
+	// workgroup instead of the ring's 32 KiB)
+	static const int async = [] { const char* e = getenv("RIC_FQZ_ASYNC"); return e ? atoi(e) : 1; }();
+	if (l <= pc1 && l == 0 && in8 && !async) hipLaunchKernelGGL((k_fwdq_pc_z<false, false>), grid, dim3(256), 0, st, d, S, 0);
+	else if (l <= pc1 && l == 0 && in8) hipLaunchKernelGGL((k_fwdq_pc_z<true, false>), grid, dim3(256), 0, st, d, S, 0);
 	else if (l <= pc1) hipLaunchKernelGGL((k_fwdq_pc_z<true, true>), grid, dim3(256), 0, st, d, S, 0);
 	else hipLaunchKernelGGL(k_fwdq_pc2_z<true>, grid, dim3(320), 0, st, d, S, 0);
 	return 0;
