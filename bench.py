@@ -97,6 +97,7 @@ def parse():
     ap.add_argument("--trans", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--no-latency", action="store_true", help="skip the one-frame ric_codec latency after timing")
     ap.add_argument("--no-gather", action="store_true", help="N>1: skip the per-step stream gather to rank 0")
     ap.add_argument("--no-split", action="store_true", help="skip the encode-only / decode-only timing")
     ap.add_argument("--coder", default=None, choices=["host", "hybrid", "gpu", "mix"],
@@ -104,7 +105,8 @@ def parse():
                          "encoder and decoder (one wave per stream), host threads doing whole round trips beside it; "
                          "mix = GPU stream encoder, each launch decoded by the host threads or the GPU stream decoder "
                          "(whichever has room)")
-    ap.add_argument("--pool", type=int, default=512, help="hybrid / gpu: frames per GPU stream-coder launch")
+    ap.add_argument("--pool", type=int, default=960,
+                    help="hybrid / gpu: frames per GPU stream-coder launch (two in flight; shrunk to fit memory)")
     ap.add_argument("--launches", type=int, default=2, help="hybrid / gpu: stream-coder launches per step")
     ap.add_argument("--distinct", type=int, default=128,
                     help="distinct frames resident in HBM (inputs, outputs) and host stream buffers; a longer step cycles them")
@@ -340,9 +342,24 @@ def main():
         n_gpu = nfr - n_host if (a.frames or a.batch) else min(a.launches * a.pool, nfr - n_host)
         nstep = n_host + n_gpu
         # stream capacity: 3 bits per pixel (a q9 C3 stream is 1.7), 16-byte multiple
-        b.cp_pool = min(a.pool, max(n_gpu, 1))
+        pool = min(a.pool, max(n_gpu, 1))
         scap = (W * H * 3 // 8 + 65536) // 16 * 16
-        b.hybrid_config(b.cp_pool, scap)
+        # the pool holds bands + records + a stream per frame in flight (C3:
+        # ~110 MB): if it does not fit this GPU's memory, shrink it
+        while True:
+            try:
+                b.hybrid_config(pool, scap)
+                break
+            except ric_amd.RicError as e:
+                if e.rc != ric_amd.RIC_E_CAPACITY or pool <= 64:
+                    raise
+                print("[bench] a stream coder pool of %d frames does not fit: %d" % (pool, pool - 64),
+                      file=sys.stderr, flush=True)
+                pool -= 64
+        b.cp_pool = pool
+        if not (a.frames or a.batch):
+            n_gpu = min(a.launches * pool, nfr - n_host)
+            nstep = n_host + n_gpu
         # one host buffer per frame's .ric file (the library rejects aliased
         # buffers: host coders and the stream copier write them concurrently)
         sbufs = [np.empty(scap, np.uint8) for _ in range(nfr)]
@@ -560,6 +577,41 @@ def main():
                    "note": "GPU stages alone (ric_batch_diag_gpu), %d frames per launch, 3 iterations, after the "
                            "timed region" % slots}
 
+    # ---- one frame's latency through ric_codec (rank 0, after timing): the
+    # serial stage on one thread, and with the bands modelled in parallel
+    lat = None
+    if rank == 0 and b is not None and not a.no_latency:
+        c = ric_amd.Codec(W, H, CH)
+        want = b.stream(0)
+        enc, same = {}, True
+        for nt in sorted({1, 4, threads}):
+            c.set_host_threads(nt)
+            ts = []
+            for _ in range(4):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                r = c.compress(frames[0], a.q, a.trans, on_device=True)
+                ts.append(time.perf_counter() - t0)
+                same = same and r == want
+            enc[str(nt)] = round(float(np.median(ts[1:])) * 1e3, 2)
+        td = []
+        for _ in range(4):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            c.decompress(want, pix_out=outs[0])
+            torch.cuda.synchronize()
+            td.append(time.perf_counter() - t0)
+        lat = {"encode_ms_by_host_threads": enc, "decode_ms": round(float(np.median(td[1:])) * 1e3, 2),
+               "bytes_equal_step_frame0": bool(same),
+               "note": "one %dx%dx%d frame through ric_codec (CompressImage / DecompressImage), pixels and decoded "
+                       "output in HBM, median of 3 after one warm call, after the timed region; host threads n: the "
+                       "bands of a plane modelled on n - 1 pool threads while the calling thread writes the stream "
+                       "(ric_codec_set_host_threads); the decoder is serial" % (W, H, CH)}
+        del c
+        if not same:
+            print(json.dumps({"error": "latency codec output differs from the step's frame 0"}), file=sys.stderr)
+            sys.exit(3)
+
     # ---- encode-only and decode-only rates of the same path (rank 0, after timing)
     split = None
     if rank == 0 and b is not None and not a.no_split and not hybrid:
@@ -646,6 +698,8 @@ def main():
         out["stream_coder"] = coder
     if iso:
         out["roofline_isolated"] = iso
+    if lat:
+        out["latency"] = lat
     if gather:
         out["gather"] = {"backend": backend, "bytes_to_rank0_per_step": gathered[0]}
         if a.workload == "C4":

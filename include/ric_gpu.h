@@ -56,6 +56,7 @@ int ric_wavelet_create(ric_wavelet** out, int x, int y, int level, int level_chg
 /* CWavelet2D::~CWavelet2D (src/lib/wavelet2d.cpp:64-67) */
 void ric_wavelet_destroy(ric_wavelet* w);
 /* run this object's kernels on an existing hipStream_t (NULL: own stream) */
+int ric_wavelet_set_host_threads(ric_wavelet* w, int n);
 int ric_wavelet_set_stream(ric_wavelet* w, void* hip_stream);
 /* block until this object's queued GPU work is done */
 int ric_wavelet_sync(ric_wavelet* w);
@@ -147,6 +148,14 @@ void ric_mux_destroy(ric_mux* m);
 int ric_codec_create(ric_codec** out, int w, int h, int channels, int device);
 void ric_codec_destroy(ric_codec* c);
 int ric_codec_set_stream(ric_codec* c, void* hip_stream);
+/* Host threads of one encode's serial stage (default 1).  n > 1: each band of
+ * a plane is modelled on its own task of an (n - 1)-thread pool owned by the
+ * object while the calling thread writes the stream in coding order from the
+ * finished bands' event lists (the models are per band, bandcodec.cpp:
+ * 487-507; only the range coder crosses bands, muxcodec.cpp:63-74): lower
+ * latency per frame, byte-identical output.  ric_wavelet_set_host_threads is
+ * the same for CWavelet2D::CodeBand. */
+int ric_codec_set_host_threads(ric_codec* c, int n);
 /* CompressImage: pix = channels planes of w*h bytes (R,G,B planar), on the
  * device if pix_on_device.  Writes the whole .ric file (9-byte header +
  * payload) to out (host), *len_out = its size. */
@@ -214,7 +223,9 @@ int ric_diag_gdec_dbg(void* dev_buf);
 /* Hybrid round trip (gray): the serial encoder runs on the GPU (one wave per
  * stream, launches of `pool_frames` frames, each stream up to stream_cap
  * bytes: a multiple of 16; a longer stream fails the call with
- * RIC_E_CAPACITY), the serial decoder on the host pool.  Configure once. */
+ * RIC_E_CAPACITY), the serial decoder on the host pool.  Configure once.
+ * A pool that does not fit in device memory returns RIC_E_CAPACITY with
+ * nothing allocated (the batch stays usable: retry with fewer frames). */
 int ric_batch_hybrid_config(ric_batch* b, int pool_frames, size_t stream_cap);
 /* As ric_batch_roundtrip (device pixels in and out, .ric files to host
  * out[i]): frames [0, n_host) encoded and decoded on the host; frames

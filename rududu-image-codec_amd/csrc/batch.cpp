@@ -35,6 +35,7 @@
 #include "entropy.h"
 #include "codec_params.h"
 #include "gcoder.h"
+#include "host_pool.h"
 
 using namespace ric;
 
@@ -52,54 +53,6 @@ double now_ms()
 {
 	return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
-
-// A fixed pool of host coder threads with a FIFO of tasks.
-class Pool {
-public:
-	explicit Pool(int n)
-	{
-		for (int i = 0; i < n; i++) th_.emplace_back([this] { run(); });
-	}
-	~Pool()
-	{
-		{
-			std::lock_guard<std::mutex> g(mu_);
-			stop_ = true;
-		}
-		cv_.notify_all();
-		for (auto& t : th_) t.join();
-	}
-	void submit(std::function<void()> f)
-	{
-		{
-			std::lock_guard<std::mutex> g(mu_);
-			q_.push_back(std::move(f));
-		}
-		cv_.notify_one();
-	}
-	int size() const { return (int)th_.size(); }
-
-private:
-	void run()
-	{
-		for (;;) {
-			std::function<void()> f;
-			{
-				std::unique_lock<std::mutex> lk(mu_);
-				cv_.wait(lk, [this] { return stop_ || !q_.empty(); });
-				if (q_.empty()) return;
-				f = std::move(q_.front());
-				q_.pop_front();
-			}
-			f();
-		}
-	}
-	std::vector<std::thread> th_;
-	std::deque<std::function<void()>> q_;
-	std::mutex mu_;
-	std::condition_variable cv_;
-	bool stop_ = false;
-};
 
 // counts down the tasks of one group
 class Latch {
@@ -202,6 +155,9 @@ struct BProf {
 }  // namespace
 
 struct ric_batch {
+	// level 0's hand-off form (ZFrames::ring): the hybrid step runs beside
+	// the stream coder's waves and takes the double buffer (less LDS)
+	int fq_ring = 1;
 	int device = 0, w = 0, h = 0, channels = 1, slots = 0;
 	double hyb_host_ms = 0, hyb_gpu_ms = 0;        // last hybrid call: when each side finished (ms from entry)
 	Pyramid P;
@@ -281,6 +237,7 @@ int gpu_encode_plane(ric_batch* b, int set, int n, int p, const uint8_t* const* 
 	for (int l = 0; l < P.nlev; l++) {
 		ZFrames fr;
 		fr.arena = b->arena(s0); fr.astride = b->astride; fr.nz = n;
+		fr.ring = b->fq_ring;
 		if (l == 0) {
 			fr.src = b->plane(s0, p); fr.sstride = b->pstride; fr.sp = b->pitch;
 		} else {
@@ -903,8 +860,17 @@ int ric_batch_hybrid_config(ric_batch* b, int pool_frames, size_t stream_cap)
 	c.n = pool_frames;
 	c.abstride = (b->P.b_end + 65535) / 65536 * 65536;
 	c.ocap = stream_cap;
-	BCHK(hipMalloc(&c.d_ab, 2 * c.abstride * c.n));
-	BCHK(hipMalloc(&c.d_out, 2 * c.ocap * c.n));
+	// out of memory: nothing stays allocated and the error is not left
+	// pending (a caller may retry with a smaller pool)
+	if (hipMalloc(&c.d_ab, 2 * c.abstride * c.n) != hipSuccess || hipMalloc(&c.d_out, 2 * c.ocap * c.n) != hipSuccess) {
+		const hipError_t e = hipGetLastError();
+		if (c.d_ab) (void)hipFree(c.d_ab);
+		c.d_ab = nullptr;
+		c.d_out = nullptr;
+		set_last_error(std::string("ric_batch_hybrid_config: pool of ") + std::to_string(pool_frames) +
+		               " frames: " + hipGetErrorString(e));
+		return e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation ? RIC_E_CAPACITY : RIC_E_HIP;
+	}
 	BCHK(hipMalloc(&c.d_res, sizeof(uint32_t) * 6 * c.n));          // per half: 2 n encoder words, n decoder words
 	BCHK(hipHostMalloc(&c.h_res, sizeof(uint32_t) * 6 * c.n, 0));
 	if (!c.d_args) BCHK(hipMalloc(&c.d_args, 2 * sizeof(GEncArgs)));
@@ -942,6 +908,12 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 	if (!outputs_distinct(out, n))
 		return set_last_error("ric_batch_roundtrip_hybrid: out[] buffers must be distinct"), RIC_E_ARG;
 	if (set_dev(b->device)) return RIC_E_HIP;
+	// level 0 beside the coder waves: the double-buffered hand-off for this call
+	struct RingGuard {
+		ric_batch* b;
+		~RingGuard() { b->fq_ring = 1; }
+	} ring_guard{b};
+	b->fq_ring = 0;
 	auto& c = b->cp;
 	Pyramid& P = b->P;
 	const int S = b->slots;

@@ -17,6 +17,8 @@
 #include "entropy.h"
 #include "codec_params.h"
 #include "wavelet_api.h"
+#include "host_pool.h"
+#include <memory>
 
 using namespace ric;
 
@@ -94,6 +96,11 @@ struct ric_wavelet {
 	// CodeBand right after it runs as one fused forward+quantiser pass.
 	bool pend = false;
 	int pend_trans = 0;
+	// CodeBand's serial half with the bands modelled on host_threads - 1
+	// pool threads (encode_bands_split); 1: one thread, no split
+	int host_threads = 1;
+	std::unique_ptr<Pool> pool;
+	std::vector<EvBuf> evbufs;
 };
 
 struct ric_mux {
@@ -322,14 +329,28 @@ int code_band_host(ric_wavelet* w, Mux& m, bool copy = true, bool state = false)
 	}
 	// serial part: LL DPCM, then coarse -> fine, V, H, D (wavelet2d.cpp:119-159)
 	const double t0 = now_ms();
-	pred_encode(m, view(w, P.coarsest_ll()));
-	for (int l = P.nlev - 1; l >= 0; l--) {
-		const int order[3] = {BV, BH, BD};
-		for (int k = 0; k < 3; k++) {
-			const Band& B = P.L[l].b[order[k]];
-			const uint64_t* rec = (const uint64_t*)(w->h_arena + P.rec_off[l][order[k]]);
-			const uint8_t* pin = l + 1 < P.nlev ? (const uint8_t*)(w->h_arena + P.pin_off[l][order[k]]) : nullptr;
-			tree_encode_records_fast(m, rec, pin, view(w, B), l == 0);
+	if (w->host_threads > 1) {
+		std::vector<BandRecs> bands;
+		for (int l = P.nlev - 1; l >= 0; l--) {
+			const int order[3] = {BV, BH, BD};
+			for (int k = 0; k < 3; k++) {
+				const Band& B = P.L[l].b[order[k]];
+				bands.push_back({(const uint64_t*)(w->h_arena + P.rec_off[l][order[k]]),
+				                 l + 1 < P.nlev ? (const uint8_t*)(w->h_arena + P.pin_off[l][order[k]]) : nullptr,
+				                 view(w, B), l == 0});
+			}
+		}
+		encode_bands_split(m, *w->pool, w->evbufs, view(w, P.coarsest_ll()), bands.data(), (int)bands.size());
+	} else {
+		pred_encode(m, view(w, P.coarsest_ll()));
+		for (int l = P.nlev - 1; l >= 0; l--) {
+			const int order[3] = {BV, BH, BD};
+			for (int k = 0; k < 3; k++) {
+				const Band& B = P.L[l].b[order[k]];
+				const uint64_t* rec = (const uint64_t*)(w->h_arena + P.rec_off[l][order[k]]);
+				const uint8_t* pin = l + 1 < P.nlev ? (const uint8_t*)(w->h_arena + P.pin_off[l][order[k]]) : nullptr;
+				tree_encode_records_fast(m, rec, pin, view(w, B), l == 0);
+			}
 		}
 	}
 	w->prof.host(S_HENC, now_ms() - t0);
@@ -914,6 +935,17 @@ void ric_codec_destroy(ric_codec* c)
 }
 
 int ric_codec_set_stream(ric_codec* c, void* s) { return c ? ric_wavelet_set_stream(c->wav, s) : RIC_E_ARG; }
+
+int ric_wavelet_set_host_threads(ric_wavelet* w, int n)
+{
+	if (!w || n < 1 || n > 64) return RIC_E_ARG;
+	w->pool.reset();
+	w->host_threads = n;
+	if (n > 1) w->pool.reset(new Pool(n - 1));
+	return RIC_OK;
+}
+
+int ric_codec_set_host_threads(ric_codec* c, int n) { return c ? ric_wavelet_set_host_threads(c->wav, n) : RIC_E_ARG; }
 
 // CompressImage, src/ric/ric.cpp:123-180
 int ric_codec_encode(ric_codec* c, const uint8_t* pix, int on_device, int q, int trans,

@@ -2689,9 +2689,10 @@ int launch_fwdq_level_z(const Pyramid& P, int l, const ZFrames& fr, int vec8, in
 	// the one-producer form on level 0 (VALU-bound), two producers above (see
 	// fq_launch_pc); knob RIC_FQZ_PC1 = the last level on one producer
 	static const int pc1 = [] { const char* e = getenv("RIC_FQZ_PC1"); return e ? atoi(e) : 0; }();
-	// knob RIC_FQZ_ASYNC=0: the double-buffered hand-off (20 KiB of LDS per
-	// workgroup instead of the ring's 32 KiB)
-	static const int async = [] { const char* e = getenv("RIC_FQZ_ASYNC"); return e ? atoi(e) : 1; }();
+	// the ring or the double-buffered hand-off (ZFrames::ring; knob
+	// RIC_FQZ_ASYNC=0/1 overrides)
+	static const int async_env = [] { const char* e = getenv("RIC_FQZ_ASYNC"); return e ? atoi(e) : -1; }();
+	const int async = async_env >= 0 ? async_env : fr.ring;
 	if (l <= pc1 && l == 0 && in8 && !async) hipLaunchKernelGGL((k_fwdq_pc_z<false, false>), grid, dim3(256), 0, st, d, S, 0);
 	else if (l <= pc1 && l == 0 && in8) hipLaunchKernelGGL((k_fwdq_pc_z<true, false>), grid, dim3(256), 0, st, d, S, 0);
 	else if (l <= pc1) hipLaunchKernelGGL((k_fwdq_pc_z<true, true>), grid, dim3(256), 0, st, d, S, 0);

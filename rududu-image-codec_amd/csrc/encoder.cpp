@@ -7,6 +7,9 @@
 #include "entropy.h"
 #include "coder_tables.h"
 #include "symbols.h"
+#include "host_pool.h"
+#include <atomic>
+#include <memory>
 
 namespace ric {
 
@@ -80,11 +83,80 @@ struct EncCore {
 	}
 };
 
+// The modelling half alone: the same calls as EncCore, recorded as events
+// for a later serial replay (replay_events).  One 64-bit event per bin, with
+// the raw bits that follow it up to the next bin (raw bits never move across
+// a bin: only a bin can normalise, and a normalisation is what places them):
+//   bit 0 the bin's symbol, bits 1-13 its freq, bit 14 a bin is present (else
+//   the event only carries raw bits: a band's leading raw field, or bits past
+//   32 after one bin), bits 16-21 the raw length (<= 32), bits 32-63 the raw
+//   value.
+struct EvCore {
+	EvBuf* buf;
+	uint64_t* p;
+	uint64_t* end;
+	uint64_t cur = 0;                 // the event being built (0: none)
+	uint32_t rlen = 0;
+	explicit EvCore(EvBuf& b) : buf(&b)
+	{
+		if (b.cap < 4096) b.grow(4096);
+		p = b.p;
+		end = b.p + b.cap;
+	}
+	__attribute__((noinline)) void grow()
+	{
+		const size_t used = (size_t)(p - buf->p);
+		buf->grow(buf->cap * 2);
+		p = buf->p + used;
+		end = buf->p + buf->cap;
+	}
+	RIC_AI void emit()
+	{
+		if (__builtin_expect(p == end, 0)) grow();
+		*p++ = cur;
+	}
+	RIC_AI void bin(uint32_t freq, uint32_t bit)
+	{
+		if (cur) emit();
+		cur = (uint64_t)((freq << 1) | bit | (1u << 14));
+		rlen = 0;
+	}
+	static constexpr uint64_t kRawOnly = 4096u << 1;      // freq 4096, symbol 0, no bin: the identity
+	RIC_AI void append(uint32_t v, uint32_t len)             // rlen + len <= 32
+	{
+		const uint64_t raw = ((cur >> 32) << len) | v;
+		rlen += len;
+		cur = (cur & 0xFFFFu) | ((uint64_t)rlen << 16) | (raw << 32);
+	}
+	RIC_AI void bits(uint32_t v, uint32_t len)
+	{
+		if (!cur) { cur = kRawOnly; rlen = 0; }
+		if (__builtin_expect(rlen + len > 32, 0)) {
+			// fill this event to 32 bits; the rest starts a raw-only event
+			const uint32_t a = 32 - rlen, b = len - a;
+			if (a) append(v >> b, a);
+			emit();
+			cur = kRawOnly;
+			rlen = 0;
+			v &= b >= 32 ? 0xFFFFFFFFu : (1u << b) - 1u;
+			len = b;
+		}
+		append(v, len);
+	}
+	size_t finish()
+	{
+		if (cur) emit();
+		cur = 0;
+		return (size_t)(p - buf->p);
+	}
+};
+
 struct BitE {                                             // CBitCodec::code
 	uint16_t freq[16];
 	uint8_t shift[16], mps[16];
 	BitE() { for (int i = 0; i < 16; i++) { freq[i] = 2048; shift[i] = 0; mps[i] = 0; } }
-	RIC_AI void code(EncCore& e, uint32_t sym, int c)
+	template <typename Core>
+	RIC_AI void code(Core& e, uint32_t sym, int c)
 	{
 		const uint32_t s = sym ^ mps[c];
 		e.bin(freq[c], s ^ 1);
@@ -110,7 +182,8 @@ struct GeoE {                                             // CGeomCodec::code
 		}
 	}
 	// magnitude - 1 then the raw sign bit (remainder and sign as one chunk)
-	RIC_AI void code_signed(EncCore& e, uint32_t sym, uint32_t sign, int c)
+	template <typename Core>
+	RIC_AI void code_signed(Core& e, uint32_t sym, uint32_t sign, int c)
 	{
 		const uint32_t k = kGeoK[idx[c]], f = freq[c];
 		const int s = kGeoShift[idx[c]];
@@ -136,7 +209,8 @@ struct GeoRegE {
 	uint32_t freq, idx;
 	RIC_AI void load(const GeoE& g, int c) { freq = g.freq[c]; idx = g.idx[c]; }
 	RIC_AI void store(GeoE& g, int c) const { g.freq[c] = (uint16_t)freq; g.idx[c] = (uint8_t)idx; }
-	RIC_AI void code_signed(EncCore& e, uint32_t sym, uint32_t sign)   // GeoE::code_signed
+	template <typename Core>
+	RIC_AI void code_signed(Core& e, uint32_t sym, uint32_t sign)   // GeoE::code_signed
 	{
 		const uint32_t k = kGeoK[idx], f = freq;
 		const int s = kGeoShift[idx];
@@ -158,14 +232,13 @@ struct GeoRegE {
 	}
 };
 
-template <typename C, bool HIGH, bool PAR>
-void tree_rec_fast(Mux& m, const uint64_t* rec, const uint8_t* pin, const BandView& b)
+template <typename Core, typename C, bool HIGH, bool PAR>
+void tree_rec_core(Core& e, const uint64_t* rec, const uint8_t* pin, const BandView& b)
 {
 	constexpr bool SH = sizeof(C) == 2;
 	static const uint8_t ginit[16] = {5,9,9,9,9,9,9,9,9,9,9,9,10,10,10,11};   // bandcodec.cpp:487
 	uint16_t kmean[16] = {2 << 10, 3 << 10, 4 << 10, 5 << 10, 8 << 10, 11 << 10, 13 << 10, 14 << 10,
 	                      15 << 10, 15 << 10, 15 << 10, 15 << 10, 15 << 10, 15 << 10, 15 << 10, 15 << 10};
-	EncCore e(m.enc_state());
 	GeoE g(ginit);
 	BitE tree, bord;
 	const C* band = (const C*)b.p;
@@ -223,14 +296,24 @@ void tree_rec_fast(Mux& m, const uint64_t* rec, const uint8_t* pin, const BandVi
 			}
 		}
 	}
-	m.set_enc_state(e.s);
 }
 
 template <typename C, bool HIGH>
 void tree_rec_disp(Mux& m, const uint64_t* rec, const uint8_t* pin, const BandView& b)
 {
-	if (pin) tree_rec_fast<C, HIGH, true>(m, rec, pin, b);
-	else tree_rec_fast<C, HIGH, false>(m, rec, pin, b);
+	EncCore e(m.enc_state());
+	if (pin) tree_rec_core<EncCore, C, HIGH, true>(e, rec, pin, b);
+	else tree_rec_core<EncCore, C, HIGH, false>(e, rec, pin, b);
+	m.set_enc_state(e.s);
+}
+
+template <typename C, bool HIGH>
+size_t tree_model_disp(EvBuf& ev, const uint64_t* rec, const uint8_t* pin, const BandView& b)
+{
+	EvCore e(ev);
+	if (pin) tree_rec_core<EvCore, C, HIGH, true>(e, rec, pin, b);
+	else tree_rec_core<EvCore, C, HIGH, false>(e, rec, pin, b);
+	return e.finish();
 }
 
 }  // namespace
@@ -239,6 +322,57 @@ void tree_encode_records_fast(Mux& m, const uint64_t* rec, const uint8_t* pin, c
 {
 	if (b.is_int) { if (high) tree_rec_disp<int32_t, true>(m, rec, pin, b); else tree_rec_disp<int32_t, false>(m, rec, pin, b); }
 	else { if (high) tree_rec_disp<int16_t, true>(m, rec, pin, b); else tree_rec_disp<int16_t, false>(m, rec, pin, b); }
+}
+
+size_t tree_model_records(EvBuf& ev, const uint64_t* rec, const uint8_t* pin, const BandView& b, bool high)
+{
+	if (b.is_int) return high ? tree_model_disp<int32_t, true>(ev, rec, pin, b) : tree_model_disp<int32_t, false>(ev, rec, pin, b);
+	return high ? tree_model_disp<int16_t, true>(ev, rec, pin, b) : tree_model_disp<int16_t, false>(ev, rec, pin, b);
+}
+
+void replay_events(Mux& m, const uint64_t* ev, size_t n)
+{
+	EncCore e(m.enc_state());
+	for (size_t i = 0; i < n; i++) {
+		const uint64_t x = ev[i];
+		const uint32_t lo = (uint32_t)x;
+		// the bin (a raw-only event is the identity bin: freq 4096, symbol 0,
+		// and no normalisation)
+		if (__builtin_expect((lo >> 14) & (e.s.range <= 4096u), 0)) e.norm();
+		const uint32_t freq = (lo >> 1) & 0x1FFFu, bit = lo & 1u;
+		const uint32_t t = (e.s.range * freq) >> 12;
+		e.s.low += t & (0u - bit);
+		e.s.range = t + ((e.s.range - 2 * t) & (0u - bit));
+		const uint32_t len = (lo >> 16) & 63u;
+		if (__builtin_expect(e.s.ebits + len > 64, 0)) e.drain();
+		e.s.ebuf = (e.s.ebuf << len) | (uint32_t)(x >> 32);
+		e.s.ebits += len;
+	}
+	m.set_enc_state(e.s);
+}
+
+void encode_bands_split(Mux& m, Pool& pool, std::vector<EvBuf>& bufs, const BandView& ll, const BandRecs* bands, int n)
+{
+	if ((int)bufs.size() < n) bufs.resize(n);
+	std::vector<size_t> cnt(n, 0);
+	std::unique_ptr<std::atomic<int>[]> done(new std::atomic<int>[n]);
+	std::vector<int> big(n);
+	for (int i = 0; i < n; i++) { done[i].store(0); big[i] = i; }
+	std::stable_sort(big.begin(), big.end(), [&](int a, int b) {
+		return (long)bands[a].v.dx * bands[a].v.dy > (long)bands[b].v.dx * bands[b].v.dy;
+	});
+	for (int k = 0; k < n; k++) {
+		const int i = big[k];
+		pool.submit([&, i] {
+			cnt[i] = tree_model_records(bufs[i], bands[i].rec, bands[i].pin, bands[i].v, bands[i].high);
+			done[i].store(1, std::memory_order_release);
+		});
+	}
+	pred_encode(m, ll);
+	for (int i = 0; i < n; i++) {
+		while (!done[i].load(std::memory_order_acquire)) std::this_thread::yield();
+		replay_events(m, bufs[i].p, cnt[i]);
+	}
 }
 
 }  // namespace ric

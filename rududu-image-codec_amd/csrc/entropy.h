@@ -8,6 +8,8 @@
 // range-coder state per stream: SURVEY.md §7.1); the data-parallel stages
 // (DWT, RD quantiser, dequantiser, inverse DWT) run on the GPU.
 #pragma once
+#include <vector>
+#include <algorithm>
 #include <cstdint>
 #include <cstddef>
 #include <cstring>
@@ -203,5 +205,43 @@ void mv_decode(Mux& m, uint32_t* mv, int dimx, int dimy);
 // (encoder.cpp): rec / pin in raster block order; pin == nullptr for a band
 // without a parent (the coarsest level).
 void tree_encode_records_fast(Mux& m, const uint64_t* rec, const uint8_t* pin, const BandView& b, bool high);
+// The same band split in two halves (encoder.cpp): the modelling alone,
+// recording the coder calls as events into ev (grown as needed; returns the
+// count) -- bands model independently, every model is per band
+// (bandcodec.cpp:487-507) -- and the serial replay of those events into the
+// stream.  tree_model_records + replay_events == tree_encode_records_fast.
+struct EvBuf {                     // a growable event list (no zero fill), kept across frames
+	uint64_t* p = nullptr;
+	size_t cap = 0;
+	EvBuf() = default;
+	EvBuf(const EvBuf&) = delete;
+	EvBuf& operator=(const EvBuf&) = delete;
+	EvBuf(EvBuf&& o) noexcept : p(o.p), cap(o.cap) { o.p = nullptr; o.cap = 0; }
+	EvBuf& operator=(EvBuf&& o) noexcept { std::swap(p, o.p); std::swap(cap, o.cap); return *this; }
+	~EvBuf() { delete[] p; }
+	void grow(size_t n)
+	{
+		uint64_t* q = new uint64_t[n];
+		if (p) { std::copy(p, p + std::min(cap, n), q); delete[] p; }
+		p = q;
+		cap = n;
+	}
+};
+size_t tree_model_records(EvBuf& ev, const uint64_t* rec, const uint8_t* pin, const BandView& b, bool high);
+void replay_events(Mux& m, const uint64_t* ev, size_t n);
+
+// One plane's CodeBand serial half with the bands modelled in parallel
+// (encoder.cpp): LL DPCM (pred_encode) on the calling thread, every band's
+// modelling a task of `pool` (largest bands first), the replays in coding
+// order on the calling thread as each band's events complete.  Byte-identical
+// to pred_encode + tree_encode_records_fast over the same bands in order.
+struct BandRecs {
+	const uint64_t* rec;
+	const uint8_t* pin;
+	BandView v;
+	bool high;
+};
+class Pool;
+void encode_bands_split(Mux& m, Pool& pool, std::vector<EvBuf>& bufs, const BandView& ll, const BandRecs* bands, int n);
 
 }  // namespace ric

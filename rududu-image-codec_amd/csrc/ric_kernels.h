@@ -66,6 +66,10 @@ struct ZFrames {
 	const void* src = nullptr; size_t sstride = 0; long sp = 0;
 	void* out = nullptr; size_t ostride = 0; long po = 0;
 	int nz = 0;
+	// level 0 of the fused forward: the LDS ring hand-off (1, 32 KiB per
+	// workgroup) or the double buffer (0, 20 KiB: more workgroups fit beside
+	// the stream coder's waves)
+	int ring = 1;
 };
 // Per-frame argument array of one batched launch, on the device; re-uploaded
 // (after a stream sync) only when it changes.

@@ -48,6 +48,7 @@ def lib():
         "ric_wavelet_create": (_I, [ctypes.POINTER(_P), _I, _I, _I, _I, _I]),
         "ric_wavelet_destroy": (None, [_P]),
         "ric_wavelet_set_stream": (_I, [_P, _P]),
+        "ric_wavelet_set_host_threads": (_I, [_P, _I]),
         "ric_wavelet_sync": (_I, [_P]),
         "ric_set_weight": (_I, [_P, _I, _F]),
         "ric_transform": (_I, [_P, _P, _I, _I, _I]),
@@ -74,6 +75,7 @@ def lib():
         "ric_codec_create": (_I, [ctypes.POINTER(_P), _I, _I, _I, _I]),
         "ric_codec_destroy": (None, [_P]),
         "ric_codec_set_stream": (_I, [_P, _P]),
+        "ric_codec_set_host_threads": (_I, [_P, _I]),
         "ric_codec_encode": (_I, [_P, _P, _I, _I, _I, _P, _S, ctypes.POINTER(_S)]),
         "ric_codec_decode": (_I, [_P, _P, _S, _I, _P, _P, _I]),
         "ric_read_header": (_I, [_P, _S, ctypes.POINTER(_I), ctypes.POINTER(_I), ctypes.POINTER(_I),
@@ -229,6 +231,10 @@ class Wavelet2D:
 
     def set_stream(self, stream_ptr):
         _chk(lib().ric_wavelet_set_stream(self.h, stream_ptr), "set_stream")
+
+    def set_host_threads(self, n):
+        """CodeBand's serial half over n host threads (bands modelled in parallel)."""
+        _chk(lib().ric_wavelet_set_host_threads(self.h, n), "set_host_threads")
 
     def sync(self):
         _chk(lib().ric_wavelet_sync(self.h), "sync")
@@ -481,6 +487,11 @@ class Codec:
 
     def set_stream(self, stream_ptr):
         _chk(lib().ric_codec_set_stream(self.h, stream_ptr), "set_stream")
+
+    def set_host_threads(self, n):
+        """The encoder's serial stage over n host threads (bands modelled in
+        parallel, one thread writing the stream): lower latency, same bytes."""
+        _chk(lib().ric_codec_set_host_threads(self.h, n), "set_host_threads")
 
     def prof_enable(self, on=True):
         _prof_enable(lib().ric_codec_wavelet(self.h), on)

@@ -24,6 +24,8 @@ def lib():
         L.hc_encode.argtypes = [_V, _L, _I, _I, _I, _I, _I, _V, _L, _V]
         L.hc_encode_rec.restype = _L
         L.hc_encode_rec.argtypes = [_V, _L, _I, _I, _I, _I, _I, _V, _L, _V, _V]
+        L.hc_encode_rec_split.restype = _L
+        L.hc_encode_rec_split.argtypes = [_V, _L, _I, _I, _I, _I, _I, _V, _L, _I, _V, _V, _V]
         L.hc_decode.restype = _L
         L.hc_decode.argtypes = [_V, _L, _I, _I, _I, _I, _I, _V, _V]
         _lib = L
@@ -41,6 +43,19 @@ def encode(bands_flat, w, h, levels, lc, records=True):
                                 ctypes.byref(s1), ctypes.byref(s2))
     else:
         n = lib().hc_encode(b.ctypes.data, b.size, 1, w, h, levels, lc, out.ctypes.data, cap, ctypes.byref(s1))
+    assert n > 0
+    return out[:n].tobytes()
+
+
+def encode_split(bands_flat, w, h, levels, lc, nthreads):
+    """encode() through the band-parallel split (encoder.cpp tree_model_records
+    + replay_events; nthreads <= 0: every band modelled, then replayed, serially)."""
+    b = np.ascontiguousarray(bands_flat, np.int32)
+    cap = w * h * 4 + 4096
+    out = np.zeros(cap, np.uint8)
+    s1, s2, s3 = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+    n = lib().hc_encode_rec_split(b.ctypes.data, b.size, 1, w, h, levels, lc, out.ctypes.data, cap, nthreads,
+                                  ctypes.byref(s1), ctypes.byref(s2), ctypes.byref(s3))
     assert n > 0
     return out[:n].tobytes()
 

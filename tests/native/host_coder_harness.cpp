@@ -6,6 +6,8 @@
 #include <cstring>
 #include <vector>
 #include <chrono>
+#include <atomic>
+#include <thread>
 #include "ric_types.h"
 #include "entropy.h"
 #include "symbols.h"
@@ -13,6 +15,7 @@
 using namespace ric;
 
 namespace {
+double now() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
 struct HostPyr {
 	Pyramid P;
 	std::vector<char> arena;
@@ -99,6 +102,52 @@ struct HostPyr {
 				                         view(P.L[l].b[order[k]]), l == 0);
 		}
 	}
+	// the band-parallel split: every band modelled on its own thread into an
+	// event list, replayed into m in coding order as each list completes
+	void encode_rec_split(Mux& m, int nthreads, double* t_model, double* t_replay) {
+		struct Job { int l, b; EvBuf* ev; size_t n = 0; std::atomic<int> done{0}; };
+		static std::vector<EvBuf> bufs(64);           // kept across calls, as a product pool would
+		std::vector<Job> jobs(3 * P.nlev);
+		for (size_t i = 0; i < jobs.size(); i++) jobs[i].ev = &bufs[i];
+		std::vector<int> order;                 // coding order
+		for (int l = P.nlev - 1; l >= 0; l--) {
+			const int ob[3] = {BV, BH, BD};
+			for (int k = 0; k < 3; k++) { jobs[order.size()].l = l; jobs[order.size()].b = ob[k]; order.push_back((int)order.size()); }
+		}
+		auto model = [&](Job& j) {
+			j.n = tree_model_records(*j.ev, recs[3 * j.l + j.b].data(), j.l + 1 < P.nlev ? pins[3 * j.l + j.b].data() : nullptr,
+			                         view(P.L[j.l].b[j.b]), j.l == 0);
+			j.done.store(1, std::memory_order_release);
+		};
+		const double t0 = now();
+		if (nthreads <= 0) {
+			for (Job& j : jobs) model(j);
+			const double t1 = now();
+			pred_encode(m, view(P.coarsest_ll()));
+			for (Job& j : jobs) replay_events(m, j.ev->p, j.n);
+			*t_model += t1 - t0;
+			*t_replay += now() - t1;
+			return;
+		}
+		std::atomic<int> next{0};
+		// largest bands first (the finest level's are the long poles)
+		std::vector<int> big(jobs.size());
+		for (size_t i = 0; i < big.size(); i++) big[i] = (int)(big.size() - 1 - i);
+		std::vector<std::thread> th;
+		for (int t = 0; t < nthreads; t++)
+			th.emplace_back([&] { for (int i; (i = next.fetch_add(1)) < (int)big.size();) model(jobs[big[i]]); });
+		pred_encode(m, view(P.coarsest_ll()));
+		double wait = 0;
+		for (Job& j : jobs) {
+			const double w0 = now();
+			while (!j.done.load(std::memory_order_acquire)) std::this_thread::yield();
+			wait += now() - w0;
+			replay_events(m, j.ev->p, j.n);
+		}
+		for (auto& x : th) x.join();
+		*t_model += wait;
+		*t_replay += now() - t0 - wait;
+	}
 	void decode(Mux& m) {
 		pred_decode(m, view(P.coarsest_ll()));
 		for (int l = P.nlev - 1; l >= 0; l--) {
@@ -111,7 +160,6 @@ struct HostPyr {
 		}
 	}
 };
-double now() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
 }  // namespace
 
 extern "C" {
@@ -135,6 +183,29 @@ long hc_encode_rec(const int32_t* bands, long per_plane, int nplanes, int w, int
 	uint8_t* e = m.end_coding();
 	if (secs) *secs = t;
 	if (rec_secs) *rec_secs = tr;
+	return m.overflow() ? -1 : (long)(e - out);
+}
+
+// hc_encode_rec through the band-parallel split (nthreads <= 0: model every
+// band, then replay, serially; t_model / t_replay: the two phases, or with
+// threads the replay thread's waits and its work)
+long hc_encode_rec_split(const int32_t* bands, long per_plane, int nplanes, int w, int h, int levels, int lc,
+                         uint8_t* out, long cap, int nthreads, double* secs, double* t_model, double* t_replay)
+{
+	HostPyr hp(w, h, levels, lc);
+	Mux m;
+	m.init_encoder(out, cap, 0);
+	double t = 0;
+	*t_model = *t_replay = 0;
+	for (int p = 0; p < nplanes; p++) {
+		hp.load(bands + p * per_plane);
+		hp.build_records();
+		const double t1 = now();
+		hp.encode_rec_split(m, nthreads, t_model, t_replay);
+		t += now() - t1;
+	}
+	uint8_t* e = m.end_coding();
+	if (secs) *secs = t;
 	return m.overflow() ? -1 : (long)(e - out);
 }
 

@@ -280,3 +280,55 @@ def test_full_range_planes(ric, port, kind, w, h, t):
         out = np.zeros((h, w), np.int16)
         W.TransformI(out, w, t)
         assert np.array_equal(out, exp_plane), ("closed loop plane", L, lc)
+
+
+@pytest.mark.parametrize("e", G["small"], ids=[e["name"] for e in G["small"]])
+def test_small_golden_split_encoder(ric, e):
+    """ric_codec_set_host_threads: bands modelled in parallel, the stream
+    written in coding order from their event lists -- the golden bytes"""
+    pix = ric.synth(e["w"], e["h"], e["channels"], e["frame"])
+    c = ric.Codec(e["w"], e["h"], e["channels"])
+    c.set_host_threads(4)
+    assert c.compress(pix, e["q"], e["trans"]) == open(os.path.join(GOLD, e["name"] + ".ric"), "rb").read()
+
+
+@pytest.mark.parametrize("name", ["C3_7680x4320_q9", "C3rgb_7680x4320_q9", "lossless53_1001x603"])
+def test_full_size_split_encoder(ric, name):
+    e = large(name)
+    pix = ric.synth(e["w"], e["h"], e["channels"], e["frame"])
+    c = ric.Codec(e["w"], e["h"], e["channels"])
+    c.set_host_threads(8)
+    for _ in range(2):                         # event buffers reused across frames
+        r = c.compress(pix, e["q"], e["trans"])
+        assert len(r) == e["ric_bytes"] and sha(r) == e["ric_sha256"]
+
+
+def test_codeband_split_encoder(ric, port):
+    """CWavelet2D::CodeBand over the split (ric_wavelet_set_host_threads),
+    with the band state the API leaves (closed loop)"""
+    w, h, t, L, lc = 300, 220, 0, 5, 1
+    pl = O.gray_plane(ric.synth(w, h, 1, 6)[0], 9)
+    exp_plane, exp_bands = port.closed_loop(pl, L, lc, t, 96, 36, 96)
+    W = ric.Wavelet2D(w, h, L, lc)
+    W.SetWeight(t)
+    W.set_host_threads(3)
+    W.Transform(pl, w, t)
+    buf = np.zeros(w * h * 4 + 4096, np.uint8)
+    m = ric.MuxCodec(buf, first_word=0)
+    W.CodeBand(m, 96, 36)
+    m.endCoding()
+    W.TSUQi(96)
+    for a, b in zip(W.bands(), exp_bands):
+        assert np.array_equal(a, b)
+    out = np.zeros((h, w), np.int16)
+    W.TransformI(out, w, t)
+    assert np.array_equal(out, exp_plane)
+    # the stream: the one-thread CodeBand's bytes
+    W1 = ric.Wavelet2D(w, h, L, lc)
+    W1.SetWeight(t)
+    W1.Transform(pl, w, t)
+    buf1 = np.zeros_like(buf)
+    m1 = ric.MuxCodec(buf1, first_word=0)
+    W1.CodeBand(m1, 96, 36)
+    m1.endCoding()
+    assert np.array_equal(buf, buf1)

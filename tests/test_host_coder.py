@@ -35,6 +35,32 @@ def test_encode_matches_oracle(w, h, q, t, L, lc, records):
 
 
 @pytest.mark.parametrize("w,h,q,t,L,lc", CASES)
+@pytest.mark.parametrize("nthreads", [0, 3])
+def test_split_encoder_matches_oracle(w, h, q, t, L, lc, nthreads):
+    """the band-parallel split (events per band, serial replay) writes the
+    reference's bytes: raw fields never move across a bin, and bins replay in
+    order (muxcodec.cpp:63-74, 536-570)"""
+    P = O.port()
+    pl = _plane(w, h, q)
+    Q = O.quants(q + 20) if q else 0
+    lam = O.quants(q + 13) if q else 0
+    flat = np.concatenate([x.ravel() for x in P.bands(pl, L, lc, t, 1, Q, lam)]).astype(np.int32)
+    assert HC.encode_split(flat, w, h, L, lc, nthreads) == P.encode_planes(pl[None], L, lc, t, [Q], [lam])
+
+
+def test_split_encoder_long_raw_fields():
+    """lossless int bands: raw fields past 24 bits and events split at 32 bits"""
+    P = O.port()
+    w, h = 300, 200
+    rng = np.random.default_rng(5)
+    pl = rng.integers(-2048, 2048, (h, w)).astype(np.int16)
+    flat = np.concatenate([x.ravel() for x in P.bands(pl, 5, 4, 1, 1, 0, 0)]).astype(np.int32)
+    exp = P.encode_planes(pl[None], 5, 4, 1, [0], [0])
+    assert HC.encode(flat, w, h, 5, 4) == exp
+    assert HC.encode_split(flat, w, h, 5, 4, 2) == exp
+
+
+@pytest.mark.parametrize("w,h,q,t,L,lc", CASES)
 def test_decode_matches_oracle(w, h, q, t, L, lc):
     P = O.port()
     pl = _plane(w, h, q)
