@@ -277,6 +277,8 @@ void ric_video_destroy(ric_video* v);
  * quants(quant + 20), the RD lambda quants(quant + 12) (rududucodec.cpp:58-71);
  * -12 <= quant <= 30 (the table's defined range) */
 int ric_video_set_quant(ric_video* v, int quant);
+/* the encoder's serial stage over n host threads (ric_codec_set_host_threads) */
+int ric_video_set_host_threads(ric_video* v, int n);
 /* CRududuCodec::encode(unsigned char* pImage, int stride, unsigned char*
  * pBuffer, CImage** outImage) (rududucodec.cpp:87-119).  pix: 3 planes R, G,
  * B of h rows x stride bytes, bottom row first (CImage::inputSGI), on the host

@@ -290,7 +290,12 @@ __global__ __launch_bounds__(64) void k_vid_epzs_full(EpzsArgs a)
 // the full-pel vector, or MV_INTRA when the full-pel SAD saturated
 __global__ __launch_bounds__(64) void k_vid_epzs_sub(EpzsArgs a)
 {
-	const int b = blockIdx.x, lane = threadIdx.x;
+	// XCD-aware block order: workgroups are dealt round-robin over the 8 XCDs,
+	// so workgroup g takes block (g % 8) * C + g / 8 -- each XCD refines one
+	// contiguous run of blocks, whose candidate windows overlap in its L2
+	const int nb = a.bx * a.by, C = (nb + 7) >> 3;
+	const int b = (int)(blockIdx.x & 7) * C + (int)(blockIdx.x >> 3), lane = threadIdx.x;
+	if (b >= nb) return;
 	const int i = b % a.bx, j = b / a.bx;
 	const uint32_t m = a.mv[b];
 	int bd = a.dist[b];
@@ -345,12 +350,26 @@ __constant__ int16_t kWin[8][8] = {                      // COBMC::window, obmc.
 // first statement is the previous prediction (the LEFT column's first
 // statement accumulates onto it: obmc.cpp:158).  Intra blocks contribute 0
 // (obmc_block_intra, :179-250).
-__global__ void k_vid_obmc(VidSubs ref, const uint32_t* __restrict__ mv, int16_t* __restrict__ pred, int w, int h,
-                           int S, long P, int bx, int by)
+// One workgroup per 64-column x 16-row tile (a lane per column, four rows at
+// a time): the rows of a tile re-read the same source windows (a block's
+// window spans 16 rows), so they share the CU's L1 and the XCD's L2 instead
+// of being fetched once per row by workgroups spread over the XCDs.
+constexpr int kObmcRows = 16;
+__device__ __forceinline__ void obmc_sample(const VidSubs& ref, const uint32_t* __restrict__ mv, int16_t* __restrict__ pred,
+                                            int w, int h, int S, long pc, int bx, int by, int x, int y);
+__global__ __launch_bounds__(256) void k_vid_obmc(VidSubs ref, const uint32_t* __restrict__ mv, int16_t* __restrict__ pred,
+                                                  int w, int h, int S, long P, int bx, int by)
 {
-	const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+	const int x = blockIdx.x * 64 + threadIdx.x;
 	if (x >= 8 * bx) return;
 	const long pc = blockIdx.z * P;
+	const int y1 = min((int)(blockIdx.y + 1) * kObmcRows, 8 * by);
+	for (int y = blockIdx.y * kObmcRows + threadIdx.y; y < y1; y += 4) obmc_sample(ref, mv, pred, w, h, S, pc, bx, by, x, y);
+}
+
+__device__ __forceinline__ void obmc_sample(const VidSubs& ref, const uint32_t* __restrict__ mv, int16_t* __restrict__ pred,
+                                            int w, int h, int S, long pc, int bx, int by, int x, int y)
+{
 	const long o = pc + (long)y * S + x;
 	int d = pred[o];
 	const int a0 = (x + 4) >> 3, b0 = (y + 4) >> 3, cu = x + 4 - 8 * a0, cv = y + 4 - 8 * b0;
@@ -456,14 +475,14 @@ int launch_vid_epzs(const VidGeom& g, const int16_t* cur, const VidSubs& ref, ui
 	a.w = g.w; a.h = g.h; a.S = g.S; a.bx = g.bx; a.by = g.by;
 	hipLaunchKernelGGL(k_vid_epzs_full, dim3(g.by), dim3(64), 0, st, a);
 	if (launched()) return -1;
-	hipLaunchKernelGGL(k_vid_epzs_sub, dim3(g.bx * g.by), dim3(64), 0, st, a);
+	hipLaunchKernelGGL(k_vid_epzs_sub, dim3(8 * ((g.bx * g.by + 7) / 8)), dim3(64), 0, st, a);
 	return launched();
 }
 
 int launch_vid_obmc(const VidGeom& g, const uint32_t* mv, const VidSubs& ref, int16_t* pred, hipStream_t st)
 {
-	hipLaunchKernelGGL(k_vid_obmc, dim3((8 * g.bx + 127) / 128, 8 * g.by, 3), dim3(128), 0, st, ref, mv, pred, g.w, g.h,
-	                   g.S, g.P, g.bx, g.by);
+	hipLaunchKernelGGL(k_vid_obmc, dim3((8 * g.bx + 63) / 64, (8 * g.by + kObmcRows - 1) / kObmcRows, 3), dim3(64, 4), 0, st,
+	                   ref, mv, pred, g.w, g.h, g.S, g.P, g.bx, g.by);
 	return launched();
 }
 

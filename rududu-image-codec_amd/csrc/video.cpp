@@ -267,6 +267,8 @@ void ric_video_destroy(ric_video* v)
 	delete v;
 }
 
+int ric_video_set_host_threads(ric_video* v, int n) { return v ? ric_wavelet_set_host_threads(v->wav, n) : RIC_E_ARG; }
+
 int ric_video_set_quant(ric_video* v, int quant)
 {
 	// quants(quant + 12) .. quants(quant + 20) must stay inside the table's

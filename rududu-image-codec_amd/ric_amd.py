@@ -76,6 +76,7 @@ def lib():
         "ric_codec_destroy": (None, [_P]),
         "ric_codec_set_stream": (_I, [_P, _P]),
         "ric_codec_set_host_threads": (_I, [_P, _I]),
+        "ric_video_set_host_threads": (_I, [_P, _I]),
         "ric_codec_encode": (_I, [_P, _P, _I, _I, _I, _P, _S, ctypes.POINTER(_S)]),
         "ric_codec_decode": (_I, [_P, _P, _S, _I, _P, _P, _I]),
         "ric_read_header": (_I, [_P, _S, ctypes.POINTER(_I), ctypes.POINTER(_I), ctypes.POINTER(_I),
@@ -562,6 +563,10 @@ class VideoCodec:
     def quant(self, q):
         _chk(lib().ric_video_set_quant(self.h, q), "CRududuCodec::quant")
         self._quant = q
+
+    def set_host_threads(self, n):
+        """the encoder's serial stage over n host threads (same bytes)"""
+        _chk(lib().ric_video_set_host_threads(self.h, n), "set_host_threads")
 
     def encode(self, frame, stride=None, on_device=None):
         """CRududuCodec::encode: returns the frame's stream (size + 2 bytes)."""

@@ -114,6 +114,7 @@ def main():
     ap.add_argument("--h", type=int, default=1080)
     ap.add_argument("--frames", type=int, default=30)
     ap.add_argument("--q", type=int, default=20)
+    ap.add_argument("--host-threads", type=int, default=8, help="the encoder's serial stage (ric_video_set_host_threads)")
     ap.add_argument("--cpu-frames", type=int, default=10,
                     help="frames of the same sequence through oracle/_ref/ricvid_ref (0: skip)")
     ap.add_argument("--kstats", default=None)
@@ -139,6 +140,7 @@ def main():
     enc = ric_amd.VideoCodec(True, a.w, a.h)
     dec = ric_amd.VideoCodec(False, a.w, a.h)
     enc.quant = dec.quant = a.q
+    enc.set_host_threads(a.host_threads)
     # warm up on a separate pair (the codec's state is the sequence's)
     we, wd = ric_amd.VideoCodec(True, a.w, a.h), ric_amd.VideoCodec(False, a.w, a.h)
     we.quant = wd.quant = a.q
@@ -156,7 +158,7 @@ def main():
     td = time.perf_counter() - t0
     mpx = a.w * a.h / 1e6
     cpu = cpu_baseline(seq[:a.cpu_frames], a.q) if a.cpu_frames > 0 else None
-    print(json.dumps({"cpu_baseline": cpu,"workload": "video: CRududuCodec %dx%d RGB, quant %d, %d frames (key every 10)"
+    print(json.dumps({"cpu_baseline": cpu, "host_threads": a.host_threads,"workload": "video: CRududuCodec %dx%d RGB, quant %d, %d frames (key every 10)"
                                   % (a.w, a.h, a.q, a.frames),
                       "encode_fps": round(a.frames / te, 2), "decode_fps": round(a.frames / td, 2),
                       "encode_ms_per_frame": round(te / a.frames * 1e3, 2), "decode_ms_per_frame": round(td / a.frames * 1e3, 2),

@@ -106,7 +106,7 @@ def _first_diff(a, b):
     return None if d.size == 0 else (tuple(int(x) for x in d[0]), int(a[tuple(d[0])]), int(b[tuple(d[0])]), len(d))
 
 
-def _check_sequence(ric, w, h, q, n, seed, tmp_path):
+def _check_sequence(ric, w, h, q, n, seed, tmp_path, host_threads=1):
     """CRududuCodec on the GPU vs the reference's classes (oracle/_ref/ricvid_ref),
     frame by frame: stream bytes, encoder output image (with its border: the
     next frame's quarter-pel pass reads it), motion field, decoder output."""
@@ -118,6 +118,8 @@ def _check_sequence(ric, w, h, q, n, seed, tmp_path):
     dec = ric.VideoCodec(False, w, h)
     enc.quant = q
     dec.quant = q
+    if host_threads > 1:
+        enc.set_host_threads(host_threads)
     B = video_seq.BORDER
     for k in range(n):
         e = want[k]
@@ -142,6 +144,12 @@ def test_video_sequences(ric, w, h, q, n, seed, tmp_path):
     """odd and non-multiple-of-8 sizes (the OBMC grid does not cover the
     frame), the finest quantiser, and testmotion.cpp's 1280x720 at quant 20"""
     _check_sequence(ric, w, h, q, n, seed, tmp_path)
+
+
+def test_video_sequence_split_encoder(ric, tmp_path):
+    """the encoder's serial stage with its bands modelled in parallel
+    (ric_video_set_host_threads): the same streams, 12 frames across a key"""
+    _check_sequence(ric, 320, 240, 6, 12, 31, tmp_path, host_threads=6)
 
 
 COMPAT_BIN = os.path.join(HERE, "native", "video_compat")
