@@ -194,8 +194,10 @@ int ric_batch_decode(ric_batch* b, const uint8_t* const* ric, const size_t* len,
  * to host out[i]), in groups of `slots` frames, pipelined. */
 int ric_batch_roundtrip(ric_batch* b, const uint8_t* const* pix, int n, int q, int trans, uint8_t* const* out,
                         const size_t* cap, size_t* len, uint8_t* const* pix_out);
-/* The whole CompressImage of n <= slots gray frames on the GPU, the serial
- * coder included (one wave per frame's stream): pix[i] device pixels; the
+/* The whole CompressImage of n <= slots frames on the GPU, the serial coder
+ * included (one wave per frame's stream; colour: the three planes into one
+ * stream on one wave, as ric.cpp:157-176, with 3 n <= 2 slots: a frame's
+ * plane pyramids take three arenas): pix[i] device pixels; the
  * .ric file of frame i to out + i * ostride (DEVICE memory, cap <= ostride
  * bytes each; cap and ostride multiples of 16, else RIC_E_ARG), its size to
  * len[i] (host).  Byte-identical to ric_batch_encode.
@@ -203,7 +205,8 @@ int ric_batch_roundtrip(ric_batch* b, const uint8_t* const* pix, int n, int q, i
  * one host thread). */
 int ric_batch_encode_gpu(ric_batch* b, const uint8_t* const* pix, int n, int q, int trans, uint8_t* out, size_t ostride,
                          size_t cap, size_t* len);
-/* The whole DecompressImage of n <= slots gray frames on the GPU, the serial
+/* The whole DecompressImage of n <= slots frames on the GPU (colour as for
+ * ric_batch_encode_gpu: 3 n <= 2 slots), the serial
  * decoder included (one wave per stream): the .ric files at in + i * istride
  * (DEVICE memory, istride a multiple of 16), their sizes len[i]; pixels to
  * device pix_out[i].  RIC_E_STREAM as ric_batch_decode. */

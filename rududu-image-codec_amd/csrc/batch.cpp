@@ -220,10 +220,16 @@ int lambda_of(int q, int p) { return q ? quants(q + 13 + (p ? 8 : 0)) : 0; }
 // conversion (p == 0), every forward level + quantiser + block records as one
 // launch per level over the group, then the bands + records of every frame
 // to the host mirrors (one strided copy).  pix: device pixels of each frame.
-int gpu_encode_plane(ric_batch* b, int set, int n, int p, const uint8_t* const* pix, int q, int trans, bool d2h = true)
+// abase / amul: frame i's arena is arena(abase + i * amul) (default: the
+// set's slots, abase = set * slots, amul 1); the GPU stream coder of colour
+// frames keeps a frame's three plane pyramids side by side (amul 3).
+int gpu_encode_plane(ric_batch* b, int set, int n, int p, const uint8_t* const* pix, int q, int trans, bool d2h = true,
+                     int abase = -1, int amul = 1)
 {
 	Pyramid& P = b->P;
 	const int s0 = set * b->slots;
+	if (abase < 0) abase = s0;
+	const size_t ast = (size_t)amul * b->astride;
 	if (p == 0) {
 		auto sp = b->prof.begin(B_PIXIN, n, b->st);
 		for (int i = 0; i < n; i++) launch_pix_in(pix[i], b->plane(s0 + i, 0), b->w, b->h, b->pitch, b->channels, q, b->st);
@@ -236,13 +242,13 @@ int gpu_encode_plane(ric_batch* b, int set, int n, int p, const uint8_t* const* 
 	int qin = quant;
 	for (int l = 0; l < P.nlev; l++) {
 		ZFrames fr;
-		fr.arena = b->arena(s0); fr.astride = b->astride; fr.nz = n;
+		fr.arena = b->arena(abase); fr.astride = ast; fr.nz = n;
 		fr.ring = b->fq_ring;
 		if (l == 0) {
 			fr.src = b->plane(s0, p); fr.sstride = b->pstride; fr.sp = b->pitch;
 		} else {
 			const Band& LL = P.L[l - 1].b[BL];
-			fr.src = b->arena(s0) + LL.off; fr.sstride = b->astride; fr.sp = LL.pitch;
+			fr.src = b->arena(abase) + LL.off; fr.sstride = ast; fr.sp = LL.pitch;
 		}
 		// coding planes: 64-element row pitch, 256-byte aligned slots
 		const int vec8 = 1, vec16 = 1;
@@ -261,7 +267,7 @@ int gpu_encode_plane(ric_batch* b, int set, int n, int p, const uint8_t* const* 
 		} else {
 			// unfused levels (5/3, Haar): the per-frame kernels
 			for (int i = 0; i < n; i++) {
-				char* ar = b->arena(s0 + i);
+				char* ar = b->arena(abase + i * amul);
 				launch_fwd_level(P.L[l], (const char*)fr.src + i * fr.sstride, fr.sp, ar, trans, vec8, b->st);
 				launch_quant_level(P, l, qp, ar, b->st);
 			}
@@ -269,7 +275,7 @@ int gpu_encode_plane(ric_batch* b, int set, int n, int p, const uint8_t* const* 
 		b->prof.end(sp);
 	}
 	for (int i = 0; i < n; i++) {
-		char* ar = b->arena(s0 + i);
+		char* ar = b->arena(abase + i * amul);
 		if (!ll_done) {
 			int Q, iQ, T0;
 			ll_params(P, quant, Q, iQ, T0);
@@ -281,6 +287,7 @@ int gpu_encode_plane(ric_batch* b, int set, int n, int p, const uint8_t* const* 
 	}
 	BCHK(hipGetLastError());
 	if (!d2h) return RIC_OK;
+	if (abase != s0 || amul != 1) return RIC_E_ARG;      // the host mirrors follow the slots
 	auto sp = b->prof.begin(B_D2H, n, b->st);
 	BCHK(hipMemcpy2DAsync(b->harena(s0), b->hstride, b->arena(s0), b->astride, P.b_end, n, hipMemcpyDeviceToHost, b->st));
 	b->prof.end(sp);
@@ -290,10 +297,14 @@ int gpu_encode_plane(ric_batch* b, int set, int n, int p, const uint8_t* const* 
 // The GPU half of DecompressImage for plane p of n frames of set `set`: the
 // host-decoded bands to the device (one strided copy), then every inverse
 // level with the fused TSUQi factors of each frame, as one launch per level.
-int gpu_decode_plane(ric_batch* b, int set, int n, int p, const int* qs, int trans, bool h2d = true)
+int gpu_decode_plane(ric_batch* b, int set, int n, int p, const int* qs, int trans, bool h2d = true, int abase = -1,
+                     int amul = 1)
 {
 	Pyramid& P = b->P;
 	const int s0 = set * b->slots;
+	if (abase < 0) abase = s0;
+	if (h2d && (abase != s0 || amul != 1)) return RIC_E_ARG;
+	const size_t ast = (size_t)amul * b->astride;
 	if (h2d) {
 		auto sp = b->prof.begin(B_H2D, n, b->st);
 		BCHK(hipMemcpy2DAsync(b->arena(s0), b->astride, b->harena(s0), b->hstride, P.a_end, n, hipMemcpyHostToDevice, b->st));
@@ -304,13 +315,13 @@ int gpu_decode_plane(ric_batch* b, int set, int n, int p, const int* qs, int tra
 	for (int l = P.nlev - 1; l >= 0; l--) {
 		const Level& L = P.L[l];
 		ZFrames fr;
-		fr.arena = b->arena(s0); fr.astride = b->astride; fr.nz = n;
+		fr.arena = b->arena(abase); fr.astride = ast; fr.nz = n;
 		int out_int;
 		if (l == 0) {
 			fr.out = b->plane(s0, p); fr.ostride = b->pstride; fr.po = b->pitch; out_int = 0;
 		} else {
 			const Band& LL = P.L[l - 1].b[BL];
-			fr.out = b->arena(s0) + LL.off; fr.ostride = b->astride; fr.po = LL.pitch; out_int = LL.is_int;
+			fr.out = b->arena(abase) + LL.off; fr.ostride = ast; fr.po = LL.pitch; out_int = LL.is_int;
 		}
 		for (int i = 0; i < n; i++) {
 			const int quant = quant_of(qs[i], p);
@@ -485,7 +496,7 @@ extern "C" {
 
 int ric_batch_create(ric_batch** out, int w, int h, int channels, int slots, int threads, int device)
 {
-	if (!out || w < 8 || h < 8 || w > 65535 || h > 65535 || (channels != 1 && channels != 3) || slots < 1 || slots > 1024 ||
+	if (!out || w < 8 || h < 8 || w > 65535 || h > 65535 || (channels != 1 && channels != 3) || slots < 1 || slots > 4096 ||
 	    threads < 1 || threads > 1024)
 		return RIC_E_ARG;
 	*out = nullptr;
@@ -721,18 +732,24 @@ int ric_batch_encode_gpu(ric_batch* b, const uint8_t* const* pix, int n, int q, 
 	if (!b || !pix || !out || !len || n < 0 || n > b->slots || q < 0 || q > 31 || trans < 0 || trans > 2 || cap > ostride ||
 	    cap > 0xFFFFFFF0u || (cap & 15) || (ostride & 15))
 		return RIC_E_ARG;
-	if (b->channels != 1) return RIC_E_ARG;      // one plane per stream here; colour goes through ric_batch_encode
+	// colour: a frame's three plane pyramids sit in arenas 3i, 3i + 1, 3i + 2
+	const int C = b->channels;
+	if (C == 3 && 3 * n > b->nslot()) return RIC_E_ARG;
 	if (n == 0) return RIC_OK;
 	if (set_dev(b->device)) return RIC_E_HIP;
-	int rc = gpu_encode_plane(b, 0, n, 0, pix, q, trans, false);
-	if (rc) return rc;
+	for (int p = 0; p < C; p++) {
+		int rc = C == 1 ? gpu_encode_plane(b, 0, n, 0, pix, q, trans, false)
+		                : gpu_encode_plane(b, 0, n, p, pix, q, trans, false, p, 3);
+		if (rc) return rc;
+	}
 	if (!b->d_genc) {
 		BCHK(hipMalloc(&b->d_genc, sizeof(GEncArgs)));
 		BCHK(hipMalloc(&b->d_res, sizeof(uint32_t) * 2 * b->nslot()));
 		BCHK(hipHostMalloc(&b->h_res, sizeof(uint32_t) * 2 * b->nslot(), 0));
 	}
 	GEncArgs& a = b->genc;
-	a.arena = b->arena(0); a.astride = b->astride;
+	a.arena = b->arena(0); a.astride = (size_t)C * b->astride;
+	a.pstride = b->astride; a.nplanes = C;
 	a.out = out; a.ostride = ostride; a.cap = cap;
 	a.res = b->d_res;
 	a.status_off = (uint32_t)b->P.status_off;
@@ -774,7 +791,8 @@ extern "C" int ric_diag_gdec_dbg(void* dev_buf)
 int ric_batch_decode_gpu(ric_batch* b, const uint8_t* in, size_t istride, const size_t* len, int n, uint8_t* const* pix_out)
 {
 	if (!b || !in || !len || !pix_out || n < 0 || n > b->slots || (istride & 15) || istride > 0xFFFFFFF0u) return RIC_E_ARG;
-	if (b->channels != 1) return RIC_E_ARG;
+	const int C = b->channels;
+	if (C == 3 && 3 * n > b->nslot()) return RIC_E_ARG;
 	if (n == 0) return RIC_OK;
 	if (set_dev(b->device)) return RIC_E_HIP;
 	if (!b->d_genc) {
@@ -793,7 +811,7 @@ int ric_batch_decode_gpu(ric_batch* b, const uint8_t* in, size_t istride, const 
 		int w, h, ch, q, t;
 		int rc = ric_read_header(hd, len[i], &w, &h, &ch, &q, &t);
 		if (rc) return rc;
-		if (w != b->w || h != b->h || ch != 1 || t > 2) return RIC_E_ARG;
+		if (w != b->w || h != b->h || ch != C || t > 2) return RIC_E_ARG;
 		if (t0 >= 0 && t != t0) return RIC_E_ARG;
 		t0 = t; q0 = q; qs[i] = q;
 	}
@@ -802,7 +820,8 @@ int ric_batch_decode_gpu(ric_batch* b, const uint8_t* in, size_t istride, const 
 	for (int i = 0; i < n; i++) b->h_res[2 * i] = (uint32_t)len[i];
 	BCHK(hipMemcpyAsync(b->d_res, b->h_res, sizeof(uint32_t) * 2 * n, hipMemcpyHostToDevice, b->st));
 	GDecArgs& a = b->gdec;
-	a.arena = b->arena(0); a.astride = b->astride;
+	a.arena = b->arena(0); a.astride = (size_t)C * b->astride;
+	a.pstride = b->astride; a.nplanes = C;
 	a.in = in; a.istride = istride;
 	a.lens = b->d_res; a.lens_stride = 2;
 	a.res = b->d_res + 2 * b->slots;          // after the lengths (2 words per frame)
@@ -813,7 +832,9 @@ int ric_batch_decode_gpu(ric_batch* b, const uint8_t* in, size_t istride, const 
 	auto sp = b->prof.begin(B_GDEC, n, b->st);
 	if (launch_gc_decode(b->d_gdec, n, b->st)) return bfail(hipGetLastError(), "k_gc_decode") ? RIC_E_HIP : RIC_E_HIP;
 	b->prof.end(sp);
-	int rc = gpu_decode_plane(b, 0, n, 0, qs.data(), t0, false);
+	int rc = RIC_OK;
+	for (int p = 0; p < C && !rc; p++)
+		rc = C == 1 ? gpu_decode_plane(b, 0, n, 0, qs.data(), t0, false) : gpu_decode_plane(b, 0, n, p, qs.data(), t0, false, p, 3);
 	if (rc) return rc;
 	rc = gpu_pix_out(b, 0, n, qs.data(), pix_out, 1);
 	if (rc) return rc;
@@ -923,6 +944,7 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 		for (int h = 0; h < 2; h++) {
 			GEncArgs& a = c.args[h];
 			a.arena = c.d_ab + (size_t)h * c.n * c.abstride; a.astride = c.abstride;
+			a.pstride = c.abstride; a.nplanes = 1;                        // gray (checked above)
 			a.out = c.d_out + (size_t)h * c.n * c.ocap; a.ostride = c.ocap; a.cap = c.ocap;
 			a.res = c.d_res + res_enc(h);
 			a.status_off = (uint32_t)P.status_off;
@@ -930,6 +952,7 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 			gc_bands(P, a.ll, a.b, a.nb);
 			GDecArgs& d = c.dargs[h];
 			d.arena = (char*)a.arena; d.astride = a.astride;
+			d.pstride = a.pstride; d.nplanes = 1;
 			d.in = a.out; d.istride = c.ocap;
 			d.lens = a.res; d.lens_stride = 2;
 			d.res = c.d_res + res_dec(h);

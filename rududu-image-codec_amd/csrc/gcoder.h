@@ -21,9 +21,13 @@ struct GBandDesc {
 
 // Frames f = 0..n-1 (blockIdx.x): arena + f * astride, out + f * ostride.
 // b[] in coding order: coarsest level first, V, H, D (CodeBand order).
+// nplanes 1 (gray) or 3 (Y, Co, Cg: ric.cpp:157-176 codes them in order into
+// one stream): plane p's pyramid at arena + f * astride + p * pstride.
 struct GEncArgs {
 	const char* arena;
 	size_t astride;
+	size_t pstride;
+	int nplanes;
 	uint8_t* out;
 	size_t ostride;
 	size_t cap;                      // bytes available at each out
@@ -42,6 +46,8 @@ struct GEncArgs {
 struct GDecArgs {
 	char* arena;
 	size_t astride;
+	size_t pstride;                  // as GEncArgs
+	int nplanes;
 	const uint8_t* in;
 	size_t istride;
 	const uint32_t* lens;

@@ -519,17 +519,21 @@ __global__ void __launch_bounds__(64) k_gc_encode(const GEncArgs* __restrict__ a
 	for (int i = (int)threadIdx.x; i < 16 * 16 + 17 * 17; i += 64)
 		g_huff[i] = i < 256 ? kHuff_HIGH[i >> 4][i & 15] : kHuff_LOW[(i - 256) / 17][(i - 256) % 17];
 	__syncthreads();
-	const int32_t status = *gld((const int32_t*)(arena + a.status_off));
+	int32_t status = 0;
+	for (int p = 0; p < a.nplanes; p++) status |= *gld((const int32_t*)(arena + p * a.pstride + a.status_off));
 	GTabs T;
 	T.init();
 	GEnc e;
 	e.init(out, (uint32_t)a.cap, 7);
 	e.hdr0 = 'R' | 'U' << 8 | 'D' << 16 | (uint32_t)'2' << 24;
 	e.hdr1 = (uint32_t)(a.w & 0xFFFF) | (uint32_t)(a.h & 0xFFFF) << 16;
-	e.hdr2 = (uint32_t)((a.q & 31) | ((a.trans & 3) << 6));
-	if (a.ll.is_int) pred_enc<int32_t>(e, T, a.ll, arena);
-	else pred_enc<int16_t>(e, T, a.ll, arena);
-	for (int b = 0; b < a.nb; b++) tree_enc(e, T, a.b[b], arena);
+	e.hdr2 = (uint32_t)((a.q & 31) | ((a.nplanes == 3) << 5) | ((a.trans & 3) << 6));
+	for (int p = 0; p < a.nplanes; p++) {               // Y, Co, Cg into the one stream (ric.cpp:157-176)
+		const char* pa = arena + p * a.pstride;
+		if (a.ll.is_int) pred_enc<int32_t>(e, T, a.ll, pa);
+		else pred_enc<int16_t>(e, T, a.ll, pa);
+		for (int b = 0; b < a.nb; b++) tree_enc(e, T, a.b[b], pa);
+	}
 	const uint32_t end = e.end();
 	uint32_t rc = 0;
 	if (status) rc = 2;                                  // a fused kernel's ring timeout
@@ -1106,7 +1110,8 @@ __global__ void __launch_bounds__(64) k_gc_decode(const GDecArgs* __restrict__ a
 	GTabs T;
 	T.init();
 	GDec d;
-	const uint32_t npay = len > 9 ? (len - 9 < (uint32_t)(a.w * a.h) ? len - 9 : (uint32_t)(a.w * a.h)) : 0u;
+	const uint32_t npix = (uint32_t)(a.w * a.h * a.nplanes);   // ric.cpp:203-205 reads W * H * C payload bytes
+	const uint32_t npay = len > 9 ? (len - 9 < npix ? len - 9 : npix) : 0u;
 	d.init(file, len, (uint32_t)a.istride, npay);
 	auto dump = [&](int k) {
 		if (a.dbg && l == 0) {
@@ -1114,6 +1119,15 @@ __global__ void __launch_bounds__(64) k_gc_decode(const GDecArgs* __restrict__ a
 			o[0] = d.range; o[1] = d.low; o[2] = d.code; o[3] = d.nbits; o[4] = d.buffer; o[5] = d.p; o[6] = d.ovf; o[7] = 0xC0DE;
 		}
 	};
+	for (int p = 0; p + 1 < a.nplanes; p++) {          // colour: Y, Co before the last plane (ric.cpp:207-225)
+		char* pa = arena + p * a.pstride;
+		pred_dec(d, T, a.ll, pa);
+		for (int b = 0; b < a.nb; b++) {
+			const GBandDesc& B = a.b[b];
+			tree_dec(d, T, B, B.par >= 0 ? &a.b[B.par] : nullptr, pa, cnk, binom);
+		}
+	}
+	arena += (a.nplanes - 1) * a.pstride;              // the last (or only) plane, with the diagnostics
 	pred_dec(d, T, a.ll, arena);
 	dump(0);
 	if (a.dbg) {                                     // the decoded LL, row-major (first 1024 values)

@@ -14,12 +14,16 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 G = json.load(open(os.path.join(HERE, "golden", "golden.json")))
 
 
+def _slots(n, c):
+    return n if c == 1 else (3 * n + 1) // 2          # colour: three plane pyramids per frame in 2 x slots arenas
+
+
 def _gpu_encode(ric, frames, q, t):
     import torch
-    h, w = frames[0].shape[-2:]
+    c, h, w = frames[0].shape[-3:]
     dev = [torch.from_numpy(np.ascontiguousarray(f)).cuda() for f in frames]
-    b = ric.Batch(w, h, 1, slots=len(frames), threads=1)
-    ostride = (w * h * 2 + 65536 + 4095) // 4096 * 4096
+    b = ric.Batch(w, h, c, slots=_slots(len(frames), c), threads=1)
+    ostride = (w * h * c * 2 + 65536 + 4095) // 4096 * 4096
     out = torch.zeros(len(frames) * ostride, dtype=torch.uint8, device="cuda")
     lens = b.compress_gpu(dev, out, ostride, q, t)
     host = out.cpu().numpy()
@@ -81,15 +85,15 @@ def test_hybrid_roundtrip(ric, port, w, h, q, t, n, n_host, pool, slots, gpu_dec
             assert np.array_equal(outs[i].cpu().numpy(), port.decode_ric(r)[0]), (rep, i)
 
 
-def _gpu_decode(ric, rics, w, h):
+def _gpu_decode(ric, rics, w, h, c=1):
     import torch
     istride = (max(len(r) for r in rics) + 4095) // 4096 * 4096
     buf = np.zeros(len(rics) * istride, np.uint8)
     for i, r in enumerate(rics):
         buf[i * istride:i * istride + len(r)] = np.frombuffer(r, np.uint8)
     src = torch.from_numpy(buf).cuda()
-    outs = [torch.zeros((1, h, w), dtype=torch.uint8, device="cuda") for _ in rics]
-    b = ric.Batch(w, h, 1, slots=len(rics), threads=1)
+    outs = [torch.zeros((c, h, w), dtype=torch.uint8, device="cuda") for _ in rics]
+    b = ric.Batch(w, h, c, slots=_slots(len(rics), c), threads=1)
     rc = b.decompress_gpu(src, istride, [len(r) for r in rics], outs)
     return rc, [o.cpu().numpy() for o in outs]
 
@@ -161,3 +165,40 @@ def test_gpu_encoder_rejects_unaligned_capacity(ric):
     for ostride, cap in ((8192, 8190), (8200, 8192), (8192, 8192)):
         rc = ric.lib().ric_batch_encode_gpu(b.h, ric._ptrs([frame]), 1, 9, 0, out.data_ptr(), ostride, cap, lens)
         assert rc == (ric.RIC_OK if (cap, ostride) == (8192, 8192) else ric.RIC_E_ARG), (ostride, cap)
+
+
+@pytest.mark.parametrize("w,h,q,t", [(320, 240, 9, 0), (129, 77, 5, 0), (640, 480, 0, 1), (257, 129, 20, 0)])
+def test_gpu_coder_colour_matches_oracle(ric, port, w, h, q, t):
+    """RGB: Y, Co, Cg coded one after the other into one stream on one wave
+    (ric.cpp:157-176, chroma quantisers +C_Q_BOOST), both directions"""
+    frames = [ric.synth(w, h, 3, 70 + i) for i in range(3)]
+    got = _gpu_encode(ric, frames, q, t)
+    for f, r in zip(frames, got):
+        assert r == port.encode_ric(f, q, t)
+    rc, dec = _gpu_decode(ric, got, w, h, 3)
+    for r, g in zip(got, dec):
+        assert np.array_equal(g.reshape(-1), port.decode_ric(r)[0].reshape(-1))
+
+
+def test_gpu_coder_colour_golden_small(ric):
+    n = 0
+    for e in G["small"]:
+        if e["channels"] != 3:
+            continue
+        frame = ric.synth(e["w"], e["h"], 3, e["frame"])
+        gold = open(os.path.join(HERE, "golden", e["name"] + ".ric"), "rb").read()
+        assert _gpu_encode(ric, [frame], e["q"], e["trans"])[0] == gold, e["name"]
+        rc, got = _gpu_decode(ric, [gold], e["w"], e["h"], 3)
+        assert hashlib.sha256(got[0].tobytes()).hexdigest() == e["decoded_sha256"], e["name"]
+        n += 1
+    assert n >= 1
+
+
+def test_gpu_coder_colour_large_sha(ric):
+    """8K RGB through the GPU stream coder both ways: the reference's SHA-256"""
+    e = [x for x in G["large"] if x["name"] == "C3rgb_7680x4320_q9"][0]
+    w, h = e["w"], e["h"]
+    got = _gpu_encode(ric, [ric.synth(w, h, 3, e["frame"])], e["q"], e["trans"])[0]
+    assert hashlib.sha256(got).hexdigest() == e["ric_sha256"]
+    rc, dec = _gpu_decode(ric, [got], w, h, 3)
+    assert hashlib.sha256(dec[0].tobytes()).hexdigest() == e["decoded_sha256"]
