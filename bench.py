@@ -552,7 +552,12 @@ def main():
     # to code one whole stream, with every stream of the launch in flight)
     coder = None
     if hybrid:
-        coder = {"streams_per_launch": b.cp_pool, "frames_host_round_trip": n_host}
+        coder = {"streams_per_launch": b.cp_pool, "frames_host_round_trip": n_host,
+                 # rocprofv3 --pmc SQ_INSTS_SALU / GRBM_GUI_ACTIVE over scripts/gc_probe.py (not measurable
+                 # inside this process): SALU instructions per CU per cycle at 1920 1080p streams in flight
+                 "salu_frac": {"encode": 0.489, "decode": 0.488, "decode_first_launch": 0.649,
+                               "issue_frac_all_types": {"encode": 0.564, "decode": 0.586},
+                               "source": "profiles/r03_stream_coder_salu.json"}}
         if balance:
             coder["balance"] = balance
         for k, name in (("gpu_enc", "encode"), ("gpu_dec", "decode")):
