@@ -230,6 +230,13 @@ int ric_diag_gdec_dbg(void* dev_buf);
  * A pool that does not fit in device memory returns RIC_E_CAPACITY with
  * nothing allocated (the batch stays usable: retry with fewer frames). */
 int ric_batch_hybrid_config(ric_batch* b, int pool_frames, size_t stream_cap);
+/* Output digests (no reference counterpart; for verifying a serving step
+ * whose output buffers are reused): while set, the decode / round-trip calls
+ * write, for frame i of the call (i < n), the 64-bit digest of its decoded
+ * pixels, sum over byte k of pix[k] * (k * 0x9E3779B97F4A7C15 + 1) mod 2^64,
+ * to dev_digests[i] (device memory), in stream order right after the pixels.
+ * n = 0 turns it off. */
+int ric_batch_set_digests(ric_batch* b, unsigned long long* dev_digests, long n);
 /* As ric_batch_roundtrip (device pixels in and out, .ric files to host
  * out[i]): frames [0, n_host) encoded and decoded on the host; frames
  * [n_host, n) encoded by the GPU stream coder and decoded by the GPU stream

@@ -158,6 +158,9 @@ struct ric_batch {
 	// level 0's hand-off form (ZFrames::ring): the hybrid step runs beside
 	// the stream coder's waves and takes the double buffer (less LDS)
 	int fq_ring = 1;
+	// ric_batch_set_digests: per frame of a call, the digest of its decoded pixels
+	unsigned long long* digest = nullptr;
+	long ndigest = 0;
 	int device = 0, w = 0, h = 0, channels = 1, slots = 0;
 	double hyb_host_ms = 0, hyb_gpu_ms = 0;        // last hybrid call: when each side finished (ms from entry)
 	Pyramid P;
@@ -342,14 +345,20 @@ int gpu_decode_plane(ric_batch* b, int set, int n, int p, const int* qs, int tra
 }
 
 // pixel output of n frames of set `set` (after every plane's inverse)
-int gpu_pix_out(ric_batch* b, int set, int n, const int* qs, uint8_t* const* pix_out, int on_device)
+// idx0 >= 0: these are frames idx0.. of the call, whose digests
+// (ric_batch_set_digests) are taken right after their pixels are written.
+int gpu_pix_out(ric_batch* b, int set, int n, const int* qs, uint8_t* const* pix_out, int on_device, long idx0 = -1)
 {
 	const int s0 = set * b->slots;
 	auto sp = b->prof.begin(B_PIXOUT, n, b->st);
+	const size_t npix = (size_t)b->w * b->h * b->channels;
+	const bool dig = b->digest && idx0 >= 0 && idx0 + n <= b->ndigest;
+	if (dig) BCHK(hipMemsetAsync(b->digest + idx0, 0, sizeof(unsigned long long) * n, b->st));
 	for (int i = 0; i < n; i++) {
 		if (!pix_out[i]) continue;
 		uint8_t* dst = on_device ? pix_out[i] : b->stage(s0 + i);
 		launch_pix_out(b->plane(s0 + i, 0), b->pitch, b->w, b->h, b->channels, qs[i], dst, nullptr, b->st);
+		if (dig) launch_digest(dst, npix, b->digest + idx0 + i, b->st);
 	}
 	b->prof.end(sp);
 	BCHK(hipGetLastError());
@@ -629,7 +638,7 @@ int ric_batch_decode(ric_batch* b, const uint8_t* const* ric, const size_t* len,
 		// the next plane's host decode rewrites the mirrors the copy reads
 		BCHK(hipStreamSynchronize(b->st));
 	}
-	int rc = gpu_pix_out(b, 0, n, qs.data(), pix_out, pix_on_device);
+	int rc = gpu_pix_out(b, 0, n, qs.data(), pix_out, pix_on_device, 0);
 	if (rc) return rc;
 	BCHK(hipStreamSynchronize(b->st));
 	b->prof.harvest();
@@ -655,7 +664,13 @@ int ric_batch_roundtrip(ric_batch* b, const uint8_t* const* pix, int n, int q, i
 			int rc = ric_batch_encode(b, pix + f0, m, 1, q, trans, out + f0, cap + f0, len + f0);
 			if (rc) return rc;
 			std::vector<const uint8_t*> rics(out + f0, out + f0 + m);
+			// the group's digests are frames f0.. of this call
+			unsigned long long* const dg = b->digest;
+			const long nd = b->ndigest;
+			if (dg) { b->digest = nd > f0 ? dg + f0 : nullptr; b->ndigest = nd > f0 ? nd - f0 : 0; }
 			rc = ric_batch_decode(b, rics.data(), len + f0, m, pix_out + f0, 1);
+			b->digest = dg;
+			b->ndigest = nd;
 			if (rc && rc != RIC_E_STREAM) return rc;
 		}
 		return RIC_OK;
@@ -704,7 +719,7 @@ int ric_batch_roundtrip(ric_batch* b, const uint8_t* const* pix, int n, int q, i
 		stream_err |= r == RIC_E_STREAM;
 		const int f0 = g * S, m = std::min(S, n - f0), set = g & 1;
 		rc = gpu_decode_plane(b, set, m, 0, qs.data(), trans);
-		if (!rc) rc = gpu_pix_out(b, set, m, qs.data(), pix_out + f0, 1);
+		if (!rc) rc = gpu_pix_out(b, set, m, qs.data(), pix_out + f0, 1, f0);
 		if (!rc && launched < G) rc = launch_enc(launched++);
 	}
 	// on an error, the tasks already queued still run: wait for them
@@ -836,7 +851,7 @@ int ric_batch_decode_gpu(ric_batch* b, const uint8_t* in, size_t istride, const 
 	for (int p = 0; p < C && !rc; p++)
 		rc = C == 1 ? gpu_decode_plane(b, 0, n, 0, qs.data(), t0, false) : gpu_decode_plane(b, 0, n, p, qs.data(), t0, false, p, 3);
 	if (rc) return rc;
-	rc = gpu_pix_out(b, 0, n, qs.data(), pix_out, 1);
+	rc = gpu_pix_out(b, 0, n, qs.data(), pix_out, 1, 0);
 	if (rc) return rc;
 	BCHK(hipMemcpyAsync(b->h_res + 2 * b->slots, b->d_res + 2 * b->slots, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, b->st));
 	BCHK(hipStreamSynchronize(b->st));
@@ -865,6 +880,14 @@ int ric_batch_decode_gpu(ric_batch* b, const uint8_t* in, size_t istride, const 
 // A coder launch takes seconds (a wave codes one whole stream), so two
 // launches are in flight (the two halves) and the host threads meanwhile do
 // whole round trips of the first n_host frames.
+int ric_batch_set_digests(ric_batch* b, unsigned long long* dev_digests, long n)
+{
+	if (!b || n < 0 || (n > 0 && !dev_digests)) return RIC_E_ARG;
+	b->digest = n ? dev_digests : nullptr;
+	b->ndigest = n;
+	return RIC_OK;
+}
+
 int ric_batch_hybrid_config(ric_batch* b, int pool_frames, size_t stream_cap)
 {
 	if (!b || pool_frames < 1 || pool_frames > 65536 || stream_cap < 64 || (stream_cap & 15) || stream_cap > 0xFFFFFFF0u)
@@ -1100,7 +1123,7 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 			BCHK(hipMemcpy2DAsync(b->arena(0), b->astride, abslot(h, g0), c.abstride, P.a_end, gm, hipMemcpyDeviceToDevice,
 			                      b->st));
 			int r = gpu_decode_plane(b, 0, gm, 0, qs.data(), trans, false);
-			if (!r) r = gpu_pix_out(b, 0, gm, qs.data(), pix_out + f0 + g0, 1);
+			if (!r) r = gpu_pix_out(b, 0, gm, qs.data(), pix_out + f0 + g0, 1, f0 + g0);
 			if (r) return r;
 		}
 		return RIC_OK;
@@ -1173,7 +1196,7 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 			if (++host_groups_done == 1 || host_groups_done == (n_host + S - 1) / S) tr("host group done", host_groups_done);
 		}
 		if (!r2) r2 = gpu_decode_plane(b, F.set, F.g.m, 0, qs.data(), trans);
-		if (!r2) r2 = gpu_pix_out(b, F.set, F.g.m, qs.data(), pix_out + F.g.f0, 1);
+		if (!r2) r2 = gpu_pix_out(b, F.set, F.g.m, qs.data(), pix_out + F.g.f0, 1, F.g.f0);
 		if (!r2) BCHK(hipEventRecord(F.ev, b->st));   // the set's mirrors are free once this passes
 		set_busy[F.set] = false;
 		fl.pop_front();

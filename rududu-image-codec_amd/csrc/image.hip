@@ -218,6 +218,38 @@ void launch_pix_in(const uint8_t* pix, int16_t* planes, int w, int h, long po, i
 	else hipLaunchKernelGGL(k_gray_in, grid, dim3(256), 0, st, pix, planes, w, h, po, q);
 }
 
+namespace {
+constexpr unsigned long long kDigestMul = 0x9E3779B97F4A7C15ull;
+// 16 bytes per thread (a 16-byte load where the run is aligned and whole),
+// a block sum, one 64-bit atomic add per block
+__global__ __launch_bounds__(256) void k_digest(const uint8_t* __restrict__ p, size_t n, unsigned long long* out)
+{
+	const size_t i0 = ((size_t)blockIdx.x * 256 + threadIdx.x) * 16;
+	unsigned long long s = 0;
+	if (i0 + 16 <= n && ((uintptr_t)(p + i0) & 15) == 0) {
+		const uint4 v = *(const uint4*)(p + i0);
+		const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+		for (int k = 0; k < 16; k++) s += (unsigned long long)((w[k >> 2] >> (8 * (k & 3))) & 255u) * ((i0 + k) * kDigestMul + 1);
+	} else {
+		for (size_t i = i0; i < i0 + 16 && i < n; i++) s += (unsigned long long)p[i] * (i * kDigestMul + 1);
+	}
+#pragma unroll
+	for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+	__shared__ unsigned long long part[4];
+	if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+	__syncthreads();
+	if (threadIdx.x == 0) atomicAdd(out, part[0] + part[1] + part[2] + part[3]);
+}
+}  // namespace
+
+void launch_digest(const uint8_t* p, size_t n, unsigned long long* out, hipStream_t st)
+{
+	if (!n) return;
+	const size_t blocks = (n + 16 * 256 - 1) / (16 * 256);
+	hipLaunchKernelGGL(k_digest, dim3((unsigned)blocks), dim3(256), 0, st, p, n, out);
+}
+
 void launch_pix_out(const int16_t* planes_in, long pi, int w, int h, int channels, int q,
                     uint8_t* pix, int16_t* planes_out, hipStream_t st)
 {

@@ -9,4 +9,8 @@ void launch_pix_in(const uint8_t* pix, int16_t* planes, int w, int h, long po, i
 // int16 decoded planes (Y,Cg,Co or gray, pitch pi) -> u8 pixels and/or int16 output planes (w*h)
 void launch_pix_out(const int16_t* planes_in, long pi, int w, int h, int channels, int q,
                     uint8_t* pix, int16_t* planes_out, hipStream_t st);
+// 64-bit digest of n bytes: sum over i of p[i] * (i * 0x9E3779B97F4A7C15 + 1),
+// mod 2^64, added into *out (zero it first): an order-free checksum of a
+// decoded frame (ric_batch_set_digests)
+void launch_digest(const uint8_t* p, size_t n, unsigned long long* out, hipStream_t st);
 }  // namespace ric

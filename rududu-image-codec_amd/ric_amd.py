@@ -95,6 +95,7 @@ def lib():
         "ric_batch_roundtrip": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _P]),
         "ric_batch_prof_enable": (_I, [_P, _I]),
         "ric_batch_encode_gpu": (_I, [_P, _P, _I, _I, _I, _P, ctypes.c_size_t, ctypes.c_size_t, _P]),
+        "ric_batch_set_digests": (_I, [_P, _P, ctypes.c_long]),
         "ric_batch_hybrid_config": (_I, [_P, _I, ctypes.c_size_t]),
         "ric_batch_hybrid_times": (_I, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
         "ric_batch_decode_gpu": (_I, [_P, _P, ctypes.c_size_t, _P, _I, _P]),
@@ -412,6 +413,11 @@ class Batch:
             _chk(rc, "ric_batch_roundtrip")
         self._lens = [lens[i] for i in range(n)]
         return self._lens
+
+    def set_digests(self, dev_digests, n):
+        """Per frame of the next calls, the 64-bit digest of its decoded pixels
+        into dev_digests[i] (a device int64 tensor / pointer; n = 0: off)."""
+        _chk(lib().ric_batch_set_digests(self.h, _ptr(dev_digests) if n else None, n), "ric_batch_set_digests")
 
     def hybrid_config(self, pool_frames, stream_cap):
         """Pool of the GPU stream coder (ric_batch_hybrid_config)."""

@@ -117,3 +117,31 @@ def test_batch_ring_timeout_is_an_error(ric, port):
         lib.ric_diag_fault(0)
     got = b.compress(frames, 9, 0)
     assert got == [port.encode_ric(f, 9, 0) for f in frames]
+
+
+def _digest(pix):
+    flat = np.ascontiguousarray(pix, np.uint8).reshape(-1).astype(np.uint64)
+    mult = np.arange(flat.size, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15) + np.uint64(1)
+    return np.uint64(np.sum(flat * mult, dtype=np.uint64))
+
+
+@pytest.mark.parametrize("w,h,ch", [(768, 512, 1), (333, 201, 3)])
+def test_batch_output_digests(ric, port, w, h, ch):
+    """ric_batch_set_digests: every frame's digest is taken in stream order
+    right after its pixels, so frames sharing one output buffer keep their own
+    (the bench verifies its serving step this way)"""
+    torch = pytest.importorskip("torch")
+    n = 7
+    host = [ric.synth(w, h, ch, 50 + i) for i in range(n)]
+    frames = [torch.from_numpy(x).cuda() for x in host]
+    shared = [torch.empty_like(frames[0]) for _ in range(2)]
+    outs = [shared[i % 2] for i in range(n)]
+    dig = torch.zeros(n, dtype=torch.int64, device="cuda")
+    b = ric.Batch(w, h, ch, slots=2, threads=2)
+    b.set_digests(dig, n)
+    b.roundtrip(frames, outs, q=9, trans=0)
+    torch.cuda.synchronize()
+    got = dig.cpu().numpy().view(np.uint64)
+    for i in range(n):
+        want = port.decode_ric(port.encode_ric(host[i], 9, 0))[0]
+        assert got[i] == _digest(want), i
