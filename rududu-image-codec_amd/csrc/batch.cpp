@@ -772,7 +772,7 @@ int ric_batch_encode_gpu(ric_batch* b, const uint8_t* const* pix, int n, int q, 
 	gc_bands(b->P, a.ll, a.b, a.nb);
 	BCHK(hipMemcpyAsync(b->d_genc, &a, sizeof(GEncArgs), hipMemcpyHostToDevice, b->st));
 	auto sp = b->prof.begin(B_GENC, n, b->st);
-	if (launch_gc_encode(b->d_genc, n, b->st)) return bfail(hipGetLastError(), "k_gc_encode") ? RIC_E_HIP : RIC_E_HIP;
+	if (launch_gc_encode(b->d_genc, n, q == 0, b->st)) return bfail(hipGetLastError(), "k_gc_encode") ? RIC_E_HIP : RIC_E_HIP;
 	b->prof.end(sp);
 	BCHK(hipMemcpyAsync(b->h_res, b->d_res, sizeof(uint32_t) * 2 * n, hipMemcpyDeviceToHost, b->st));
 	BCHK(hipStreamSynchronize(b->st));
@@ -1031,7 +1031,7 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 		BCHK(hipEventRecord(c.ev_fwd[h], b->st));
 		BCHK(hipStreamWaitEvent(c.st[h], c.ev_fwd[h], 0));
 		auto sp = b->prof.begin(B_GENC, m, c.st[h]);
-		if (launch_gc_encode(c.d_args + h, m, c.st[h])) return bfail(hipGetLastError(), "k_gc_encode") ? RIC_E_HIP : RIC_E_HIP;
+		if (launch_gc_encode(c.d_args + h, m, q == 0, c.st[h])) return bfail(hipGetLastError(), "k_gc_encode") ? RIC_E_HIP : RIC_E_HIP;
 		b->prof.end(sp);
 		BCHK(hipMemcpyAsync(c.h_res + res_enc(h), c.d_res + res_enc(h), sizeof(uint32_t) * 2 * c.n, hipMemcpyDeviceToHost,
 		                    c.st[h]));

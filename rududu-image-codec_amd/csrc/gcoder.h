@@ -63,7 +63,8 @@ int launch_gc_decode(const GDecArgs* dev_args, int nframes, hipStream_t st);
 
 // k_gc_encode over n frames: the whole .ric file of each (gray, one plane).
 // dev_args: the argument block in device memory.
-int launch_gc_encode(const GEncArgs* dev_args, int nframes, hipStream_t st);
+// lossless: q == 0 (the 8 KiB byte ring; lossy streams take a 4 KiB one).
+int launch_gc_encode(const GEncArgs* dev_args, int nframes, int lossless, hipStream_t st);
 
 // Fill the band descriptors (coding order) of a pyramid.
 inline void gc_bands(const Pyramid& P, GBandDesc& ll, GBandDesc* b, int& nb)

@@ -69,15 +69,24 @@ struct GTabs {
 // lanes, 16-byte stores) once no reservation slot points into them: single
 // byte stores would each hold the vector-memory counter the walk's prefetch
 // loads are waited on with.
-constexpr uint32_t kRing = 8192;        // bytes of LDS per wave (small: the wave shares its CU with the level kernels)
+// Two ring sizes, one kernel each: 8 KiB for lossless streams (a chunk of 64
+// blocks of wide int coefficients can write ~4 KiB), 4 KiB for lossy ones,
+// whose chunks write well under 3 KiB: a 4 KiB ring keeps the wave's LDS at
+// ~9 KiB like the decoder's, so the level kernels still fit beside many
+// coder waves on a CU.  A chunk that overruns its ring is flagged either way.
 constexpr uint32_t kFlush = 1024;
-__shared__ __attribute__((aligned(16))) uint8_t g_ring[kRing];
+__shared__ __attribute__((aligned(16))) uint8_t g_ring8[8192];
+__shared__ __attribute__((aligned(16))) uint8_t g_ring4[4096];
+template <uint32_t R> GC_DI uint8_t* ring_base();
+template <> GC_DI uint8_t* ring_base<8192>() { return g_ring8; }
+template <> GC_DI uint8_t* ring_base<4096>() { return g_ring4; }
 __shared__ uint16_t g_huff[16 * 16 + 17 * 17];  // kHuff_HIGH rows, then kHuff_LOW rows
 __shared__ uint32_t g_coef[64 * 16];             // the current chunk's coefficients, 16 per block
 
 // CMuxCodec encoder state.  Byte positions are offsets from `out`; the four
 // reservation slots of the carry-less coder (last[], muxcodec.cpp:63-74) are a
 // FIFO q0..q3: normalize_enc writes the front one and appends p.
+template <uint32_t kRing>
 struct GEnc {
 	uint8_t* out;
 	uint32_t cap;
@@ -91,23 +100,23 @@ struct GEnc {
 
 	// every lane writes the same byte (no exec-mask change per byte); the
 	// capacity is checked where bytes leave the ring (maybe_flush / end)
-	GC_DI void put(uint32_t slot, uint32_t v) { g_ring[slot & (kRing - 1)] = (uint8_t)v; }
+	GC_DI void put(uint32_t slot, uint32_t v) { ring_base<kRing>()[slot & (kRing - 1)] = (uint8_t)v; }
 	// copy ring bytes [flushed, upto) (upto a multiple of 16, or the end) to HBM
 	GC_DI void flush_to(uint32_t upto)
 	{
 		if (flushed == 0 && upto > 0) {
 			// the header overwrites the coder's two leading bytes (out + 7, + 8)
 			if (lane_id() == 0) {
-				uint32_t* r = (uint32_t*)g_ring;
+				uint32_t* r = (uint32_t*)ring_base<kRing>();
 				r[0] = hdr0; r[1] = hdr1;
-				g_ring[8] = (uint8_t)hdr2;
+				ring_base<kRing>()[8] = (uint8_t)hdr2;
 			}
 		}
 		const uint32_t l = lane_id();
 		for (uint32_t b = flushed; b < upto; b += 64 * 16) {
 			const uint32_t o = b + l * 16;
 			if (o < upto && o + 16 <= cap) {
-				const u32x4 v = *(const u32x4*)(g_ring + (o & (kRing - 1)));
+				const u32x4 v = *(const u32x4*)(ring_base<kRing>() + (o & (kRing - 1)));
 				*gst((u32x4*)(out + o)) = v;
 			}
 		}
@@ -207,7 +216,8 @@ struct GEnc {
 struct GBit {
 	uint32_t st;
 	GC_DI void init() { st = 2048u; }
-	GC_DI void code(GEnc& e, const GTabs& T, uint32_t sym, uint32_t c)   // bitcodec.h:52-60, 81-92
+	template <typename E>
+	GC_DI void code(E& e, const GTabs& T, uint32_t sym, uint32_t c)   // bitcodec.h:52-60, 81-92
 	{
 		const uint32_t v = lget(st, c);
 		uint32_t freq = v & 0xFFFFu, sh = (v >> 16) & 0xFFu, mps = v >> 24;
@@ -236,8 +246,8 @@ struct GGeoCtx {
 	GC_DI uint32_t packed() const { return freq | idx << 16; }
 	// magnitude - 1 (unary + k raw bits) then, if SIGNED, one raw sign bit:
 	// the remainder and the sign as one chunk
-	template <bool SIGNED>
-	GC_DI void code(GEnc& e, const GTabs& T, uint32_t sym, uint32_t sign)
+	template <bool SIGNED, typename E>
+	GC_DI void code(E& e, const GTabs& T, uint32_t sym, uint32_t sign)
 	{
 		const uint32_t f = freq;
 		uint32_t fr = freq;
@@ -287,7 +297,8 @@ GC_DI void taboo_lanes(uint32_t& nbl, uint32_t& suml)   // lane i < 32: nb[i], s
 	nbl = l < 2 ? 1u : fb;
 	suml = sm;
 }
-GC_DI void taboo_code(GEnc& e, uint32_t nbv)
+template <typename E>
+GC_DI void taboo_code(E& e, uint32_t nbv)
 {
 	uint32_t nbl, suml;
 	taboo_lanes(nbl, suml);
@@ -315,8 +326,8 @@ GC_DI void taboo_code(GEnc& e, uint32_t nbv)
 // CBandCodec::pred<encode> (LL DPCM), bandcodec.cpp:62-104.  The residuals and
 // contexts of a 64-coefficient run of a row are computed by the lanes; the
 // scalar walk codes them in order.
-template <typename C>
-GC_DI void pred_enc(GEnc& e, const GTabs& T, const GBandDesc& B, const char* arena)
+template <typename C, typename E>
+GC_DI void pred_enc(E& e, const GTabs& T, const GBandDesc& B, const char* arena)
 {
 	static constexpr uint8_t ginit[16] = {9,10,11,12,13,14,15,16,17,18,19,20,21,22,23,15};
 	const GAS C* c = gld((const C*)(arena + B.off));
@@ -412,7 +423,8 @@ GC_DI RecChunk fetch_recs(const uint64_t* rec, const uint8_t* pin, int dx, int d
 // The coefficients of one block: unary + raw remainder + sign each, one
 // geometric context (CGeomCodec::code, geomcodec.h:41-57; block_enum's
 // coefficient loop, bandcodec.cpp:392-401).
-GC_DI void code_coefs(GEnc& e, const GTabs& T, uint32_t& geo, uint32_t gc, uint32_t mask, uint32_t cv, uint32_t cb)
+template <typename E>
+GC_DI void code_coefs(E& e, const GTabs& T, uint32_t& geo, uint32_t gc, uint32_t mask, uint32_t cv, uint32_t cb)
 {
 	GGeoCtx g;
 	g.load(geo, gc, T);
@@ -428,7 +440,8 @@ GC_DI void code_coefs(GEnc& e, const GTabs& T, uint32_t& geo, uint32_t gc, uint3
 // CBandCodec::tree<encode> over the GPU block records (encoder.cpp
 // tree_rec_fast; bandcodec.cpp:484-589 with block_enum :346-478).  high: the
 // finest level (HIGH tables); par: the band has a parent level.
-GC_DI void tree_enc(GEnc& e, const GTabs& T, const GBandDesc& B, const char* arena)
+template <typename E>
+GC_DI void tree_enc(E& e, const GTabs& T, const GBandDesc& B, const char* arena)
 {
 	const bool high = B.high, par = B.has_pin;
 	const uint64_t* rec = (const uint64_t*)(arena + B.rec_off);
@@ -510,6 +523,7 @@ GC_DI void tree_enc(GEnc& e, const GTabs& T, const GBandDesc& B, const char* are
 // fine, V, H, D.  The .ric file goes to out + f * ostride: the 9-byte header
 // (ric.cpp:142-152) then the payload; the coder buffer starts at out + 7 and
 // the header overwrites its two dropped leading bytes (as ric_codec).
+template <uint32_t RING>
 __global__ void __launch_bounds__(64) k_gc_encode(const GEncArgs* __restrict__ ap)
 {
 	const GEncArgs& a = *ap;
@@ -523,7 +537,7 @@ __global__ void __launch_bounds__(64) k_gc_encode(const GEncArgs* __restrict__ a
 	for (int p = 0; p < a.nplanes; p++) status |= *gld((const int32_t*)(arena + p * a.pstride + a.status_off));
 	GTabs T;
 	T.init();
-	GEnc e;
+	GEnc<RING> e;
 	e.init(out, (uint32_t)a.cap, 7);
 	e.hdr0 = 'R' | 'U' << 8 | 'D' << 16 | (uint32_t)'2' << 24;
 	e.hdr1 = (uint32_t)(a.w & 0xFFFF) | (uint32_t)(a.h & 0xFFFF) << 16;
@@ -1172,11 +1186,16 @@ static size_t gc_dyn_lds(const void* kernel)
 	return (size_t)want > fa.sharedSizeBytes ? (size_t)want - fa.sharedSizeBytes : 0;
 }
 
-int launch_gc_encode(const GEncArgs* dev_args, int nframes, hipStream_t st)
+int launch_gc_encode(const GEncArgs* dev_args, int nframes, int lossless, hipStream_t st)
 {
 	if (nframes <= 0) return 0;
-	static const size_t dyn = gc_dyn_lds((const void*)k_gc_encode);
-	hipLaunchKernelGGL(k_gc_encode, dim3(nframes), dim3(64), dyn, st, dev_args);
+	if (lossless) {
+		static const size_t dyn = gc_dyn_lds((const void*)k_gc_encode<8192>);
+		hipLaunchKernelGGL(k_gc_encode<8192>, dim3(nframes), dim3(64), dyn, st, dev_args);
+	} else {
+		static const size_t dyn = gc_dyn_lds((const void*)k_gc_encode<4096>);
+		hipLaunchKernelGGL(k_gc_encode<4096>, dim3(nframes), dim3(64), dyn, st, dev_args);
+	}
 	return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
