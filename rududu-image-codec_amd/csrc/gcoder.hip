@@ -18,6 +18,9 @@
 // Output is byte-identical to the host coder (encoder.cpp / entropy.cpp),
 // i.e. to the reference's tree<encode> / pred<encode> / CMuxCodec.
 #include <hip/hip_runtime.h>
+#include <mutex>
+#include <vector>
+#include <cstdlib>
 #include <cstdint>
 #include <cstdlib>
 
@@ -573,6 +576,15 @@ constexpr uint32_t kDMargin = 512;     // staged bytes kept ahead of a block / a
 __shared__ __attribute__((aligned(16))) uint8_t g_dring[kDRing];
 __shared__ int32_t g_blk[64 * 16];     // the current chunk's decoded blocks, 16 values each
 
+// enumDecode<16> patterns for k = 1..8 (filled once per device by
+// launch_gc_decode): g_enum16[g_enum16_off[k] + code]
+// Constant memory: the index is wave-uniform, so the load is a scalar one
+// (s_load_dword through the scalar cache, counted on lgkmcnt), which does not
+// wait on the walk's vector prefetch loads the way a vector load would.
+constexpr int kEnum16N = 39202;
+__constant__ uint32_t g_enum16[(kEnum16N + 1) / 2];       // two patterns per word, low half first
+__constant__ uint32_t g_enum16_off[9];
+
 struct GDec {
 	// Staging-only values, held in VGPRs (the lanes use them; the scalar walk
 	// never does): the file's address, the payload size n (ric.cpp: at most
@@ -792,6 +804,23 @@ struct GDec {
 		}
 		return out;
 	}
+	// enumDecode<16> by table (the host decoder's decoder.cpp enum16): the
+	// pattern of (k, code) for k <= 8, complemented above 8.  One load from a
+	// 78 KB table in HBM (L2 / scalar-cache resident) instead of k ballot rows.
+	GC_DI uint32_t enum16(const uint32_t (&cnk)[2], const uint32_t (&binom)[2], uint32_t k)
+	{
+		const bool comp = k > 8;
+		const uint32_t kk = comp ? 16 - k : k;
+		uint32_t c = enum_code(cnk, kk, 16);
+		// C(16, kk) = C(15, kk) + C(15, kk - 1): the host reads code 0 past it (corrupt streams)
+		const uint32_t i1 = (kk - 1) * 16 + 15, i0 = (kk - 2) * 16 + 15;
+		const uint32_t a1 = i1 < 64 ? lget(binom[0], i1) : lget(binom[1], i1 - 64);
+		const uint32_t a0 = kk < 2 ? 1u : (i0 < 64 ? lget(binom[0], i0) : lget(binom[1], i0 - 64));
+		if (c >= a1 + a0) c = 0;
+		const uint32_t i = g_enum16_off[kk] + c;
+		const uint32_t m = (g_enum16[i >> 1] >> ((i & 1) * 16)) & 0xFFFFu;
+		return comp ? ~m & 0xFFFFu : m;
+	}
 	GC_DI uint32_t max_dec(uint32_t max)                 // maxDecode, muxcodec.cpp:526-534
 	{
 		uint32_t value = 0;
@@ -1004,6 +1033,7 @@ GC_DI uint32_t block_info(const GBandDesc& B, const GBandDesc* P, const char* ar
 // chunks of 64 blocks in scan order; each chunk's values are built in LDS and
 // stored by the lanes (every position of every block, so no Clear() pass), the
 // parent anchors the chunk consumed are cleared by the lanes too.
+template <bool ETAB>
 GC_DI void tree_dec(GDec& d, const GTabs& T, const GBandDesc& B, const GBandDesc* P, char* arena,
                     const uint32_t (&cnk)[2], const uint32_t (&binom)[2])
 {
@@ -1050,7 +1080,7 @@ GC_DI void tree_dec(GDec& d, const GTabs& T, const GBandDesc& B, const GBandDesc
 				const uint32_t hrow = l < hn ? (uint32_t)g_huff[hbase + idx * hn + l] : 0u;
 				const uint32_t k = d.huff(hrow, hn) + (high ? 1u : 0u);
 				if (high || k != 0) {
-					uint32_t sig = k != 16 ? d.enum_n(cnk, binom, k, 16, true) : 0xFFFFu;
+					uint32_t sig = k == 16 ? 0xFFFFu : ETAB ? d.enum16(cnk, binom, k) : d.enum_n(cnk, binom, k, 16, true);
 					GGeoD g;
 					g.load(geo, k - 1, T);
 					while (sig) {
@@ -1100,6 +1130,7 @@ GC_DI void tree_dec(GDec& d, const GTabs& T, const GBandDesc& B, const GBandDesc
 // order (src/ric/ric.cpp:207-225 -> CWavelet2D::DecodeBand,
 // src/lib/wavelet2d.cpp:179-222): the coarsest LL, then coarse to fine V, H, D.
 // The bands land in the frame's arena, ready for the inverse kernels.
+template <bool ETAB>
 __global__ void __launch_bounds__(64) k_gc_decode(const GDecArgs* __restrict__ ap)
 {
 	const GDecArgs& a = *ap;
@@ -1138,7 +1169,7 @@ __global__ void __launch_bounds__(64) k_gc_decode(const GDecArgs* __restrict__ a
 		pred_dec(d, T, a.ll, pa);
 		for (int b = 0; b < a.nb; b++) {
 			const GBandDesc& B = a.b[b];
-			tree_dec(d, T, B, B.par >= 0 ? &a.b[B.par] : nullptr, pa, cnk, binom);
+			tree_dec<ETAB>(d, T, B, B.par >= 0 ? &a.b[B.par] : nullptr, pa, cnk, binom);
 		}
 	}
 	arena += (a.nplanes - 1) * a.pstride;              // the last (or only) plane, with the diagnostics
@@ -1151,7 +1182,7 @@ __global__ void __launch_bounds__(64) k_gc_decode(const GDecArgs* __restrict__ a
 	}
 	for (int b = 0; b < a.nb; b++) {
 		const GBandDesc& B = a.b[b];
-		tree_dec(d, T, B, B.par >= 0 ? &a.b[B.par] : nullptr, arena, cnk, binom);
+		tree_dec<ETAB>(d, T, B, B.par >= 0 ? &a.b[B.par] : nullptr, arena, cnk, binom);
 		dump(b + 1);
 	}
 	// status in bits 0-3; on a staging overrun, the read position (diagnostic)
@@ -1199,11 +1230,55 @@ int launch_gc_encode(const GEncArgs* dev_args, int nframes, int lossless, hipStr
 	return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// the enumDecode<16> table, once per device (enumCode, muxcodec.cpp:352-359:
+// code = sum over set bits of C(position, rank + 1))
+static int enum16_upload(hipStream_t st)
+{
+	static std::mutex mu;
+	static uint64_t done = 0;                        // devices 0..63
+	int dev = 0;
+	if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return -1;
+	std::lock_guard<std::mutex> g(mu);
+	if (done >> dev & 1) return 0;
+	uint32_t C[17][17];
+	for (int n = 0; n < 17; n++)
+		for (int r = 0; r < 17; r++) C[n][r] = r == 0 ? 1 : n == 0 ? 0 : C[n - 1][r - 1] + C[n - 1][r];
+	uint32_t off[9] = {0};
+	uint32_t n = 0;
+	for (int k = 1; k <= 8; k++) { off[k] = n; n += C[16][k]; }
+	if (n != (uint32_t)kEnum16N) return -1;
+	std::vector<uint16_t> pat(n, 0);
+	for (uint32_t b = 1; b < 65536; b++) {
+		const int k = __builtin_popcount(b);
+		if (k > 8) continue;
+		uint32_t code = 0, row = 0;
+		for (int i = 0; i < 16; i++)
+			if (b & (1u << i)) { code += C[i][row + 1]; row++; }
+		pat[off[k] + code] = (uint16_t)b;
+	}
+	pat.resize((n + 1) & ~1u, 0);
+	if (hipMemcpyToSymbolAsync(HIP_SYMBOL(g_enum16), pat.data(), pat.size() * sizeof(uint16_t), 0, hipMemcpyHostToDevice, st) !=
+	        hipSuccess ||
+	    hipMemcpyToSymbolAsync(HIP_SYMBOL(g_enum16_off), off, sizeof(off), 0, hipMemcpyHostToDevice, st) != hipSuccess ||
+	    hipStreamSynchronize(st) != hipSuccess)
+		return -1;
+	done |= 1ull << dev;
+	return 0;
+}
+
 int launch_gc_decode(const GDecArgs* dev_args, int nframes, hipStream_t st)
 {
 	if (nframes <= 0) return 0;
-	static const size_t dyn = gc_dyn_lds((const void*)k_gc_decode);
-	hipLaunchKernelGGL(k_gc_decode, dim3(nframes), dim3(64), dyn, st, dev_args);
+	// RIC_GC_ETAB=0: the lane-parallel enumerative decode instead of the table
+	static const bool etab = [] { const char* e = getenv("RIC_GC_ETAB"); return !e || atoi(e) != 0; }();
+	if (etab) {
+		if (enum16_upload(st)) return -1;
+		static const size_t dyn = gc_dyn_lds((const void*)k_gc_decode<true>);
+		hipLaunchKernelGGL(k_gc_decode<true>, dim3(nframes), dim3(64), dyn, st, dev_args);
+	} else {
+		static const size_t dyn = gc_dyn_lds((const void*)k_gc_decode<false>);
+		hipLaunchKernelGGL(k_gc_decode<false>, dim3(nframes), dim3(64), dyn, st, dev_args);
+	}
 	return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
