@@ -125,8 +125,8 @@ def default_n_host(a, threads):
 
 def host_frames_room(a, threads):
     """Host round trips a step has frames for: with --coder gpu and no --n-host
-    the split is balanced after the warmup (up to 64 per thread)."""
-    return 64 * threads if (a.n_host < 0 and a.coder == "gpu") else default_n_host(a, threads)
+    the split is balanced after the warmup (up to 112 per thread)."""
+    return 112 * threads if (a.n_host < 0 and a.coder == "gpu") else default_n_host(a, threads)
 
 
 def host_info():
