@@ -104,6 +104,21 @@ int ric_band_write(ric_wavelet* w, int index, const int32_t* host_in);
  * from the device; the mirror stays authoritative -- what the caller writes
  * there is what the next GPU stage reads -- until a stage rewrites the bands. */
 int ric_band_host(ric_wavelet* w, int index, void** ptr, int* pitch);
+/* CBand's operations on one band (band index as ric_band_info), run on the
+ * device (bands written through ric_band_host go to the device first; the host
+ * mirror is stale afterwards):
+ *   ric_band_tsuq   CBand::TSUQ<C>(Quant, Thres) (src/lib/band.h:65-92), the
+ *                   non-zero count and the Max / Min of the quantised values;
+ *   ric_band_tsuqi  CBand::TSUQi<C>(Quant) (band.h:94-107);
+ *   ric_band_sums   CBand::Mean's Sum and SSum (band.h:116-132: int products,
+ *                   int64 sums); Mean and Var follow from them on the host;
+ *   ric_band_add    CBand::Add<C>(val) (band.h:135-141), padding included;
+ *   ric_band_clear  CBand::Clear (band.cpp). */
+int ric_band_tsuq(ric_wavelet* w, int index, int quant, float thres, unsigned int* count, int* max, int* min);
+int ric_band_tsuqi(ric_wavelet* w, int index, int quant);
+int ric_band_sums(ric_wavelet* w, int index, int64_t* sum, int64_t* ssum);
+int ric_band_add(ric_wavelet* w, int index, int val);
+int ric_band_clear(ric_wavelet* w, int index);
 
 /* ------------------------------------------------------------- ric_mux */
 /* CMuxCodec(unsigned char* pStream, unsigned short firstWord)

@@ -185,67 +185,37 @@ public:
 	BandData pBand;
 	band_t type = sshort;
 
-	// src/lib/band.h:65-92, on the host mirror
+	// src/lib/band.h:65-92, on the device (ric_band_tsuq)
 	template <class C> unsigned int TSUQ(int Quant, float Thres)
 	{
-		Quant = (int)(Quant / Weight);
-		if (Quant == 0) Quant = 1;
-		const int iQuant = (int)(1 << 16) / Quant;
-		const C T = (C)(Thres * Quant);
-		int mn = 0, mx = 0;
-		Count = 0;
-		C* p = (C*)pBand;
-		for (unsigned int j = 0; j < DimY; j++, p += DimXAlign)
-			for (unsigned int i = 0; i < DimX; i++) {
-				if ((unsigned int)(p[i] + T) <= (unsigned int)(2 * T)) {
-					p[i] = 0;
-				} else {
-					Count++;
-					p[i] = (C)((int)((unsigned int)p[i] * (unsigned int)iQuant + (1u << 15)) >> 16);
-					if (p[i] > mx) mx = p[i];
-					if (p[i] < mn) mn = p[i];
-				}
-			}
-		Min = mn;
+		unsigned int n = 0;
+		int mx = 0, mn = 0;
+		ric_check(ric_band_tsuq(pBand.w_, pBand.index_, Quant, Thres, &n, &mx, &mn), "CBand::TSUQ");
+		Count = n;
 		Max = mx;
+		Min = mn;
 		return Count;
 	}
-	// src/lib/band.h:94-107
-	template <class C> void TSUQi(C Quant)
-	{
-		Quant = (C)(Quant / Weight);
-		if (Quant == 0) Quant = 1;
-		C* p = (C*)pBand;
-		for (unsigned int j = 0; j < DimY; j++, p += DimXAlign)
-			for (unsigned int i = 0; i < DimX; i++) p[i] = (C)(p[i] * Quant);
-	}
-	// src/lib/band.h:116-132, the reference's arithmetic: the products in
-	// int, the sample-count square in unsigned (both wrap on big bands)
+	// src/lib/band.h:94-107, on the device
+	template <class C> void TSUQi(C Quant) { ric_check(ric_band_tsuqi(pBand.w_, pBand.index_, (int)Quant), "CBand::TSUQi"); }
+	// src/lib/band.h:116-132: the sums on the device (the reference's
+	// arithmetic: int products, int64 sums), then its float formula with the
+	// sample-count square in unsigned (both wrap on big bands)
 	template <class C> void Mean(float& Mean, float& Var)
 	{
 		int64_t Sum = 0, SSum = 0;
-		const C* p = (const C*)pBand;
-		for (unsigned int j = 0; j < DimY; j++)
-			for (unsigned int i = 0; i < DimX; i++) {
-				const int v = p[i + j * DimXAlign];
-				Sum += v;
-				SSum += (int)((unsigned int)v * (unsigned int)v);
-			}
+		ric_check(ric_band_sums(pBand.w_, pBand.index_, &Sum, &SSum), "CBand::Mean");
 		const unsigned int n = DimX * DimY;
 		Mean = (float)Sum * Weight / n;
 		Var = ((float)(SSum - Sum * Sum)) * Weight * Weight / (n * n);
 	}
-	// src/lib/band.h:135-141
-	template <class C> void Add(C val)
-	{
-		C* p = (C*)pBand;
-		for (unsigned int i = 0; i < BandSize; i++) p[i] += val;
-	}
-	// src/lib/band.cpp:162-167 (recurse: the finer bands too)
+	// src/lib/band.h:135-141, on the device (every sample of the rows)
+	template <class C> void Add(C val) { ric_check(ric_band_add(pBand.w_, pBand.index_, (int)val), "CBand::Add"); }
+	// src/lib/band.cpp:162-167 (recurse: the finer bands too), on the device
 	void Clear(bool recurse = false)
 	{
 		if (!pBand) return;
-		std::memset((void*)pBand, 0, (size_t)BandSize * (type == sint ? 4 : 2));
+		ric_check(ric_band_clear(pBand.w_, pBand.index_), "CBand::Clear");
 		if (recurse && pChild) pChild->Clear(true);
 	}
 	// src/lib/band.h:145-155

@@ -749,6 +749,94 @@ int ric_tsuqi(ric_wavelet* w, int quant)
 	return tsuqi(w, quant);
 }
 
+// ---- one band on the device (CBand, src/lib/band.h:65-141).  Bands a caller
+// wrote through pBand go to the device first; the host mirror is stale after.
+namespace {
+int band_begin(ric_wavelet* w, int index)
+{
+	if (!w || index < 0 || index >= w->P.nbands()) return RIC_E_ARG;
+	if (set_dev(w->device)) return RIC_E_HIP;
+	if (flush_pending(w)) return RIC_E_HIP;
+	return to_device(w);
+}
+}  // namespace
+
+int ric_band_tsuq(ric_wavelet* w, int index, int quant, float thres, unsigned int* count, int* max, int* min)
+{
+	int rc = band_begin(w, index);
+	if (rc) return rc;
+	const Band& B = w->P.band(index);
+	// band.h:68-72: Quant = (int)(Quant / Weight), at least 1; T = (C)(Thres * Quant)
+	int Q = (int)((float)quant / B.weight);
+	if (Q == 0) Q = 1;
+	const int iQ = (1 << 16) / Q;
+	const int T0 = tr_any(!B.is_int, (int)(thres * (float)Q));
+	int* d = nullptr;
+	HIPCHK(hipMallocAsync((void**)&d, 3 * sizeof(int), w->st));
+	HIPCHK(hipMemsetAsync(d, 0, 3 * sizeof(int), w->st));
+	launch_band_tsuq(B, iQ, T0, w->d_arena, d, w->st);
+	int h[3] = {0, 0, 0};
+	HIPCHK(hipMemcpyAsync(h, d, sizeof(h), hipMemcpyDeviceToHost, w->st));
+	HIPCHK(hipFreeAsync(d, w->st));
+	HIPCHK(hipStreamSynchronize(w->st));
+	w->host_valid = false;
+	if (count) *count = (unsigned int)h[0];
+	if (max) *max = h[1];
+	if (min) *min = h[2];
+	return RIC_OK;
+}
+
+int ric_band_tsuqi(ric_wavelet* w, int index, int quant)
+{
+	int rc = band_begin(w, index);
+	if (rc) return rc;
+	const Band& B = w->P.band(index);
+	launch_dequant_band(B, tsuqi_factor(B, quant), w->d_arena, w->st);   // band.h:94-107
+	HIPCHK(hipGetLastError());
+	HIPCHK(hipStreamSynchronize(w->st));
+	w->host_valid = false;
+	return RIC_OK;
+}
+
+int ric_band_sums(ric_wavelet* w, int index, int64_t* sum, int64_t* ssum)
+{
+	int rc = band_begin(w, index);
+	if (rc) return rc;
+	unsigned long long* d = nullptr;
+	HIPCHK(hipMallocAsync((void**)&d, 2 * sizeof(unsigned long long), w->st));
+	HIPCHK(hipMemsetAsync(d, 0, 2 * sizeof(unsigned long long), w->st));
+	launch_band_sums(w->P.band(index), w->d_arena, d, w->st);
+	unsigned long long h[2] = {0, 0};
+	HIPCHK(hipMemcpyAsync(h, d, sizeof(h), hipMemcpyDeviceToHost, w->st));
+	HIPCHK(hipFreeAsync(d, w->st));
+	HIPCHK(hipStreamSynchronize(w->st));
+	if (sum) *sum = (int64_t)h[0];
+	if (ssum) *ssum = (int64_t)h[1];
+	return RIC_OK;
+}
+
+int ric_band_add(ric_wavelet* w, int index, int val)
+{
+	int rc = band_begin(w, index);
+	if (rc) return rc;
+	launch_band_add(w->P.band(index), val, w->d_arena, w->st);
+	HIPCHK(hipGetLastError());
+	HIPCHK(hipStreamSynchronize(w->st));
+	w->host_valid = false;
+	return RIC_OK;
+}
+
+int ric_band_clear(ric_wavelet* w, int index)
+{
+	int rc = band_begin(w, index);
+	if (rc) return rc;
+	const Band& B = w->P.band(index);
+	HIPCHK(hipMemsetAsync(w->d_arena + B.off, 0, B.bytes(), w->st));
+	HIPCHK(hipStreamSynchronize(w->st));
+	w->host_valid = false;
+	return RIC_OK;
+}
+
 int ric_band_count(ric_wavelet* w) { return w ? w->P.nbands() : RIC_E_ARG; }
 
 int ric_band_info(ric_wavelet* w, int index, int* dimx, int* dimy, int* is_int, float* weight)

@@ -134,7 +134,99 @@ __global__ void k_dequant(T* p, int pitch, int dx, int dy, int q)
 	*e = (T)tr<SH>((int)((uint32_t)(int)*e * (uint32_t)q));
 }
 
+// CBand::TSUQ on one band with its statistics (band.h:65-92): stats[0] +=
+// the non-zero count, stats[1] = max(stats[1], quantised value), stats[2] =
+// min(...), over the values the reference compares (the stored C value).
+template <typename T>
+__global__ __launch_bounds__(256) void k_band_tsuq(T* p, int pitch, int dx, int dy, int iQ, int T0, int* stats)
+{
+	constexpr bool SH = sizeof(T) == 2;
+	const int i = blockIdx.x * blockDim.x + threadIdx.x;
+	unsigned nz = 0;
+	int mx = 0, mn = 0;
+	if (i < dx * dy) {
+		T* q = p + (long)(i / dx) * pitch + i % dx;
+		const int v = *q;
+		if ((uint32_t)(v + T0) <= (uint32_t)(2 * T0)) *q = 0;
+		else {
+			const int r = tr<SH>((int)((uint32_t)v * (uint32_t)iQ + 32768u) >> 16);
+			*q = (T)r;
+			nz = 1; mx = r > 0 ? r : 0; mn = r < 0 ? r : 0;
+		}
+	}
+#pragma unroll
+	for (int o = 32; o > 0; o >>= 1) {
+		mx = max(mx, __shfl_xor(mx, o, 64));
+		mn = min(mn, __shfl_xor(mn, o, 64));
+	}
+	const unsigned long long b = __ballot(nz);
+	if ((threadIdx.x & 63) == 0) {
+		if (b) atomicAdd(stats, (int)__popcll(b));
+		if (mx) atomicMax(stats + 1, mx);
+		if (mn) atomicMin(stats + 2, mn);
+	}
+}
+
+// CBand::Mean's sums (band.h:116-132): Sum of the values (int64), SSum of
+// their squares as the reference computes them (an int product, wrapping)
+template <typename T>
+__global__ __launch_bounds__(256) void k_band_sums(const T* p, int pitch, int dx, int dy, unsigned long long* out)
+{
+	const int i = blockIdx.x * blockDim.x + threadIdx.x;
+	long long s = 0, ss = 0;
+	if (i < dx * dy) {
+		const int v = p[(long)(i / dx) * pitch + i % dx];
+		s = v;
+		ss = (int)((uint32_t)v * (uint32_t)v);
+	}
+#pragma unroll
+	for (int o = 32; o > 0; o >>= 1) {
+		s += __shfl_xor(s, o, 64);
+		ss += __shfl_xor(ss, o, 64);
+	}
+	if ((threadIdx.x & 63) == 0) {
+		atomicAdd(out, (unsigned long long)s);
+		atomicAdd(out + 1, (unsigned long long)ss);
+	}
+}
+
+// CBand::Add (band.h:135-141): every sample of the band's rows, padding included
+template <typename T>
+__global__ __launch_bounds__(256) void k_band_add(T* p, long n, int val)
+{
+	constexpr bool SH = sizeof(T) == 2;
+	const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+	if (i < n) p[i] = (T)tr<SH>((int)((uint32_t)(int)p[i] + (uint32_t)val));
+}
+
 }  // namespace
+
+void launch_band_tsuq(const Band& B, int iQ, int T0, char* arena, int* stats, hipStream_t st)
+{
+	const int n = B.dx * B.dy;
+	if (n == 0) return;
+	const dim3 grid((n + 255) / 256);
+	if (B.is_int) hipLaunchKernelGGL(k_band_tsuq<int32_t>, grid, dim3(256), 0, st, (int32_t*)(arena + B.off), B.pitch, B.dx, B.dy, iQ, T0, stats);
+	else hipLaunchKernelGGL(k_band_tsuq<int16_t>, grid, dim3(256), 0, st, (int16_t*)(arena + B.off), B.pitch, B.dx, B.dy, iQ, T0, stats);
+}
+
+void launch_band_sums(const Band& B, const char* arena, unsigned long long* out, hipStream_t st)
+{
+	const int n = B.dx * B.dy;
+	if (n == 0) return;
+	const dim3 grid((n + 255) / 256);
+	if (B.is_int) hipLaunchKernelGGL(k_band_sums<int32_t>, grid, dim3(256), 0, st, (const int32_t*)(arena + B.off), B.pitch, B.dx, B.dy, out);
+	else hipLaunchKernelGGL(k_band_sums<int16_t>, grid, dim3(256), 0, st, (const int16_t*)(arena + B.off), B.pitch, B.dx, B.dy, out);
+}
+
+void launch_band_add(const Band& B, int val, char* arena, hipStream_t st)
+{
+	const long n = (long)B.pitch * B.dy;
+	if (n == 0) return;
+	const dim3 grid((unsigned)((n + 255) / 256));
+	if (B.is_int) hipLaunchKernelGGL(k_band_add<int32_t>, grid, dim3(256), 0, st, (int32_t*)(arena + B.off), n, val);
+	else hipLaunchKernelGGL(k_band_add<int16_t>, grid, dim3(256), 0, st, (int16_t*)(arena + B.off), n, val);
+}
 
 void launch_quant_level(const Pyramid& P, int l, const QuantParams& qp, char* arena, hipStream_t st)
 {

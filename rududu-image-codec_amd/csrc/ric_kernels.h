@@ -56,6 +56,13 @@ void launch_blocks_level(const Pyramid& P, int l, bool do_rec, bool do_pin, char
 void launch_tsuq_band(const Band& B, int iQ, int T0, char* arena, unsigned int* count, hipStream_t st);
 // CBand::TSUQi on one band (src/lib/band.h:94-107).
 void launch_dequant_band(const Band& B, int q, char* arena, hipStream_t st);
+// CBand::TSUQ with its statistics: stats[0] += non-zeros, stats[1] max=,
+// stats[2] min= (device ints, initialised by the caller to 0, 0, 0)
+void launch_band_tsuq(const Band& B, int iQ, int T0, char* arena, int* stats, hipStream_t st);
+// CBand::Mean's Sum and SSum (device u64[2], zeroed by the caller)
+void launch_band_sums(const Band& B, const char* arena, unsigned long long* out, hipStream_t st);
+// CBand::Add(val) over the band's rows (padding included)
+void launch_band_add(const Band& B, int val, char* arena, hipStream_t st);
 // ------------------------------------------------------- batched launches
 // nz frames at fixed strides: frame f's arena is arena + f * astride, its
 // level input src + f * sstride (bytes, row pitch sp elements), its inverse

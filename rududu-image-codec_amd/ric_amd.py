@@ -49,6 +49,11 @@ def lib():
         "ric_wavelet_destroy": (None, [_P]),
         "ric_wavelet_set_stream": (_I, [_P, _P]),
         "ric_wavelet_set_host_threads": (_I, [_P, _I]),
+        "ric_band_tsuq": (_I, [_P, _I, _I, ctypes.c_float, _P, _P, _P]),
+        "ric_band_tsuqi": (_I, [_P, _I, _I]),
+        "ric_band_sums": (_I, [_P, _I, _P, _P]),
+        "ric_band_add": (_I, [_P, _I, _I]),
+        "ric_band_clear": (_I, [_P, _I]),
         "ric_wavelet_sync": (_I, [_P]),
         "ric_set_weight": (_I, [_P, _I, _F]),
         "ric_transform": (_I, [_P, _P, _I, _I, _I]),
@@ -237,6 +242,28 @@ class Wavelet2D:
     def set_host_threads(self, n):
         """CodeBand's serial half over n host threads (bands modelled in parallel)."""
         _chk(lib().ric_wavelet_set_host_threads(self.h, n), "set_host_threads")
+
+    # CBand's operations on band i (device): TSUQ, TSUQi, Mean's sums, Add, Clear
+    def band_tsuq(self, i, quant, thres):
+        """-> (count, max, min)"""
+        c, mx, mn = ctypes.c_uint(), ctypes.c_int(), ctypes.c_int()
+        _chk(lib().ric_band_tsuq(self.h, i, quant, thres, ctypes.byref(c), ctypes.byref(mx), ctypes.byref(mn)),
+             "CBand::TSUQ")
+        return c.value, mx.value, mn.value
+
+    def band_tsuqi(self, i, quant):
+        _chk(lib().ric_band_tsuqi(self.h, i, quant), "CBand::TSUQi")
+
+    def band_sums(self, i):
+        s, ss = ctypes.c_int64(), ctypes.c_int64()
+        _chk(lib().ric_band_sums(self.h, i, ctypes.byref(s), ctypes.byref(ss)), "CBand::Mean")
+        return s.value, ss.value
+
+    def band_add(self, i, val):
+        _chk(lib().ric_band_add(self.h, i, val), "CBand::Add")
+
+    def band_clear(self, i):
+        _chk(lib().ric_band_clear(self.h, i), "CBand::Clear")
 
     def sync(self):
         _chk(lib().ric_wavelet_sync(self.h), "sync")

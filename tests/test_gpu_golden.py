@@ -332,3 +332,51 @@ def test_codeband_split_encoder(ric, port):
     W1.CodeBand(m1, 96, 36)
     m1.endCoding()
     assert np.array_equal(buf, buf1)
+
+
+def test_band_operations(ric):
+    """CBand's TSUQ / TSUQi / Mean / Add / Clear on single bands, on the
+    device (ric_band_*), against numpy restatements of src/lib/band.h:65-141"""
+    w, h = 257, 130
+    pl = O.gray_plane(ric.synth(w, h, 1, 3)[0], 9)
+    W = ric.Wavelet2D(w, h, 5, 1)
+    W.SetWeight(0)
+    W.Transform(pl, w, 0)
+    raw = W.bands()
+    f32 = np.float32
+    for i in range(W.band_count()):
+        _, _, isint, wt = W.band_info(i)
+        # TSUQ(96, 0.6)
+        Q = int(f32(96) / f32(wt)) or 1
+        iQ = 65536 // Q
+        T = int(f32(0.6) * f32(Q))
+        T = T if isint else int(np.int16(T))
+        v = raw[i].astype(np.int64)
+        dead = ((v + T) & 0xFFFFFFFF) <= ((2 * T) & 0xFFFFFFFF)
+        q = (((v * iQ + 32768) & 0xFFFFFFFF).astype(np.uint32).view(np.int32) >> 16).astype(np.int64)
+        q = q if isint else q.astype(np.int16).astype(np.int64)
+        exp = np.where(dead, 0, q)
+        cnt, mx, mn = W.band_tsuq(i, 96, 0.6)
+        got = W.bands()[i]
+        assert np.array_equal(got, exp), i
+        assert cnt == int((~dead).sum()) and mx == max(0, int(exp.max())) and mn == min(0, int(exp.min())), i
+        # Mean's sums
+        s, ss = W.band_sums(i)
+        e = exp.astype(np.int64)
+        assert s == int(e.sum())
+        assert ss == int(((e * e) & 0xFFFFFFFF).astype(np.uint32).view(np.int32).astype(np.int64).sum())
+        # TSUQi(40)
+        W.band_tsuqi(i, 40)
+        qi = 40 if isint else int(np.int16(40))
+        qi = int(f32(qi) / f32(wt))
+        qi = (qi if isint else int(np.int16(qi))) or 1
+        e2 = e * qi
+        e2 = e2.astype(np.int32) if isint else e2.astype(np.int16)
+        assert np.array_equal(W.bands()[i], e2.astype(np.int64)), i
+        # Add(-3), Clear
+        W.band_add(i, -3)
+        e3 = e2.astype(np.int64) - 3
+        e3 = e3.astype(np.int32) if isint else e3.astype(np.int16)
+        assert np.array_equal(W.bands()[i], e3.astype(np.int64)), i
+    W.band_clear(0)
+    assert not W.bands()[0].any()
