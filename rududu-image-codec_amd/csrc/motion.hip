@@ -250,27 +250,62 @@ __global__ __launch_bounds__(64) void k_vid_epzs_full(EpzsArgs a)
 			for (int k = 1; k < n; k++)                     // sets B and C (:151-161)
 				if (cand[k] != kVidIntra && bd > sd[k]) { best = cand[k]; bd = sd[k]; }
 			// DiamondSearch (obme.cpp:79-108): the four neighbours of the
-			// centre, never straight back along the last two moves
+			// centre, never straight back along the last two moves.  The
+			// SADs come two steps at a time: one round of loads covers the
+			// 12 positions within two unit moves of the centre (lane k of
+			// vsd: ring 1 in the step order up, down, left, right, then
+			// (0,-2) (0,2) (-2,0) (2,0) (-1,-1) (1,-1) (-1,1) (1,1); lane 12,
+			// the centre, is never taken: going back is excluded), and the
+			// second step reads its four candidates there (kStep2) instead
+			// of waiting on another round of loads.
+			constexpr int kOx[12] = {0, 0, -1, 1, 0, 0, -2, 2, -1, 1, -1, 1};
+			constexpr int kOy[12] = {-1, 1, 0, 0, -2, 2, 0, 0, -1, -1, 1, 1};
+			// step-2 candidates (up, down, left, right) after step-1 move m,
+			// 4 bits each, up in the high nibble of m's 16 bits
+			constexpr uint64_t kStep2 = 0x4C89ull | 0xC5ABull << 16 | 0x8A6Cull << 32 | 0x9BC7ull << 48;
+			const int dx[4] = {0, 0, -1, 1}, dy[4] = {-1, 1, 0, 0};
+			const int tst[4] = {kDown, kUp, kRight, kLeft}, stp[4] = {kUp, kDown, kLeft, kRight};
 			int last = 0, last2 = 0;
-			for (int it = 0; it < 65536; it++) {
+			for (int it = 0; it < 65536; it += 2) {
 				const int bxv = mvx(best), byv = mvy(best);
-				const int dx[4] = {0, 0, -1, 1}, dy[4] = {-1, 1, 0, 0};
-				const int tst[4] = {kDown, kUp, kRight, kLeft}, stp[4] = {kUp, kDown, kLeft, kRight};
-				int q[4];
+				int q[12];
 #pragma unroll
-				for (int k = 0; k < 4; k++)
-					q[k] = ref_px(ref, a, cx + (int16_t)(bxv + dx[k]), cy + (int16_t)(byv + dy[k]), lane);
-				int d4[4];
+				for (int k = 0; k < 12; k++)
+					q[k] = ref_px(ref, a, cx + (int16_t)(bxv + kOx[k]), cy + (int16_t)(byv + kOy[k]), lane);
+				int vsd = 0x7FFFFFFF;
 #pragma unroll
-				for (int k = 0; k < 4; k++) d4[k] = sad_of(abs(cur - q[k]));
-				int move = 0;
+				for (int k = 0; k < 12; k++) {
+					const int d = sad_of(abs(cur - q[k]));
+					vsd = lane == k ? d : vsd;
+				}
+				// step 1: ring 1, lanes 0..3
+				int move = 0, mk = 0;
 #pragma unroll
-				for (int k = 0; k < 4; k++)
-					if (!(last2 & tst[k]) && bd > d4[k]) {
+				for (int k = 0; k < 4; k++) {
+					const int d = __builtin_amdgcn_readlane(vsd, k);
+					if (!(last2 & tst[k]) && bd > d) {
 						best = mvmake(bxv + dx[k], byv + dy[k]);
-						bd = d4[k];
+						bd = d;
+						move = stp[k];
+						mk = k;
+					}
+				}
+				last2 = move | last;
+				last = move;
+				if (!last) break;
+				// step 2 from the new centre, candidates from the same round
+				const int b2x = mvx(best), b2y = mvy(best);
+				move = 0;
+#pragma unroll
+				for (int k = 0; k < 4; k++) {
+					const int idx = (int)((kStep2 >> (16 * mk + 4 * (3 - k))) & 15u);
+					const int d = __builtin_amdgcn_readlane(vsd, idx);
+					if (!(last2 & tst[k]) && bd > d) {
+						best = mvmake(b2x + dx[k], b2y + dy[k]);
+						bd = d;
 						move = stp[k];
 					}
+				}
 				last2 = move | last;
 				last = move;
 				if (!last) break;
