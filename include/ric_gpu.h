@@ -269,9 +269,11 @@ int ric_batch_hybrid_times(ric_batch* b, double* host_ms, double* gpu_ms);
  * in, 1..8 forward level 0..7 (fused DWT + quantiser + records), 9 D2H of
  * bands + records, 10 host encode, 11 host decode, 12 H2D of the bands,
  * 13..20 inverse level 0..7 (fused TSUQi), 21 pixel conversion out, 22 / 23 the
- * GPU stream encoder / decoder launches (ms = kernel time, frames = streams).  ms are
+ * GPU stream encoder / decoder launches (ms = kernel time, frames = streams), 24
+ * the compacted payload values of host-coded frames to the host (host-timed;
+ * stage 9 then covers only the dense rest: int bands, LL, records).  ms are
  * sums; frames = frames covered; launches = GPU launches (host: frames). */
-#define RIC_BATCH_STAGES 24
+#define RIC_BATCH_STAGES 25
 /* Diagnostics: the batch's GPU stages alone, iters times over n <= slots
  * device frames (forward levels + D2H, H2D + inverse levels of the bands just
  * quantised, pixel output to pix_out if given); no host coding. */

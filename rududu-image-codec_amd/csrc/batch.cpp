@@ -36,6 +36,7 @@
 #include "codec_params.h"
 #include "gcoder.h"
 #include "host_pool.h"
+#include "compact.h"
 
 using namespace ric;
 
@@ -86,8 +87,9 @@ private:
 // inv level 0..7, pix_out, gpu stream encode, gpu stream decode
 // (RIC_BATCH_STAGES; the stream coder stages are per launch: ms = kernel
 // time, frames = streams).
+// B_D2HV: the compacted values of a host-coded frame (host-timed, per frame)
 enum { B_PIXIN = 0, B_FWD = 1, B_D2H = 9, B_HENC = 10, B_HDEC = 11, B_H2D = 12, B_INV = 13, B_PIXOUT = 21, B_GENC = 22, B_GDEC = 23,
-       B_COUNT = 24 };
+       B_D2HV = 24, B_COUNT = 25 };
 
 struct BProf {
 	bool on = false;
@@ -158,6 +160,22 @@ struct ric_batch {
 	// level 0's hand-off form (ZFrames::ring): the hybrid step runs beside
 	// the stream coder's waves and takes the double buffer (less LDS)
 	int fq_ring = 1;
+	// The host encoder's payload compacted on the GPU (compact.hip): the
+	// 16-bit bands' values in walk order instead of the dense bands.  Per
+	// slot: the stream (d_cmp), chunk counts / offsets, its value count (also
+	// pinned on the host); cmp_ok[s]: slot s's last forward pass compacted.
+	bool compact = true;
+	char* d_cmp = nullptr;
+	size_t cmp_stride = 0;
+	uint32_t* d_cmp_cnt = nullptr;
+	size_t cmp_cstride = 0;
+	uint32_t* d_cmp_total = nullptr;
+	uint32_t* h_cmp_total = nullptr;
+	CmpArgs* d_cmp_args = nullptr;                 // one block per slot set
+	int cmp_nchunk = 0;
+	size_t cmp_dense = 0;                          // arena offset where the dense part starts
+	std::vector<char> cmp_ok;
+	std::vector<hipStream_t> cmp_st;               // per slot: the task's own copy stream
 	// ric_batch_set_digests: per frame of a call, the digest of its decoded pixels
 	unsigned long long* digest = nullptr;
 	long ndigest = 0;
@@ -291,6 +309,20 @@ int gpu_encode_plane(ric_batch* b, int set, int n, int p, const uint8_t* const* 
 	BCHK(hipGetLastError());
 	if (!d2h) return RIC_OK;
 	if (abase != s0 || amul != 1) return RIC_E_ARG;      // the host mirrors follow the slots
+	if (b->compact) {
+		// the 16-bit bands' values in walk order (compact.hip), their counts
+		// to the host; the dense rest (int bands, LL, region B) by one copy.
+		// Each host task copies its own frame's values once the group's
+		// event has passed (host_encode_plane).
+		if (launch_compact(b->d_cmp_args + set, b->cmp_nchunk, n, b->st)) return bfail(hipGetLastError(), "compact") ? RIC_E_HIP : RIC_E_HIP;
+		BCHK(hipMemcpyAsync(b->h_cmp_total + s0, b->d_cmp_total + s0, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, b->st));
+		auto sp = b->prof.begin(B_D2H, n, b->st);
+		BCHK(hipMemcpy2DAsync(b->harena(s0) + b->cmp_dense, b->hstride, b->arena(s0) + b->cmp_dense, b->astride,
+		                      P.b_end - b->cmp_dense, n, hipMemcpyDeviceToHost, b->st));
+		b->prof.end(sp);
+		for (int i = 0; i < n; i++) b->cmp_ok[s0 + i] = 1;
+		return RIC_OK;
+	}
 	auto sp = b->prof.begin(B_D2H, n, b->st);
 	BCHK(hipMemcpy2DAsync(b->harena(s0), b->hstride, b->arena(s0), b->astride, P.b_end, n, hipMemcpyDeviceToHost, b->st));
 	b->prof.end(sp);
@@ -387,6 +419,19 @@ int host_encode_plane(ric_batch* b, int s, int p, int q, int trans, uint8_t* out
 		set_last_error("fused level kernel: LDS ring hand-off timed out (device status word set; output discarded)");
 		return RIC_E_HIP;
 	}
+	const int16_t* cp = nullptr;
+	if (b->compact && b->cmp_ok[s]) {
+		// this frame's compacted values (the group's event has passed)
+		const double tc = now_ms();
+		const size_t nb = (size_t)b->h_cmp_total[s] * 2;
+		if (nb > b->cmp_stride) return set_last_error("compacted payload larger than its slot"), RIC_E_HIP;
+		if (nb) {
+			BCHK(hipMemcpyAsync(b->harena(s), b->d_cmp + (size_t)s * b->cmp_stride, nb, hipMemcpyDeviceToHost, b->cmp_st[s]));
+			BCHK(hipStreamSynchronize(b->cmp_st[s]));
+		}
+		b->prof.host(B_D2HV, now_ms() - tc);
+		cp = (const int16_t*)b->harena(s);
+	}
 	const double t0 = now_ms();
 	pred_encode(m, b->view(s, P.coarsest_ll()));
 	for (int l = P.nlev - 1; l >= 0; l--) {
@@ -395,7 +440,8 @@ int host_encode_plane(ric_batch* b, int s, int p, int q, int trans, uint8_t* out
 			const Band& B = P.L[l].b[order[k]];
 			const uint64_t* rec = (const uint64_t*)(b->harena(s) + P.rec_off[l][order[k]]);
 			const uint8_t* pin = l + 1 < P.nlev ? (const uint8_t*)(b->harena(s) + P.pin_off[l][order[k]]) : nullptr;
-			tree_encode_records_fast(m, rec, pin, b->view(s, B), l == 0);
+			if (cp && !B.is_int) tree_encode_records_compact(m, rec, pin, b->view(s, B), l == 0, &cp);
+			else tree_encode_records_fast(m, rec, pin, b->view(s, B), l == 0);
 		}
 	}
 	if (p + 1 == b->channels) {
@@ -531,6 +577,41 @@ int ric_batch_create(ric_batch** out, int w, int h, int channels, int slots, int
 		return RIC_E_HIP;
 	}
 	memset(b->h_arena, 0, ns * b->hstride);
+	// compacted payloads (RIC_COMPACT=0: dense bands to the host)
+	static const bool cmp_env = [] { const char* e = getenv("RIC_COMPACT"); return !e || atoi(e) != 0; }();
+	b->compact = cmp_env;
+	if (b->compact) {
+		CmpArgs a{};
+		cmp_args(b->P, a);
+		b->cmp_nchunk = a.nchunk;
+		b->cmp_dense = cmp_dense_from(b->P);
+		b->cmp_stride = up(cmp_values(b->P) * 2, 256);
+		b->cmp_cstride = up((size_t)a.nchunk, 64);
+		b->cmp_ok.assign(ns, 0);
+		b->cmp_st.assign(ns, nullptr);
+		bool bad = b->cmp_stride > b->cmp_dense ||      // the values land in the mirror's band area
+		           bfail(hipMalloc(&b->d_cmp, ns * b->cmp_stride), "hipMalloc compact") ||
+		           bfail(hipMalloc(&b->d_cmp_cnt, ns * b->cmp_cstride * sizeof(uint32_t)), "hipMalloc compact") ||
+		           bfail(hipMalloc(&b->d_cmp_total, ns * sizeof(uint32_t)), "hipMalloc compact") ||
+		           bfail(hipHostMalloc(&b->h_cmp_total, ns * sizeof(uint32_t), 0), "hipHostMalloc compact") ||
+		           bfail(hipMalloc(&b->d_cmp_args, 2 * sizeof(CmpArgs)), "hipMalloc compact");
+		for (size_t i = 0; i < ns && !bad; i++)
+			bad = bfail(hipStreamCreateWithFlags(&b->cmp_st[i], hipStreamNonBlocking), "hipStreamCreate");
+		CmpArgs h[2];
+		for (int set = 0; set < 2 && !bad; set++) {
+			h[set] = a;
+			const size_t s0 = (size_t)set * slots;
+			h[set].arena = b->arena((int)s0); h[set].astride = b->astride;
+			h[set].out = b->d_cmp + s0 * b->cmp_stride; h[set].ostride = b->cmp_stride;
+			h[set].cnt = b->d_cmp_cnt + s0 * b->cmp_cstride; h[set].cstride = b->cmp_cstride;
+			h[set].total = b->d_cmp_total + s0;
+		}
+		if (!bad) bad = bfail(hipMemcpy(b->d_cmp_args, h, sizeof(h), hipMemcpyHostToDevice), "hipMemcpy compact");
+		if (bad) {
+			ric_batch_destroy(b);
+			return RIC_E_HIP;
+		}
+	}
 	b->enc = std::vector<Mux>(ns);
 	b->dec = std::vector<Mux>(ns);
 	b->pool = new Pool(threads);
@@ -549,6 +630,13 @@ void ric_batch_destroy(ric_batch* b)
 	b->prof.destroy();
 	if (b->d_arena) (void)hipFree(b->d_arena);
 	if (b->h_arena) (void)hipHostFree(b->h_arena);
+	if (b->d_cmp) (void)hipFree(b->d_cmp);
+	if (b->d_cmp_cnt) (void)hipFree(b->d_cmp_cnt);
+	if (b->d_cmp_total) (void)hipFree(b->d_cmp_total);
+	if (b->h_cmp_total) (void)hipHostFree(b->h_cmp_total);
+	if (b->d_cmp_args) (void)hipFree(b->d_cmp_args);
+	for (hipStream_t cs : b->cmp_st)
+		if (cs) (void)hipStreamDestroy(cs);
 	if (b->d_planes) (void)hipFree(b->d_planes);
 	if (b->d_stage) (void)hipFree(b->d_stage);
 	if (b->d_genc) (void)hipFree(b->d_genc);

@@ -1,0 +1,178 @@
+// compact.hip -- the host coder's payload of a frame, compacted on the GPU.
+//
+// The host encoder (encoder.cpp tree_rec_core) reads, per coded block, the
+// values at the set bits of its significance mask, in the walk order of
+// CBandCodec::tree<encode> (bandcodec.cpp:509-523: block rows serpentine,
+// coarse levels first, V, H, D).  A 16-bit band at C3 q9 is ~55 % zeros, so
+// instead of the dense bands (2 B per coefficient) the frame's short bands go
+// to the host as one stream of just those values, in the order the walk
+// consumes them: every block contributes popcount(mask) values (insignificant
+// blocks have an empty mask; a propagated block's values are skipped by the
+// walk, which still steps over them).  The int bands (the coarsest levels),
+// the LL, the block records and the parent info stay dense.
+//
+// Three passes per group of frames (blockIdx.z = frame): counts per chunk of
+// 64 blocks, one exclusive scan per frame, then the chunk's values written at
+// its offset (a wave-level prefix places each block).
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include "ric_types.h"
+#include "symbols.h"
+#include "compact.h"
+
+namespace ric {
+namespace {
+
+__device__ __forceinline__ int wave_excl(int v, int& total)
+{
+	// inclusive scan over the 64 lanes by shuffles, then exclusive
+	int x = v;
+	const int l = (int)__lane_id();
+#pragma unroll
+	for (int o = 1; o < 64; o <<= 1) {
+		const int y = __shfl_up(x, o, 64);
+		if (l >= o) x += y;
+	}
+	total = __shfl(x, 63, 64);
+	return x - v;
+}
+
+// the band and chunk of flattened chunk index c (bands in coding order)
+__device__ __forceinline__ int band_of(const CmpArgs& a, int c)
+{
+	int b = 0;
+	while (b + 1 < a.nb && c >= a.band[b + 1].chunk0) b++;
+	return b;
+}
+
+__device__ __forceinline__ uint32_t block_mask(const CmpArgs& a, const char* arena, int b, int s)
+{
+	const CmpBand& B = a.band[b];
+	if (s >= B.nblk) return 0;
+	int bx, by;
+	scan_block(s, B.dx, B.dy, bx, by);
+	const uint64_t r = ((const uint64_t*)(arena + B.rec_off))[(long)by * ((B.dx + 3) >> 2) + bx];
+	return BlockRec::mask(r);
+}
+
+__global__ __launch_bounds__(64) void k_cmp_count(const CmpArgs* __restrict__ ap)
+{
+	const CmpArgs& a = *ap;
+	const int c = blockIdx.x, f = blockIdx.z;
+	if (c >= a.nchunk) return;
+	const char* arena = a.arena + (size_t)f * a.astride;
+	const int b = band_of(a, c);
+	const int s = (c - a.band[b].chunk0) * 64 + (int)threadIdx.x;
+	int n = __popc(block_mask(a, arena, b, s));
+#pragma unroll
+	for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o, 64);
+	if (threadIdx.x == 0) a.cnt[(size_t)f * a.cstride + c] = (uint32_t)n;
+}
+
+// one workgroup per frame: exclusive scan of the chunk counts in place, the
+// frame's total to total[f]
+__global__ __launch_bounds__(1024) void k_cmp_scan(const CmpArgs* __restrict__ ap)
+{
+	const CmpArgs& a = *ap;
+	const int f = blockIdx.z;
+	uint32_t* cnt = a.cnt + (size_t)f * a.cstride;
+	__shared__ uint32_t part[16];
+	__shared__ uint32_t carry;
+	if (threadIdx.x == 0) carry = 0;
+	__syncthreads();
+	const int l = (int)threadIdx.x & 63, w = (int)threadIdx.x >> 6;
+	for (int base = 0; base < a.nchunk; base += 1024) {
+		const int i = base + (int)threadIdx.x;
+		const int v = i < a.nchunk ? (int)cnt[i] : 0;
+		int tot;
+		const int ex = wave_excl(v, tot);
+		if (l == 0) part[w] = (uint32_t)tot;
+		__syncthreads();
+		uint32_t before = carry;
+		for (int k = 0; k < w; k++) before += part[k];
+		if (i < a.nchunk) cnt[i] = before + (uint32_t)ex;
+		__syncthreads();
+		if (threadIdx.x == 0) {
+			uint32_t t = 0;
+			for (int k = 0; k < 16; k++) t += part[k];
+			carry += t;
+		}
+		__syncthreads();
+	}
+	if (threadIdx.x == 0) a.total[f] = carry;
+}
+
+__global__ __launch_bounds__(64) void k_cmp_write(const CmpArgs* __restrict__ ap)
+{
+	const CmpArgs& a = *ap;
+	const int c = blockIdx.x, f = blockIdx.z;
+	if (c >= a.nchunk) return;
+	const char* arena = a.arena + (size_t)f * a.astride;
+	int16_t* out = (int16_t*)(a.out + (size_t)f * a.ostride);
+	const int b = band_of(a, c);
+	const CmpBand& B = a.band[b];
+	const int s = (c - B.chunk0) * 64 + (int)threadIdx.x;
+	uint32_t m = block_mask(a, arena, b, s);
+	int tot;
+	const int ex = wave_excl(__popc(m), tot);
+	uint32_t o = a.cnt[(size_t)f * a.cstride + c] + (uint32_t)ex;
+	if (!m) return;
+	int bx, by;
+	scan_block(s, B.dx, B.dy, bx, by);
+	const int w = B.dx - bx * 4 < 4 ? B.dx - bx * 4 : 4;
+	const int16_t* band = (const int16_t*)(arena + B.off) + (long)by * 4 * B.pitch + bx * 4;
+	while (m) {                                      // the walk's order: ctz, raster over the w-wide block
+		const int i = __builtin_ctz(m);
+		m &= m - 1;
+		out[o++] = band[(long)(i / w) * B.pitch + i % w];
+	}
+}
+
+}  // namespace
+
+void cmp_args(const Pyramid& P, CmpArgs& a)
+{
+	a.nb = 0;
+	int chunk = 0;
+	const int order[3] = {BV, BH, BD};
+	for (int l = P.nlev - 1; l >= 0; l--)
+		for (int k = 0; k < 3; k++) {
+			const Band& B = P.L[l].b[order[k]];
+			if (B.is_int) continue;                      // int bands stay dense
+			CmpBand& d = a.band[a.nb++];
+			d.off = (uint32_t)B.off;
+			d.rec_off = (uint32_t)P.rec_off[l][order[k]];
+			d.dx = B.dx; d.dy = B.dy; d.pitch = B.pitch;
+			d.nblk = B.bw() * B.bh();
+			d.chunk0 = chunk;
+			chunk += (d.nblk + 63) / 64;
+		}
+	a.nchunk = chunk;
+}
+
+size_t cmp_values(const Pyramid& P)
+{
+	size_t n = 0;
+	for (int l = 0; l < P.nlev; l++)
+		for (int b = 0; b < 3; b++)
+			if (!P.L[l].b[b].is_int) n += (size_t)P.L[l].b[b].dx * P.L[l].b[b].dy;
+	return n;
+}
+
+size_t cmp_dense_from(const Pyramid& P)
+{
+	for (int l = 0; l < P.nlev; l++)
+		if (P.L[l].b[BD].is_int) return P.L[l].b[BD].off;
+	return P.L[P.nlev - 1].b[BL].off;
+}
+
+int launch_compact(const CmpArgs* dev_args, int nchunk, int nframes, hipStream_t st)
+{
+	if (nframes <= 0 || nchunk <= 0) return 0;
+	hipLaunchKernelGGL(k_cmp_count, dim3(nchunk, 1, nframes), dim3(64), 0, st, dev_args);
+	hipLaunchKernelGGL(k_cmp_scan, dim3(1, 1, nframes), dim3(1024), 0, st, dev_args);
+	hipLaunchKernelGGL(k_cmp_write, dim3(nchunk, 1, nframes), dim3(64), 0, st, dev_args);
+	return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace ric

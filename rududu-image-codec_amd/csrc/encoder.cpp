@@ -232,9 +232,13 @@ struct GeoRegE {
 	}
 };
 
-template <typename Core, typename C, bool HIGH, bool PAR>
-void tree_rec_core(Core& e, const uint64_t* rec, const uint8_t* pin, const BandView& b)
+// CMP: the values come from the frame's compacted stream (compact.hip) in
+// walk order -- *cp, advanced by every block's mask population, read or
+// skipped -- instead of from the dense band.
+template <typename Core, typename C, bool HIGH, bool PAR, bool CMP = false>
+void tree_rec_core(Core& e, const uint64_t* rec, const uint8_t* pin, const BandView& b, const int16_t** cpp = nullptr)
 {
+	const int16_t* cp = CMP ? *cpp : nullptr;
 	constexpr bool SH = sizeof(C) == 2;
 	static const uint8_t ginit[16] = {5,9,9,9,9,9,9,9,9,9,9,9,10,10,10,11};   // bandcodec.cpp:487
 	uint16_t kmean[16] = {2 << 10, 3 << 10, 4 << 10, 5 << 10, 8 << 10, 11 << 10, 13 << 10, 14 << 10,
@@ -256,25 +260,25 @@ void tree_rec_core(Core& e, const uint64_t* rec, const uint8_t* pin, const BandV
 			uint32_t mask = BlockRec::mask(r);
 			if (__builtin_expect(BlockRec::edge(r), 0)) {
 				bord.code(e, ins, 0);
-				if (ins) continue;
+				if (ins) { if (CMP) cp += __builtin_popcount(mask); continue; }
 				RIC_STAT(4, BlockRec::rawlen(r));
 				e.bits(BlockRec::raw(r), BlockRec::rawlen(r));
 				const int w = BlockRec::w(r), gc = BlockRec::gctx(r);
 				while (mask) {
 					const int i = __builtin_ctz(mask);
 					mask &= mask - 1;
-					const int v = blk[(i / w) * st + (i % w)];
+					const int v = CMP ? *cp++ : blk[(i / w) * st + (i % w)];
 					g.code_signed(e, (uc<SH>(v) >> 1) - 1, v & 1, gc);
 				}
 			} else {
 				int ctx = 15;
 				if (PAR) {
 					const uint32_t pi = pin[rb + bx];
-					if (BlockRec::pin_prop(pi)) continue;
+					if (BlockRec::pin_prop(pi)) { if (CMP) cp += __builtin_popcount(mask); continue; }
 					ctx = (int)BlockRec::pin_ctx(pi);
 				}
 				tree.code(e, ins, ctx);
-				if (ins) continue;
+				if (ins) { if (CMP) cp += __builtin_popcount(mask); continue; }
 				const uint32_t k = BlockRec::k(r);
 				const int idx = (kmean[ctx] + (1 << 9)) >> 10;
 				const uint16_t h = HIGH ? kHuff_HIGH[idx][k - 1] : kHuff_LOW[idx][k];
@@ -287,7 +291,7 @@ void tree_rec_core(Core& e, const uint64_t* rec, const uint8_t* pin, const BandV
 				while (mask) {
 					const int i = __builtin_ctz(mask);
 					mask &= mask - 1;
-					const int v = blk[(i >> 2) * st + (i & 3)];
+					const int v = CMP ? *cp++ : blk[(i >> 2) * st + (i & 3)];
 					gr.code_signed(e, (uc<SH>(v) >> 1) - 1, v & 1);
 				}
 				gr.store(g, gc);
@@ -296,6 +300,7 @@ void tree_rec_core(Core& e, const uint64_t* rec, const uint8_t* pin, const BandV
 			}
 		}
 	}
+	if (CMP) *cpp = cp;
 }
 
 template <typename C, bool HIGH>
@@ -322,6 +327,20 @@ void tree_encode_records_fast(Mux& m, const uint64_t* rec, const uint8_t* pin, c
 {
 	if (b.is_int) { if (high) tree_rec_disp<int32_t, true>(m, rec, pin, b); else tree_rec_disp<int32_t, false>(m, rec, pin, b); }
 	else { if (high) tree_rec_disp<int16_t, true>(m, rec, pin, b); else tree_rec_disp<int16_t, false>(m, rec, pin, b); }
+}
+
+void tree_encode_records_compact(Mux& m, const uint64_t* rec, const uint8_t* pin, const BandView& b, bool high,
+                                 const int16_t** cp)
+{
+	EncCore e(m.enc_state());
+	if (pin) {
+		if (high) tree_rec_core<EncCore, int16_t, true, true, true>(e, rec, pin, b, cp);
+		else tree_rec_core<EncCore, int16_t, false, true, true>(e, rec, pin, b, cp);
+	} else {
+		if (high) tree_rec_core<EncCore, int16_t, true, false, true>(e, rec, pin, b, cp);
+		else tree_rec_core<EncCore, int16_t, false, false, true>(e, rec, pin, b, cp);
+	}
+	m.set_enc_state(e.s);
 }
 
 size_t tree_model_records(EvBuf& ev, const uint64_t* rec, const uint8_t* pin, const BandView& b, bool high)

@@ -205,6 +205,11 @@ void mv_decode(Mux& m, uint32_t* mv, int dimx, int dimy);
 // (encoder.cpp): rec / pin in raster block order; pin == nullptr for a band
 // without a parent (the coarsest level).
 void tree_encode_records_fast(Mux& m, const uint64_t* rec, const uint8_t* pin, const BandView& b, bool high);
+// The same for a 16-bit band whose values come from the frame's compacted
+// stream (compact.hip) instead of b's samples (b gives the geometry): *cp is
+// advanced past the band's values.
+void tree_encode_records_compact(Mux& m, const uint64_t* rec, const uint8_t* pin, const BandView& b, bool high,
+                                 const int16_t** cp);
 // The same band split in two halves (encoder.cpp): the modelling alone,
 // recording the coder calls as events into ev (grown as needed; returns the
 // count) -- bands model independently, every model is per band

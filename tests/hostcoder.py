@@ -26,6 +26,8 @@ def lib():
         L.hc_encode_rec.argtypes = [_V, _L, _I, _I, _I, _I, _I, _V, _L, _V, _V]
         L.hc_encode_rec_split.restype = _L
         L.hc_encode_rec_split.argtypes = [_V, _L, _I, _I, _I, _I, _I, _V, _L, _I, _V, _V, _V]
+        L.hc_encode_rec_compact.restype = _L
+        L.hc_encode_rec_compact.argtypes = [_V, _L, _I, _I, _I, _I, _I, _V, _L]
         L.hc_decode.restype = _L
         L.hc_decode.argtypes = [_V, _L, _I, _I, _I, _I, _I, _V, _V]
         _lib = L
@@ -56,6 +58,17 @@ def encode_split(bands_flat, w, h, levels, lc, nthreads):
     s1, s2, s3 = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
     n = lib().hc_encode_rec_split(b.ctypes.data, b.size, 1, w, h, levels, lc, out.ctypes.data, cap, nthreads,
                                   ctypes.byref(s1), ctypes.byref(s2), ctypes.byref(s3))
+    assert n > 0
+    return out[:n].tobytes()
+
+
+def encode_compact(bands_flat, w, h, levels, lc):
+    """encode() through the compacted-payload walk (encoder.cpp
+    tree_encode_records_compact over the stream compact.hip writes)."""
+    b = np.ascontiguousarray(bands_flat, np.int32)
+    cap = w * h * 4 + 4096
+    out = np.zeros(cap, np.uint8)
+    n = lib().hc_encode_rec_compact(b.ctypes.data, b.size, 1, w, h, levels, lc, out.ctypes.data, cap)
     assert n > 0
     return out[:n].tobytes()
 

@@ -148,6 +148,43 @@ struct HostPyr {
 		*t_model += wait;
 		*t_replay += now() - t0 - wait;
 	}
+	// the compacted payload path: the 16-bit bands' values in walk order (the
+	// layout compact.hip writes), the int bands dense
+	void encode_rec_compact(Mux& m) {
+		std::vector<int16_t> stream;
+		for (int l = P.nlev - 1; l >= 0; l--) {
+			const int order[3] = {BV, BH, BD};
+			for (int k = 0; k < 3; k++) {
+				const Band& B = P.L[l].b[order[k]];
+				if (B.is_int) continue;
+				const std::vector<uint64_t>& R = recs[3 * l + order[k]];
+				const int16_t* bp = (const int16_t*)(arena.data() + B.off);
+				for (int sidx = 0; sidx < B.bw() * B.bh(); sidx++) {
+					int bx, by;
+					scan_block(sidx, B.dx, B.dy, bx, by);
+					uint32_t mk = BlockRec::mask(R[(size_t)by * B.bw() + bx]);
+					const int w = B.dx - bx * 4 < 4 ? B.dx - bx * 4 : 4;
+					while (mk) {
+						const int i = __builtin_ctz(mk);
+						mk &= mk - 1;
+						stream.push_back(bp[(size_t)(by * 4 + i / w) * B.pitch + bx * 4 + i % w]);
+					}
+				}
+			}
+		}
+		const int16_t* cp = stream.data();
+		pred_encode(m, view(P.coarsest_ll()));
+		for (int l = P.nlev - 1; l >= 0; l--) {
+			const int order[3] = {BV, BH, BD};
+			for (int k = 0; k < 3; k++) {
+				const Band& B = P.L[l].b[order[k]];
+				const uint64_t* rec = recs[3 * l + order[k]].data();
+				const uint8_t* pin = l + 1 < P.nlev ? pins[3 * l + order[k]].data() : nullptr;
+				if (B.is_int) tree_encode_records_fast(m, rec, pin, view(B), l == 0);
+				else tree_encode_records_compact(m, rec, pin, view(B), l == 0, &cp);
+			}
+		}
+	}
 	void decode(Mux& m) {
 		pred_decode(m, view(P.coarsest_ll()));
 		for (int l = P.nlev - 1; l >= 0; l--) {
@@ -206,6 +243,22 @@ long hc_encode_rec_split(const int32_t* bands, long per_plane, int nplanes, int 
 	}
 	uint8_t* e = m.end_coding();
 	if (secs) *secs = t;
+	return m.overflow() ? -1 : (long)(e - out);
+}
+
+// hc_encode_rec through the compacted-payload encoder
+long hc_encode_rec_compact(const int32_t* bands, long per_plane, int nplanes, int w, int h, int levels, int lc,
+                           uint8_t* out, long cap)
+{
+	HostPyr hp(w, h, levels, lc);
+	Mux m;
+	m.init_encoder(out, cap, 0);
+	for (int p = 0; p < nplanes; p++) {
+		hp.load(bands + p * per_plane);
+		hp.build_records();
+		hp.encode_rec_compact(m);
+	}
+	uint8_t* e = m.end_coding();
 	return m.overflow() ? -1 : (long)(e - out);
 }
 

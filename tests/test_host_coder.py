@@ -48,6 +48,18 @@ def test_split_encoder_matches_oracle(w, h, q, t, L, lc, nthreads):
     assert HC.encode_split(flat, w, h, L, lc, nthreads) == P.encode_planes(pl[None], L, lc, t, [Q], [lam])
 
 
+@pytest.mark.parametrize("w,h,q,t,L,lc", CASES)
+def test_compact_encoder_matches_oracle(w, h, q, t, L, lc):
+    """the host walk over the compacted payload (values in walk order, int
+    bands dense) writes the reference's bytes"""
+    P = O.port()
+    pl = _plane(w, h, q)
+    Q = O.quants(q + 20) if q else 0
+    lam = O.quants(q + 13) if q else 0
+    flat = np.concatenate([x.ravel() for x in P.bands(pl, L, lc, t, 1, Q, lam)]).astype(np.int32)
+    assert HC.encode_compact(flat, w, h, L, lc) == P.encode_planes(pl[None], L, lc, t, [Q], [lam])
+
+
 def test_split_encoder_long_raw_fields():
     """lossless int bands: raw fields past 24 bits and events split at 32 bits"""
     P = O.port()
