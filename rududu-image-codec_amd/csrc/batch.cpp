@@ -176,6 +176,12 @@ struct ric_batch {
 	size_t cmp_dense = 0;                          // arena offset where the dense part starts
 	std::vector<char> cmp_ok;
 	std::vector<hipStream_t> cmp_st;               // per slot: the task's own copy stream
+	// the decode side: the host decoder's finest level compacted
+	// (tree_decode_compact), scattered on the device (k_dcmp_expand)
+	bool dcompact = false;
+	DcmpLayout dl;
+	std::vector<size_t> dcmp_bytes;
+	std::vector<char> dcmp_ok;
 	// ric_batch_set_digests: per frame of a call, the digest of its decoded pixels
 	unsigned long long* digest = nullptr;
 	long ndigest = 0;
@@ -341,8 +347,38 @@ int gpu_decode_plane(ric_batch* b, int set, int n, int p, const int* qs, int tra
 	if (h2d && (abase != s0 || amul != 1)) return RIC_E_ARG;
 	const size_t ast = (size_t)amul * b->astride;
 	if (h2d) {
+		bool cmp = b->dcompact;
+		for (int i = 0; i < n && cmp; i++) cmp = b->dcmp_ok[s0 + i] != 0;
 		auto sp = b->prof.begin(B_H2D, n, b->st);
-		BCHK(hipMemcpy2DAsync(b->arena(s0), b->astride, b->harena(s0), b->hstride, P.a_end, n, hipMemcpyHostToDevice, b->st));
+		if (cmp) {
+			// levels 1.. and the LL dense; each frame's compacted finest level,
+			// scattered into its three bands on the device
+			const size_t d0 = P.L[1].b[BD].off;
+			BCHK(hipMemcpy2DAsync(b->arena(s0) + d0, b->astride, b->harena(s0) + d0, b->hstride, P.a_end - d0, n,
+			                      hipMemcpyHostToDevice, b->st));
+			for (int i = 0; i < n; i++) {
+				BCHK(hipMemcpyAsync(b->d_cmp + (size_t)(s0 + i) * b->cmp_stride, b->harena(s0 + i), b->dcmp_bytes[s0 + i],
+				                    hipMemcpyHostToDevice, b->st));
+				b->dcmp_ok[s0 + i] = 0;
+			}
+			DcmpArgs a;
+			a.arena = b->arena(s0); a.astride = b->astride;
+			a.in = b->d_cmp + (size_t)s0 * b->cmp_stride; a.istride = b->cmp_stride;
+			int ch = 0;
+			for (int k = 0; k < 3; k++) {
+				const Band& B = P.L[0].b[b->dl.band[k]];
+				a.off[k] = (uint32_t)B.off; a.dx[k] = B.dx; a.dy[k] = B.dy; a.pitch[k] = B.pitch;
+				a.mask_off[k] = (uint32_t)b->dl.mask_off[k]; a.coff_off[k] = (uint32_t)b->dl.coff_off[k];
+				a.nblk[k] = b->dl.nblk[k];
+				a.chunk0[k] = ch;
+				ch += b->dl.nch[k];
+			}
+			a.chunk0[3] = ch;
+			a.vals_off = (uint32_t)b->dl.vals_off;
+			if (launch_dcmp_expand(a, n, b->st)) return bfail(hipGetLastError(), "k_dcmp_expand") ? RIC_E_HIP : RIC_E_HIP;
+		} else {
+			BCHK(hipMemcpy2DAsync(b->arena(s0), b->astride, b->harena(s0), b->hstride, P.a_end, n, hipMemcpyHostToDevice, b->st));
+		}
 		b->prof.end(sp);
 	}
 	P.set_weight(trans);
@@ -469,15 +505,29 @@ int host_decode_plane(ric_batch* b, int s, int p, const uint8_t* ric, size_t len
 		m.init_decoder_payload(ric + 9, pay);
 	}
 	const double t0 = now_ms();
+	// the finest level compacted into the mirror's level-0 area (DcmpLayout)
+	const bool cmp = b->dcompact;
+	char* blk = b->harena(s);
+	uint32_t* nval = (uint32_t*)blk;
 	pred_decode(m, b->view(s, P.coarsest_ll()));
 	for (int l = P.nlev - 1; l >= 0; l--) {
 		const int order[3] = {BV, BH, BD};
+		uint32_t vsum = 0;
 		for (int k = 0; k < 3; k++) {
 			BandView par;
 			if (l + 1 < P.nlev) par = b->view(s, P.L[l + 1].b[order[k]]);
-			tree_decode_fast(m, b->view(s, P.L[l].b[order[k]]), par, l == 0, l > 0);
+			if (cmp && l == 0) {
+				const DcmpLayout& L = b->dl;
+				nval[k] = tree_decode_compact(m, b->view(s, P.L[l].b[order[k]]), par, (uint16_t*)(blk + L.mask_off[k]),
+				                              (uint32_t*)(blk + L.coff_off[k]), (int16_t*)(blk + L.vals_off) + vsum);
+				vsum += nval[k];
+				b->dcmp_bytes[s] = L.vals_off + (size_t)vsum * 2;
+			} else {
+				tree_decode_fast(m, b->view(s, P.L[l].b[order[k]]), par, l == 0, l > 0);
+			}
 		}
 	}
+	if (cmp) b->dcmp_ok[s] = 1;
 	b->prof.host(B_HDEC, now_ms() - t0);
 	return m.overflow() ? RIC_E_STREAM : RIC_OK;
 }
@@ -611,6 +661,14 @@ int ric_batch_create(ric_batch** out, int w, int h, int channels, int slots, int
 			ric_batch_destroy(b);
 			return RIC_E_HIP;
 		}
+		// decode side: the block must fit the mirror's level-0 area and a device slot
+		b->dl = dcmp_layout(b->P);
+		size_t l0 = 0;
+		for (int k = 0; k < 3; k++) l0 += (size_t)b->P.L[0].b[k].dx * b->P.L[0].b[k].dy;
+		const size_t most = b->dl.vals_off + l0 * 2;
+		b->dcompact = b->dl.ok && most <= b->P.L[1].b[BD].off && most <= b->cmp_stride;
+		b->dcmp_bytes.assign(ns, 0);
+		b->dcmp_ok.assign(ns, 0);
 	}
 	b->enc = std::vector<Mux>(ns);
 	b->dec = std::vector<Mux>(ns);

@@ -41,4 +41,30 @@ size_t cmp_dense_from(const Pyramid& P);
 // the three passes over nframes frames
 int launch_compact(const CmpArgs* dev_args, int nchunk, int nframes, hipStream_t st);
 
+// ---- the decode side: the host decoder's finest level (three 16-bit bands
+// without children) comes back compacted (decoder.cpp tree_decode_compact)
+// and is scattered into the dense bands on the device.  One block per frame:
+//   u32 nval[3]           values of each band (coding order V, H, D)
+//   u16 mask[nblk_b]      per band, per block in walk order
+//   u32 chunk_off[nch_b]  per band, the value count before each 64 blocks
+//   i16 vals[]            per band, in walk order, bands back to back
+struct DcmpLayout {
+	int band[3];                      // BV, BH, BD of level 0
+	size_t mask_off[3], coff_off[3], vals_off;
+	int nblk[3], nch[3];
+	bool ok = false;                  // level 0 is 16-bit and has no int bands
+};
+DcmpLayout dcmp_layout(const Pyramid& P);
+struct DcmpArgs {
+	char* arena;                      // frame f: arena + f * astride
+	size_t astride;
+	const char* in;                   // frame f's block: in + f * istride
+	size_t istride;
+	uint32_t off[3];                  // band offsets in the arena
+	int dx[3], dy[3], pitch[3];
+	uint32_t mask_off[3], coff_off[3], vals_off;
+	int nblk[3], chunk0[4];           // chunk0[3] = total chunks
+};
+int launch_dcmp_expand(const DcmpArgs& a, int nframes, hipStream_t st);
+
 }  // namespace ric

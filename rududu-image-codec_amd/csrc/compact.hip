@@ -128,7 +128,66 @@ __global__ __launch_bounds__(64) void k_cmp_write(const CmpArgs* __restrict__ ap
 	}
 }
 
+// the decode side: one wave per chunk of 64 blocks (flattened over the three
+// bands): every position of each block written, a value where its mask bit is set
+__global__ __launch_bounds__(64) void k_dcmp_expand(DcmpArgs a)
+{
+	const int c = blockIdx.x, f = blockIdx.z;
+	if (c >= a.chunk0[3]) return;
+	const int b = c >= a.chunk0[2] ? 2 : c >= a.chunk0[1] ? 1 : 0;
+	const char* in = a.in + (size_t)f * a.istride;
+	const uint32_t* nval = (const uint32_t*)in;
+	uint32_t vbase = 0;
+	for (int k = 0; k < b; k++) vbase += nval[k];
+	const int ch = c - a.chunk0[b];
+	const int s = ch * 64 + (int)threadIdx.x;
+	const uint32_t m = s < a.nblk[b] ? ((const uint16_t*)(in + a.mask_off[b]))[s] : 0u;
+	int tot;
+	const int ex = wave_excl(__popc(m), tot);
+	if (s >= a.nblk[b]) return;
+	uint32_t o = vbase + ((const uint32_t*)(in + a.coff_off[b]))[ch] + (uint32_t)ex;
+	const int16_t* vals = (const int16_t*)(in + a.vals_off);
+	int bx, by;
+	scan_block(s, a.dx[b], a.dy[b], bx, by);
+	const int w = a.dx[b] - bx * 4 < 4 ? a.dx[b] - bx * 4 : 4, h = a.dy[b] - by * 4 < 4 ? a.dy[b] - by * 4 : 4;
+	int16_t* band = (int16_t*)(a.arena + (size_t)f * a.astride + a.off[b]) + (long)by * 4 * a.pitch[b] + bx * 4;
+	for (int r = 0; r < h; r++)
+		for (int q = 0; q < w; q++) {
+			const int i = r * w + q;
+			band[(long)r * a.pitch[b] + q] = (m >> i) & 1 ? vals[o++] : (int16_t)0;
+		}
+}
+
 }  // namespace
+
+DcmpLayout dcmp_layout(const Pyramid& P)
+{
+	DcmpLayout L;
+	const int order[3] = {BV, BH, BD};
+	size_t off = 16;
+	for (int k = 0; k < 3; k++) {
+		const Band& B = P.L[0].b[order[k]];
+		L.band[k] = order[k];
+		L.nblk[k] = B.bw() * B.bh();
+		L.nch[k] = (L.nblk[k] + 63) / 64;
+		L.mask_off[k] = off;
+		off += ((size_t)L.nblk[k] * 2 + 15) / 16 * 16;
+	}
+	for (int k = 0; k < 3; k++) {
+		L.coff_off[k] = off;
+		off += ((size_t)L.nch[k] * 4 + 15) / 16 * 16;
+	}
+	L.vals_off = off;
+	L.ok = P.nlev >= 2 && !P.L[0].b[BD].is_int;
+	return L;
+}
+
+int launch_dcmp_expand(const DcmpArgs& a, int nframes, hipStream_t st)
+{
+	if (nframes <= 0 || a.chunk0[3] <= 0) return 0;
+	hipLaunchKernelGGL(k_dcmp_expand, dim3(a.chunk0[3], 1, nframes), dim3(64), 0, st, a);
+	return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 
 void cmp_args(const Pyramid& P, CmpArgs& a)
 {

@@ -315,12 +315,29 @@ RIC_AI int max_len2_dec(const P* p, long st)                    // maxLen<2, dec
 	return bitlen((uint32_t)(mn > mx ? mn : mx));
 }
 
-template <typename C, bool HIGH>
-RIC_AI int block_full_dec(DecCore& d, GeoM& g, C* blk, long st, int idx)
+// The compacted output of a finest-level band (no children, so no marks):
+// per block in walk order its mask of decoded positions (raster over its w
+// columns), every 64 blocks the value count so far, and the values in walk
+// order -- the layout k_cmp_expand (compact.hip) scatters back on the device.
+struct CmpSink {
+	uint16_t* mask;
+	uint32_t* chunk_off;
+	int16_t* vals;
+	uint32_t nblk = 0, nval = 0;
+	RIC_AI void block(uint32_t m)                              // after the block's values
+	{
+		if (!(nblk & 63)) chunk_off[nblk >> 6] = nval - (uint32_t)__builtin_popcount(m);
+		mask[nblk++] = (uint16_t)m;
+	}
+};
+
+template <typename C, bool HIGH, bool CMP = false>
+RIC_AI int block_full_dec(DecCore& d, GeoM& g, C* blk, long st, int idx, CmpSink* cs = nullptr)
 {
 	constexpr bool SH = sizeof(C) == 2;
 	const int t = HIGH ? 17 + idx : idx;
 	const uint32_t k = HIGH ? d.huff(t, kHuff_HIGH[idx], 16) + 1 : d.huff(t, kHuff_LOW[idx], 17);
+	uint32_t m = 0;
 	if (HIGH || k != 0) {
 		uint32_t sig = k != 16 ? d.enum16(k) : 0xFFFFu;
 		const int gc = (int)k - 1;
@@ -330,34 +347,43 @@ RIC_AI int block_full_dec(DecCore& d, GeoM& g, C* blk, long st, int idx)
 			const int b = 31 - __builtin_clz(sig);      // bit 15 = raster position 0
 			sig &= ~(1u << b);
 			const int i = 15 - b;
-			blk[(i >> 2) * st + (i & 3)] = (C)tr<SH>(r.template decode_signed<kUnaryMax<C>>(d));
+			const C v = (C)tr<SH>(r.template decode_signed<kUnaryMax<C>>(d));
+			if (CMP) { cs->vals[cs->nval++] = (int16_t)v; m |= 1u << i; }
+			else blk[(i >> 2) * st + (i & 3)] = v;
 		}
 		r.store(g, gc);
 	}
+	if (CMP) cs->block(m);
 	return (int)k - (HIGH ? 1 : 0);
 }
 
-template <typename C, bool HIGH>
-void block_edge_dec(DecCore& d, GeoM& g, C* blk, long st, int w, int h)
+template <typename C, bool HIGH, bool CMP = false>
+void block_edge_dec(DecCore& d, GeoM& g, C* blk, long st, int w, int h, CmpSink* cs = nullptr)
 {
 	constexpr bool SH = sizeof(C) == 2;
 	const uint32_t cnt = (uint32_t)(w * h);
 	uint32_t k = HIGH ? d.max_dec(cnt - 1) + 1 : d.max_dec(cnt);
 	if (k > cnt) k = cnt;                                       // corrupt-stream guard
+	uint32_t m = 0;
 	if (HIGH || k != 0) {
 		uint32_t sig = k != cnt ? d.enum_n(k, cnt) : (1u << cnt) - 1;
 		const int gc = kKConv2[kKConv1[cnt]][k - 1];
 		for (int j = 0; j < h; j++)
 			for (int i = 0; i < w; i++) {
-				if (sig & (1u << (cnt - 1))) blk[j * st + i] = (C)tr<SH>(g.template decode_signed<kUnaryMax<C>>(d, gc));
+				if (sig & (1u << (cnt - 1))) {
+					const C v = (C)tr<SH>(g.template decode_signed<kUnaryMax<C>>(d, gc));
+					if (CMP) { cs->vals[cs->nval++] = (int16_t)v; m |= 1u << (j * w + i); }
+					else blk[j * st + i] = v;
+				}
 				sig <<= 1;
 			}
 	}
+	if (CMP) cs->block(m);
 }
 
 // CBandCodec::tree<decode>, src/lib/bandcodec.cpp:484-589
-template <typename C, typename P, bool HIGH>
-void tree_dec(Mux& m, const BandView& b, const BandView& par, bool has_child)
+template <typename C, typename P, bool HIGH, bool CMP = false>
+void tree_dec(Mux& m, const BandView& b, const BandView& par, bool has_child, CmpSink* cs = nullptr)
 {
 	constexpr bool SH = sizeof(C) == 2;
 	static const uint8_t ginit[16] = {5,9,9,9,9,9,9,9,9,9,9,9,10,10,10,11};
@@ -373,11 +399,13 @@ void tree_dec(Mux& m, const BandView& b, const BandView& par, bool has_child)
 	const int pdx = par.dx, pdy = par.dy;
 	const C mark = (C)tr<SH>(has_child ? kInsignif : 0);
 	C* band = (C*)b.p;
-	for (int j = 0; j < dy; j++) memset(band + j * st, 0, sizeof(C) * dx);   // Clear(), :503
+	if (!CMP)
+		for (int j = 0; j < dy; j++) memset(band + j * st, 0, sizeof(C) * dx);   // Clear(), :503
 
 	auto edge = [&](C* c1, int i, int w, int h, P* pp, bool chk_row, int j) {
 		if (pp && (i >> 1) < pdx && (!chk_row || (j >> 1) < pdy) && pp[i >> 1] == kInsignif) pp[i >> 1] = 0;
-		if (!bord.decode(d, 0)) block_edge_dec<C, HIGH>(d, g, c1 + i, st, w, h);
+		if (!bord.decode(d, 0)) block_edge_dec<C, HIGH, CMP>(d, g, c1 + i, st, w, h, cs);
+		else if (CMP) cs->block(0);
 	};
 
 	int j = 0;
@@ -398,16 +426,18 @@ void tree_dec(Mux& m, const BandView& b, const BandView& par, bool has_child)
 			if (pp) {
 				if (pp[k] == kInsignif) {
 					pp[k] = 0;
-					c1[i] = c1[i + 2] = c2[i] = c2[i + 2] = mark;
+					if (CMP) cs->block(0);                   // the finest level: mark == 0
+					else c1[i] = c1[i + 2] = c2[i] = c2[i + 2] = mark;
 					continue;
 				}
 				ctx = max_len2_dec<P>(pp + k, pst);
 			}
 			if (tree.decode(d, ctx)) {
-				c1[i] = c1[i + 2] = c2[i] = c2[i + 2] = mark;
+				if (CMP) cs->block(0);
+				else c1[i] = c1[i + 2] = c2[i] = c2[i + 2] = mark;
 			} else {
 				const int idx = (kmean[ctx] + (1 << 9)) >> 10;
-				const int kk = block_full_dec<C, HIGH>(d, g, c1 + i, st, idx);
+				const int kk = block_full_dec<C, HIGH, CMP>(d, g, c1 + i, st, idx, cs);
 				kmean[ctx] = (uint16_t)(kmean[ctx] + ((uint32_t)kk << 7) - (kmean[ctx] >> 3));
 			}
 		}
@@ -426,7 +456,8 @@ void tree_dec(Mux& m, const BandView& b, const BandView& par, bool has_child)
 		}
 		for (; i >= 0 && i + 4 <= dx; i += bs) {
 			if (pp && (j >> 1) < pdy && pp[i >> 1] == kInsignif) pp[i >> 1] = 0;
-			if (!bord.decode(d, 0)) block_edge_dec<C, HIGH>(d, g, c1 + i, st, 4, h);
+			if (!bord.decode(d, 0)) block_edge_dec<C, HIGH, CMP>(d, g, c1 + i, st, 4, h, cs);
+			else if (CMP) cs->block(0);
 		}
 		if (i > 0 && i < dx) edge(c1, i, dx - i, h, pp, true, j);
 	}
@@ -434,6 +465,16 @@ void tree_dec(Mux& m, const BandView& b, const BandView& par, bool has_child)
 }
 
 }  // namespace
+
+uint32_t tree_decode_compact(Mux& m, const BandView& b, const BandView& par, uint16_t* mask, uint32_t* chunk_off,
+                             int16_t* vals)
+{
+	CmpSink cs;
+	cs.mask = mask; cs.chunk_off = chunk_off; cs.vals = vals;
+	if (par.p && par.is_int) tree_dec<int16_t, int32_t, true, true>(m, b, par, false, &cs);
+	else tree_dec<int16_t, int16_t, true, true>(m, b, par, false, &cs);
+	return cs.nval;
+}
 
 void tree_decode_fast(Mux& m, const BandView& b, const BandView& par, bool high, bool has_child)
 {

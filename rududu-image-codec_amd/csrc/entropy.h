@@ -208,6 +208,13 @@ void tree_encode_records_fast(Mux& m, const uint64_t* rec, const uint8_t* pin, c
 // The same for a 16-bit band whose values come from the frame's compacted
 // stream (compact.hip) instead of b's samples (b gives the geometry): *cp is
 // advanced past the band's values.
+// tree_decode_fast of a finest-level 16-bit band (no children) into the
+// compacted layout k_cmp_expand reads: per block in walk order its mask of
+// decoded positions (mask[], one per block), every 64 blocks the value count
+// so far (chunk_off[]), the values in walk order (vals[]); returns the value
+// count.  b gives the geometry (its samples are not written).
+uint32_t tree_decode_compact(Mux& m, const BandView& b, const BandView& par, uint16_t* mask, uint32_t* chunk_off,
+                             int16_t* vals);
 void tree_encode_records_compact(Mux& m, const uint64_t* rec, const uint8_t* pin, const BandView& b, bool high,
                                  const int16_t** cp);
 // The same band split in two halves (encoder.cpp): the modelling alone,

@@ -28,6 +28,8 @@ def lib():
         L.hc_encode_rec_split.argtypes = [_V, _L, _I, _I, _I, _I, _I, _V, _L, _I, _V, _V, _V]
         L.hc_encode_rec_compact.restype = _L
         L.hc_encode_rec_compact.argtypes = [_V, _L, _I, _I, _I, _I, _I, _V, _L]
+        L.hc_decode_compact.restype = _L
+        L.hc_decode_compact.argtypes = [_V, _L, _I, _I, _I, _I, _I, _V, _V]
         L.hc_decode.restype = _L
         L.hc_decode.argtypes = [_V, _L, _I, _I, _I, _I, _I, _V, _V]
         _lib = L
@@ -79,4 +81,14 @@ def decode(buf, w, h, levels, lc, total):
     out = np.zeros(total, np.int32)
     s = ctypes.c_double()
     lib().hc_decode(b.ctypes.data, len(buf), 1, w, h, levels, lc, out.ctypes.data, ctypes.byref(s))
+    return out
+
+
+def decode_compact(buf, w, h, levels, lc, total):
+    """decode() with the finest level through tree_decode_compact, scattered
+    back as k_dcmp_expand does."""
+    b = np.frombuffer(buf, np.uint8).copy()
+    out = np.zeros(total, np.int32)
+    s = ctypes.c_double()
+    lib().hc_decode_compact(b.ctypes.data, len(buf), 1, w, h, levels, lc, out.ctypes.data, ctypes.byref(s))
     return out

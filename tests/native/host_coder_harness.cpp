@@ -185,6 +185,36 @@ struct HostPyr {
 			}
 		}
 	}
+	// the finest level through tree_decode_compact, scattered back on the CPU
+	// the way k_dcmp_expand does (every position of each block)
+	void decode_compact(Mux& m) {
+		pred_decode(m, view(P.coarsest_ll()));
+		for (int l = P.nlev - 1; l >= 0; l--) {
+			const int order[3] = {BV, BH, BD};
+			for (int k = 0; k < 3; k++) {
+				const Band& B = P.L[l].b[order[k]];
+				BandView par;
+				if (l + 1 < P.nlev) par = view(P.L[l + 1].b[order[k]]);
+				if (l > 0 || B.is_int) { tree_decode_fast(m, view(B), par, l == 0, l > 0); continue; }
+				const int nblk = B.bw() * B.bh();
+				std::vector<uint16_t> mask(nblk);
+				std::vector<uint32_t> coff((nblk + 63) / 64);
+				std::vector<int16_t> vals((size_t)B.dx * B.dy);
+				tree_decode_compact(m, view(B), par, mask.data(), coff.data(), vals.data());
+				int16_t* band = (int16_t*)(arena.data() + B.off);
+				size_t o = 0;
+				for (int sidx = 0; sidx < nblk; sidx++) {
+					if ((sidx & 63) == 0) o = coff[sidx >> 6];          // as the device: the chunk's recorded offset
+					int bx, by;
+					scan_block(sidx, B.dx, B.dy, bx, by);
+					const int w = B.dx - bx * 4 < 4 ? B.dx - bx * 4 : 4, h = B.dy - by * 4 < 4 ? B.dy - by * 4 : 4;
+					for (int r = 0; r < h; r++)
+						for (int q = 0; q < w; q++)
+							band[(size_t)(by * 4 + r) * B.pitch + bx * 4 + q] = (mask[sidx] >> (r * w + q)) & 1 ? vals[o++] : 0;
+				}
+			}
+		}
+	}
 	void decode(Mux& m) {
 		pred_decode(m, view(P.coarsest_ll()));
 		for (int l = P.nlev - 1; l >= 0; l--) {
@@ -297,6 +327,28 @@ long hc_decode(const uint8_t* in, long len, int nplanes, int w, int h, int level
 		std::memset(hp.arena.data(), 0xA5, hp.arena.size());
 		double t0 = now();
 		hp.decode(m);
+		t += now() - t0;
+		off += hp.dump(bands_out + off);
+	}
+	if (secs) *secs = t;
+	return off;
+}
+
+// hc_decode with the finest level through the compacted output
+long hc_decode_compact(const uint8_t* in, long len, int nplanes, int w, int h, int levels, int lc,
+               int32_t* bands_out, double* secs)
+{
+	HostPyr hp(w, h, levels, lc);
+	Mux m;
+	m.init_decoder(in, len);
+	double t = 0;
+	long off = 0;
+	for (int p = 0; p < nplanes; p++) {
+		// stale data in the bands (the product reuses its pinned arena across
+		// frames): the decoder must clear every coefficient itself
+		std::memset(hp.arena.data(), 0xA5, hp.arena.size());
+		double t0 = now();
+		hp.decode_compact(m);
 		t += now() - t0;
 		off += hp.dump(bands_out + off);
 	}

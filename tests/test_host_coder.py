@@ -84,6 +84,20 @@ def test_decode_matches_oracle(w, h, q, t, L, lc):
     assert np.array_equal(HC.decode(buf, w, h, L, lc, exp.size), exp)
 
 
+@pytest.mark.parametrize("w,h,q,t,L,lc", CASES)
+def test_compact_decoder_matches_oracle(w, h, q, t, L, lc):
+    """the finest level decoded into the compacted layout and scattered back
+    equals the dense decode (and the oracle's bands)"""
+    P = O.port()
+    pl = _plane(w, h, q)
+    Q = O.quants(q + 20) if q else 0
+    lam = O.quants(q + 13) if q else 0
+    buf = P.encode_planes(pl[None], L, lc, t, [Q], [lam])
+    _, exp = P.decode_planes(buf, 1, w, h, L, lc, t, [Q], want_bands=True)
+    exp = np.concatenate([x.ravel() for x in exp])
+    assert np.array_equal(HC.decode_compact(buf, w, h, L, lc, exp.size), exp)
+
+
 def test_c2_full_size_stream():
     e = [x for x in G["large"] if x["name"] == "C2_4096x4096_q9"][0]
     import hashlib
