@@ -16,6 +16,7 @@
 // its offset (a wave-level prefix places each block).
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <algorithm>
 #include "ric_types.h"
 #include "symbols.h"
 #include "compact.h"
@@ -55,18 +56,27 @@ __device__ __forceinline__ uint32_t block_mask(const CmpArgs& a, const char* are
 	return BlockRec::mask(r);
 }
 
-__global__ __launch_bounds__(64) void k_cmp_count(const CmpArgs* __restrict__ ap)
+// A few workgroups of 4 waves per frame, each wave striding over the chunks:
+// a workgroup per chunk would be hundreds of thousands of tiny dispatches,
+// which crawl when the stream coder's waves fill the CUs.
+constexpr int kCmpWaves = 4;
+__device__ __forceinline__ int wave_gid() { return (int)(blockIdx.x * kCmpWaves + (threadIdx.x >> 6)); }
+__device__ __forceinline__ int wave_count() { return (int)(gridDim.x * kCmpWaves); }
+__device__ __forceinline__ int lane64() { return (int)(threadIdx.x & 63); }
+
+__global__ __launch_bounds__(64 * kCmpWaves) void k_cmp_count(const CmpArgs* __restrict__ ap)
 {
 	const CmpArgs& a = *ap;
-	const int c = blockIdx.x, f = blockIdx.z;
-	if (c >= a.nchunk) return;
+	const int f = blockIdx.z;
 	const char* arena = a.arena + (size_t)f * a.astride;
-	const int b = band_of(a, c);
-	const int s = (c - a.band[b].chunk0) * 64 + (int)threadIdx.x;
-	int n = __popc(block_mask(a, arena, b, s));
+	for (int c = wave_gid(); c < a.nchunk; c += wave_count()) {
+		const int b = band_of(a, c);
+		const int s = (c - a.band[b].chunk0) * 64 + lane64();
+		int n = __popc(block_mask(a, arena, b, s));
 #pragma unroll
-	for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o, 64);
-	if (threadIdx.x == 0) a.cnt[(size_t)f * a.cstride + c] = (uint32_t)n;
+		for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o, 64);
+		if (lane64() == 0) a.cnt[(size_t)f * a.cstride + c] = (uint32_t)n;
+	}
 }
 
 // one workgroup per frame: exclusive scan of the chunk counts in place, the
@@ -102,60 +112,62 @@ __global__ __launch_bounds__(1024) void k_cmp_scan(const CmpArgs* __restrict__ a
 	if (threadIdx.x == 0) a.total[f] = carry;
 }
 
-__global__ __launch_bounds__(64) void k_cmp_write(const CmpArgs* __restrict__ ap)
+__global__ __launch_bounds__(64 * kCmpWaves) void k_cmp_write(const CmpArgs* __restrict__ ap)
 {
 	const CmpArgs& a = *ap;
-	const int c = blockIdx.x, f = blockIdx.z;
-	if (c >= a.nchunk) return;
+	const int f = blockIdx.z;
 	const char* arena = a.arena + (size_t)f * a.astride;
 	int16_t* out = (int16_t*)(a.out + (size_t)f * a.ostride);
-	const int b = band_of(a, c);
-	const CmpBand& B = a.band[b];
-	const int s = (c - B.chunk0) * 64 + (int)threadIdx.x;
-	uint32_t m = block_mask(a, arena, b, s);
-	int tot;
-	const int ex = wave_excl(__popc(m), tot);
-	uint32_t o = a.cnt[(size_t)f * a.cstride + c] + (uint32_t)ex;
-	if (!m) return;
-	int bx, by;
-	scan_block(s, B.dx, B.dy, bx, by);
-	const int w = B.dx - bx * 4 < 4 ? B.dx - bx * 4 : 4;
-	const int16_t* band = (const int16_t*)(arena + B.off) + (long)by * 4 * B.pitch + bx * 4;
-	while (m) {                                      // the walk's order: ctz, raster over the w-wide block
-		const int i = __builtin_ctz(m);
-		m &= m - 1;
-		out[o++] = band[(long)(i / w) * B.pitch + i % w];
+	for (int c = wave_gid(); c < a.nchunk; c += wave_count()) {
+		const int b = band_of(a, c);
+		const CmpBand& B = a.band[b];
+		const int s = (c - B.chunk0) * 64 + lane64();
+		uint32_t m = block_mask(a, arena, b, s);
+		int tot;
+		const int ex = wave_excl(__popc(m), tot);
+		uint32_t o = a.cnt[(size_t)f * a.cstride + c] + (uint32_t)ex;
+		if (!m) continue;
+		int bx, by;
+		scan_block(s, B.dx, B.dy, bx, by);
+		const int w = B.dx - bx * 4 < 4 ? B.dx - bx * 4 : 4;
+		const int16_t* band = (const int16_t*)(arena + B.off) + (long)by * 4 * B.pitch + bx * 4;
+		while (m) {                                  // the walk's order: ctz, raster over the w-wide block
+			const int i = __builtin_ctz(m);
+			m &= m - 1;
+			out[o++] = band[(long)(i / w) * B.pitch + i % w];
+		}
 	}
 }
 
 // the decode side: one wave per chunk of 64 blocks (flattened over the three
 // bands): every position of each block written, a value where its mask bit is set
-__global__ __launch_bounds__(64) void k_dcmp_expand(DcmpArgs a)
+__global__ __launch_bounds__(64 * kCmpWaves) void k_dcmp_expand(DcmpArgs a)
 {
-	const int c = blockIdx.x, f = blockIdx.z;
-	if (c >= a.chunk0[3]) return;
-	const int b = c >= a.chunk0[2] ? 2 : c >= a.chunk0[1] ? 1 : 0;
+	const int f = blockIdx.z;
 	const char* in = a.in + (size_t)f * a.istride;
 	const uint32_t* nval = (const uint32_t*)in;
-	uint32_t vbase = 0;
-	for (int k = 0; k < b; k++) vbase += nval[k];
-	const int ch = c - a.chunk0[b];
-	const int s = ch * 64 + (int)threadIdx.x;
-	const uint32_t m = s < a.nblk[b] ? ((const uint16_t*)(in + a.mask_off[b]))[s] : 0u;
-	int tot;
-	const int ex = wave_excl(__popc(m), tot);
-	if (s >= a.nblk[b]) return;
-	uint32_t o = vbase + ((const uint32_t*)(in + a.coff_off[b]))[ch] + (uint32_t)ex;
 	const int16_t* vals = (const int16_t*)(in + a.vals_off);
-	int bx, by;
-	scan_block(s, a.dx[b], a.dy[b], bx, by);
-	const int w = a.dx[b] - bx * 4 < 4 ? a.dx[b] - bx * 4 : 4, h = a.dy[b] - by * 4 < 4 ? a.dy[b] - by * 4 : 4;
-	int16_t* band = (int16_t*)(a.arena + (size_t)f * a.astride + a.off[b]) + (long)by * 4 * a.pitch[b] + bx * 4;
-	for (int r = 0; r < h; r++)
-		for (int q = 0; q < w; q++) {
-			const int i = r * w + q;
-			band[(long)r * a.pitch[b] + q] = (m >> i) & 1 ? vals[o++] : (int16_t)0;
-		}
+	for (int c = wave_gid(); c < a.chunk0[3]; c += wave_count()) {
+		const int b = c >= a.chunk0[2] ? 2 : c >= a.chunk0[1] ? 1 : 0;
+		uint32_t vbase = 0;
+		for (int k = 0; k < b; k++) vbase += nval[k];
+		const int ch = c - a.chunk0[b];
+		const int s = ch * 64 + lane64();
+		const uint32_t m = s < a.nblk[b] ? ((const uint16_t*)(in + a.mask_off[b]))[s] : 0u;
+		int tot;
+		const int ex = wave_excl(__popc(m), tot);
+		if (s >= a.nblk[b]) continue;
+		uint32_t o = vbase + ((const uint32_t*)(in + a.coff_off[b]))[ch] + (uint32_t)ex;
+		int bx, by;
+		scan_block(s, a.dx[b], a.dy[b], bx, by);
+		const int w = a.dx[b] - bx * 4 < 4 ? a.dx[b] - bx * 4 : 4, h = a.dy[b] - by * 4 < 4 ? a.dy[b] - by * 4 : 4;
+		int16_t* band = (int16_t*)(a.arena + (size_t)f * a.astride + a.off[b]) + (long)by * 4 * a.pitch[b] + bx * 4;
+		for (int r = 0; r < h; r++)
+			for (int q = 0; q < w; q++) {
+				const int i = r * w + q;
+				band[(long)r * a.pitch[b] + q] = (m >> i) & 1 ? vals[o++] : (int16_t)0;
+			}
+	}
 }
 
 }  // namespace
@@ -185,7 +197,8 @@ DcmpLayout dcmp_layout(const Pyramid& P)
 int launch_dcmp_expand(const DcmpArgs& a, int nframes, hipStream_t st)
 {
 	if (nframes <= 0 || a.chunk0[3] <= 0) return 0;
-	hipLaunchKernelGGL(k_dcmp_expand, dim3(a.chunk0[3], 1, nframes), dim3(64), 0, st, a);
+	const int g = std::min(128, (a.chunk0[3] + 4 * kCmpWaves - 1) / (4 * kCmpWaves));
+	hipLaunchKernelGGL(k_dcmp_expand, dim3(g, 1, nframes), dim3(64 * kCmpWaves), 0, st, a);
 	return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -228,9 +241,11 @@ size_t cmp_dense_from(const Pyramid& P)
 int launch_compact(const CmpArgs* dev_args, int nchunk, int nframes, hipStream_t st)
 {
 	if (nframes <= 0 || nchunk <= 0) return 0;
-	hipLaunchKernelGGL(k_cmp_count, dim3(nchunk, 1, nframes), dim3(64), 0, st, dev_args);
+	// about 4 chunks per wave, at most 128 workgroups per frame
+	const int g = std::min(128, (nchunk + 4 * kCmpWaves - 1) / (4 * kCmpWaves));
+	hipLaunchKernelGGL(k_cmp_count, dim3(g, 1, nframes), dim3(64 * kCmpWaves), 0, st, dev_args);
 	hipLaunchKernelGGL(k_cmp_scan, dim3(1, 1, nframes), dim3(1024), 0, st, dev_args);
-	hipLaunchKernelGGL(k_cmp_write, dim3(nchunk, 1, nframes), dim3(64), 0, st, dev_args);
+	hipLaunchKernelGGL(k_cmp_write, dim3(g, 1, nframes), dim3(64 * kCmpWaves), 0, st, dev_args);
 	return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
