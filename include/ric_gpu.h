@@ -270,8 +270,9 @@ int ric_batch_hybrid_times(ric_batch* b, double* host_ms, double* gpu_ms);
  * bands + records, 10 host encode, 11 host decode, 12 H2D of the bands,
  * 13..20 inverse level 0..7 (fused TSUQi), 21 pixel conversion out, 22 / 23 the
  * GPU stream encoder / decoder launches (ms = kernel time, frames = streams), 24
- * the compacted payload values of host-coded frames to the host (host-timed;
- * stage 9 then covers only the dense rest: int bands, LL, records).  ms are
+ * the compacted payload values of host-coded frames to the host (a kernel
+ * writing the device-mapped mirrors; stage 9 then covers only the dense rest:
+ * int bands, LL, records).  ms are
  * sums; frames = frames covered; launches = GPU launches (host: frames). */
 #define RIC_BATCH_STAGES 25
 /* Diagnostics: the batch's GPU stages alone, iters times over n <= slots

@@ -87,7 +87,7 @@ private:
 // inv level 0..7, pix_out, gpu stream encode, gpu stream decode
 // (RIC_BATCH_STAGES; the stream coder stages are per launch: ms = kernel
 // time, frames = streams).
-// B_D2HV: the compacted values of a host-coded frame (host-timed, per frame)
+// B_D2HV: the compacted values of host-coded frames, written into the host mirrors by k_cmp_to_host
 enum { B_PIXIN = 0, B_FWD = 1, B_D2H = 9, B_HENC = 10, B_HDEC = 11, B_H2D = 12, B_INV = 13, B_PIXOUT = 21, B_GENC = 22, B_GDEC = 23,
        B_D2HV = 24, B_COUNT = 25 };
 
@@ -175,7 +175,6 @@ struct ric_batch {
 	int cmp_nchunk = 0;
 	size_t cmp_dense = 0;                          // arena offset where the dense part starts
 	std::vector<char> cmp_ok;
-	std::vector<hipStream_t> cmp_st;               // per slot: the task's own copy stream
 	// the decode side: the host decoder's finest level compacted
 	// (tree_decode_compact), scattered on the device (k_dcmp_expand)
 	bool dcompact = false;
@@ -192,6 +191,7 @@ struct ric_batch {
 	long pitch = 0;                                // coding plane row pitch (elements)
 	char* d_arena = nullptr;                       // 2 * slots slots
 	char* h_arena = nullptr;
+	char* h_arena_dev = nullptr;                   // the mirror's device-mapped address (k_cmp_to_host)
 	int16_t* d_planes = nullptr;
 	uint8_t* d_stage = nullptr;                    // host pixels in / out, w*h*channels per slot
 	hipStream_t st = nullptr;
@@ -316,12 +316,20 @@ int gpu_encode_plane(ric_batch* b, int set, int n, int p, const uint8_t* const* 
 	if (!d2h) return RIC_OK;
 	if (abase != s0 || amul != 1) return RIC_E_ARG;      // the host mirrors follow the slots
 	if (b->compact) {
-		// the 16-bit bands' values in walk order (compact.hip), their counts
-		// to the host; the dense rest (int bands, LL, region B) by one copy.
-		// Each host task copies its own frame's values once the group's
-		// event has passed (host_encode_plane).
+		// the 16-bit bands' values in walk order (compact.hip), written by a
+		// kernel into the head of each frame's host mirror (only the values,
+		// no per-frame copy on another stream: the host tasks find them there
+		// once the group's event has passed); their counts and the dense rest
+		// (int bands, LL, region B) by copies
 		if (launch_compact(b->d_cmp_args + set, b->cmp_nchunk, n, b->st)) return bfail(hipGetLastError(), "compact") ? RIC_E_HIP : RIC_E_HIP;
 		BCHK(hipMemcpyAsync(b->h_cmp_total + s0, b->d_cmp_total + s0, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, b->st));
+		{
+			auto sv = b->prof.begin(B_D2HV, n, b->st);
+			if (launch_cmp_to_host(b->d_cmp + (size_t)s0 * b->cmp_stride, b->cmp_stride, b->h_arena_dev + (size_t)s0 * b->hstride,
+			                       b->hstride, b->d_cmp_total + s0, n, b->st))
+				return bfail(hipGetLastError(), "compact to host") ? RIC_E_HIP : RIC_E_HIP;
+			b->prof.end(sv);
+		}
 		auto sp = b->prof.begin(B_D2H, n, b->st);
 		BCHK(hipMemcpy2DAsync(b->harena(s0) + b->cmp_dense, b->hstride, b->arena(s0) + b->cmp_dense, b->astride,
 		                      P.b_end - b->cmp_dense, n, hipMemcpyDeviceToHost, b->st));
@@ -457,15 +465,9 @@ int host_encode_plane(ric_batch* b, int s, int p, int q, int trans, uint8_t* out
 	}
 	const int16_t* cp = nullptr;
 	if (b->compact && b->cmp_ok[s]) {
-		// this frame's compacted values (the group's event has passed)
-		const double tc = now_ms();
-		const size_t nb = (size_t)b->h_cmp_total[s] * 2;
-		if (nb > b->cmp_stride) return set_last_error("compacted payload larger than its slot"), RIC_E_HIP;
-		if (nb) {
-			BCHK(hipMemcpyAsync(b->harena(s), b->d_cmp + (size_t)s * b->cmp_stride, nb, hipMemcpyDeviceToHost, b->cmp_st[s]));
-			BCHK(hipStreamSynchronize(b->cmp_st[s]));
-		}
-		b->prof.host(B_D2HV, now_ms() - tc);
+		// this frame's compacted values, already in the mirror's head (k_cmp_to_host)
+		if ((size_t)b->h_cmp_total[s] * 2 > b->cmp_stride)
+			return set_last_error("compacted payload larger than its slot"), RIC_E_HIP;
 		cp = (const int16_t*)b->harena(s);
 	}
 	const double t0 = now_ms();
@@ -638,15 +640,13 @@ int ric_batch_create(ric_batch** out, int w, int h, int channels, int slots, int
 		b->cmp_stride = up(cmp_values(b->P) * 2, 256);
 		b->cmp_cstride = up((size_t)a.nchunk, 64);
 		b->cmp_ok.assign(ns, 0);
-		b->cmp_st.assign(ns, nullptr);
 		bool bad = b->cmp_stride > b->cmp_dense ||      // the values land in the mirror's band area
 		           bfail(hipMalloc(&b->d_cmp, ns * b->cmp_stride), "hipMalloc compact") ||
 		           bfail(hipMalloc(&b->d_cmp_cnt, ns * b->cmp_cstride * sizeof(uint32_t)), "hipMalloc compact") ||
 		           bfail(hipMalloc(&b->d_cmp_total, ns * sizeof(uint32_t)), "hipMalloc compact") ||
 		           bfail(hipHostMalloc(&b->h_cmp_total, ns * sizeof(uint32_t), 0), "hipHostMalloc compact") ||
 		           bfail(hipMalloc(&b->d_cmp_args, 2 * sizeof(CmpArgs)), "hipMalloc compact");
-		for (size_t i = 0; i < ns && !bad; i++)
-			bad = bfail(hipStreamCreateWithFlags(&b->cmp_st[i], hipStreamNonBlocking), "hipStreamCreate");
+		if (!bad) bad = bfail(hipHostGetDevicePointer((void**)&b->h_arena_dev, b->h_arena, 0), "hipHostGetDevicePointer");
 		CmpArgs h[2];
 		for (int set = 0; set < 2 && !bad; set++) {
 			h[set] = a;
@@ -693,8 +693,6 @@ void ric_batch_destroy(ric_batch* b)
 	if (b->d_cmp_total) (void)hipFree(b->d_cmp_total);
 	if (b->h_cmp_total) (void)hipHostFree(b->h_cmp_total);
 	if (b->d_cmp_args) (void)hipFree(b->d_cmp_args);
-	for (hipStream_t cs : b->cmp_st)
-		if (cs) (void)hipStreamDestroy(cs);
 	if (b->d_planes) (void)hipFree(b->d_planes);
 	if (b->d_stage) (void)hipFree(b->d_stage);
 	if (b->d_genc) (void)hipFree(b->d_genc);

@@ -101,6 +101,10 @@ struct ric_wavelet {
 	int host_threads = 1;
 	std::unique_ptr<Pool> pool;
 	std::vector<EvBuf> evbufs;
+	// the one-band reductions' result words (ric_band_tsuq / ric_band_sums):
+	// a device block and its pinned mirror, allocated with the arena
+	char* d_small = nullptr;
+	char* h_small = nullptr;
 };
 
 struct ric_mux {
@@ -571,6 +575,8 @@ int ric_wavelet_create(ric_wavelet** out, int x, int y, int level, int level_chg
 	// memset would not be ordered before this stream's copies and kernels
 	if (hip_fail(hipMalloc(&w->d_arena, w->P.arena_bytes), "hipMalloc arena") ||
 	    hip_fail(hipHostMalloc(&w->h_arena, w->P.arena_bytes, 0), "hipHostMalloc arena") ||
+	    hip_fail(hipMalloc(&w->d_small, 64), "hipMalloc small") ||
+	    hip_fail(hipHostMalloc(&w->h_small, 64, 0), "hipHostMalloc small") ||
 	    hip_fail(hipStreamCreateWithFlags(&w->st, hipStreamNonBlocking), "hipStreamCreate") ||
 	    hip_fail(hipMemsetAsync(w->d_arena, 0, w->P.arena_bytes, w->st), "hipMemset arena") ||
 	    hip_fail(hipStreamSynchronize(w->st), "hipStreamSynchronize")) {
@@ -592,6 +598,8 @@ void ric_wavelet_destroy(ric_wavelet* w)
 	if (w->d_arena) (void)hipFree(w->d_arena);
 	if (w->d_img) (void)hipFree(w->d_img);
 	if (w->h_arena) (void)hipHostFree(w->h_arena);
+	if (w->d_small) (void)hipFree(w->d_small);
+	if (w->h_small) (void)hipHostFree(w->h_small);
 	if (w->own_stream && w->st) (void)hipStreamDestroy(w->st);
 	delete w;
 }
@@ -720,8 +728,7 @@ int ric_tsuq(ric_wavelet* w, int quant, float thres, unsigned int* count)
 	if (flush_pending(w)) return RIC_E_HIP;
 	int rc = to_device(w);
 	if (rc) return rc;
-	unsigned int* d_count = nullptr;
-	HIPCHK(hipMallocAsync((void**)&d_count, sizeof(unsigned int), w->st));
+	unsigned int* d_count = (unsigned int*)w->d_small;
 	HIPCHK(hipMemsetAsync(d_count, 0, sizeof(unsigned int), w->st));
 	Pyramid& P = w->P;
 	for (int i = 0; i < P.nbands(); i++) {
@@ -733,9 +740,8 @@ int ric_tsuq(ric_wavelet* w, int quant, float thres, unsigned int* count)
 		const int T0 = tr_any(!B.is_int, (int)(th * (float)Q));
 		launch_tsuq_band(B, iQ, T0, w->d_arena, d_count, w->st);
 	}
-	unsigned int h = 0;
+	unsigned int& h = *(unsigned int*)w->h_small;
 	HIPCHK(hipMemcpyAsync(&h, d_count, sizeof(unsigned int), hipMemcpyDeviceToHost, w->st));
-	HIPCHK(hipFreeAsync(d_count, w->st));
 	HIPCHK(hipStreamSynchronize(w->st));
 	if (count) *count = h;
 	return RIC_OK;
@@ -771,13 +777,12 @@ int ric_band_tsuq(ric_wavelet* w, int index, int quant, float thres, unsigned in
 	if (Q == 0) Q = 1;
 	const int iQ = (1 << 16) / Q;
 	const int T0 = tr_any(!B.is_int, (int)(thres * (float)Q));
-	int* d = nullptr;
-	HIPCHK(hipMallocAsync((void**)&d, 3 * sizeof(int), w->st));
+	int* d = (int*)w->d_small;
+	int* h = (int*)w->h_small;
 	HIPCHK(hipMemsetAsync(d, 0, 3 * sizeof(int), w->st));
 	launch_band_tsuq(B, iQ, T0, w->d_arena, d, w->st);
-	int h[3] = {0, 0, 0};
-	HIPCHK(hipMemcpyAsync(h, d, sizeof(h), hipMemcpyDeviceToHost, w->st));
-	HIPCHK(hipFreeAsync(d, w->st));
+	HIPCHK(hipGetLastError());
+	HIPCHK(hipMemcpyAsync(h, d, 3 * sizeof(int), hipMemcpyDeviceToHost, w->st));
 	HIPCHK(hipStreamSynchronize(w->st));
 	w->host_valid = false;
 	if (count) *count = (unsigned int)h[0];
@@ -802,13 +807,12 @@ int ric_band_sums(ric_wavelet* w, int index, int64_t* sum, int64_t* ssum)
 {
 	int rc = band_begin(w, index);
 	if (rc) return rc;
-	unsigned long long* d = nullptr;
-	HIPCHK(hipMallocAsync((void**)&d, 2 * sizeof(unsigned long long), w->st));
+	unsigned long long* d = (unsigned long long*)w->d_small;
+	unsigned long long* h = (unsigned long long*)w->h_small;
 	HIPCHK(hipMemsetAsync(d, 0, 2 * sizeof(unsigned long long), w->st));
 	launch_band_sums(w->P.band(index), w->d_arena, d, w->st);
-	unsigned long long h[2] = {0, 0};
-	HIPCHK(hipMemcpyAsync(h, d, sizeof(h), hipMemcpyDeviceToHost, w->st));
-	HIPCHK(hipFreeAsync(d, w->st));
+	HIPCHK(hipGetLastError());
+	HIPCHK(hipMemcpyAsync(h, d, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, w->st));
 	HIPCHK(hipStreamSynchronize(w->st));
 	if (sum) *sum = (int64_t)h[0];
 	if (ssum) *ssum = (int64_t)h[1];

@@ -40,6 +40,10 @@ size_t cmp_values(const Pyramid& P);
 size_t cmp_dense_from(const Pyramid& P);
 // the three passes over nframes frames
 int launch_compact(const CmpArgs* dev_args, int nchunk, int nframes, hipStream_t st);
+// frame f's values (total[f] int16, from src + f * sstride, rounded up to 16
+// bytes) to dst + f * dstride: a device-mapped host mirror, written by the kernel
+int launch_cmp_to_host(const char* src, size_t sstride, char* dst, size_t dstride, const uint32_t* total, int nframes,
+                       hipStream_t st);
 
 // ---- the decode side: the host decoder's finest level (three 16-bit bands
 // without children) comes back compacted (decoder.cpp tree_decode_compact)

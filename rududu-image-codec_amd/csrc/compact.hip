@@ -170,7 +170,28 @@ __global__ __launch_bounds__(64 * kCmpWaves) void k_dcmp_expand(DcmpArgs a)
 	}
 }
 
+// the group's value streams straight into the host mirrors (pinned memory,
+// device-mapped): frame f's total[f] values, 16 bytes per lane per step, so
+// the host tasks find them in place once the group's event has passed
+__global__ __launch_bounds__(256) void k_cmp_to_host(const char* __restrict__ src, size_t sstride, char* dst,
+                                                     size_t dstride, const uint32_t* __restrict__ total)
+{
+	const int f = blockIdx.z;
+	const size_t n16 = ((size_t)total[f] * 2 + 15) / 16;
+	const uint4* s = (const uint4*)(src + (size_t)f * sstride);
+	uint4* d = (uint4*)(dst + (size_t)f * dstride);
+	for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (size_t)gridDim.x * 256) d[i] = s[i];
+}
+
 }  // namespace
+
+int launch_cmp_to_host(const char* src, size_t sstride, char* dst, size_t dstride, const uint32_t* total, int nframes,
+                       hipStream_t st)
+{
+	if (nframes <= 0) return 0;
+	hipLaunchKernelGGL(k_cmp_to_host, dim3(32, 1, nframes), dim3(256), 0, st, src, sstride, dst, dstride, total);
+	return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 
 DcmpLayout dcmp_layout(const Pyramid& P)
 {
