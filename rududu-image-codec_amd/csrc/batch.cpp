@@ -1163,7 +1163,7 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 	// batch j: forward levels in groups of S (slot set 0; stream order keeps it
 	// clear of the groups using the arenas), bands + records into pool half
 	// j & 1, then the coder launches on that half's stream
-	auto kick = [&](int j) -> int {
+	auto kick_fwd = [&](int j) -> int {
 		const int f0 = batch_f0(j), m = batch_m(j), h = j & 1;
 		for (int g0 = 0; g0 < m; g0 += S) {
 			const int gm = std::min(S, m - g0);
@@ -1173,7 +1173,15 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 			                      b->st));
 		}
 		BCHK(hipEventRecord(c.ev_fwd[h], b->st));
+		return RIC_OK;
+	};
+	// wait_other: the launch also waits for the other half's forward levels
+	// (the first two batches: every forward level of both, and of the first
+	// host groups, runs before any coder wave takes the CUs)
+	auto kick_coder = [&](int j, bool wait_other) -> int {
+		const int m = batch_m(j), h = j & 1;
 		BCHK(hipStreamWaitEvent(c.st[h], c.ev_fwd[h], 0));
+		if (wait_other) BCHK(hipStreamWaitEvent(c.st[h], c.ev_fwd[h ^ 1], 0));
 		auto sp = b->prof.begin(B_GENC, m, c.st[h]);
 		if (launch_gc_encode(c.d_args + h, m, q == 0, c.st[h])) return bfail(hipGetLastError(), "k_gc_encode") ? RIC_E_HIP : RIC_E_HIP;
 		b->prof.end(sp);
@@ -1207,6 +1215,10 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 		BCHK(hipEventRecord(c.ev_done[h], c.st[h]));
 		copied[j].reset(bgpu[j] ? 0 : m);
 		return RIC_OK;
+	};
+	auto kick = [&](int j) -> int {
+		const int r = kick_fwd(j);
+		return r ? r : kick_coder(j, false);
 	};
 	// batch j's coder launches are done: (host decode) its decode groups become
 	// ready; (gpu_decode) its frames go through the inverse levels right away
@@ -1347,6 +1359,9 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 		return r2;
 	};
 	bool running[2] = {false, false};
+	// RIC_FWD_AHEAD=0: each batch's coder launch starts after its own forward
+	// levels (the second batch's then run beside the first batch's coder waves)
+	static const bool fwd_ahead = [] { const char* e = getenv("RIC_FWD_AHEAD"); return !e || atoi(e) != 0; }();
 	while (rc == RIC_OK && (finished < nbatch || !ready_host.empty() || !ready_dec.empty() || !fl.empty())) {
 		// the oldest batch whose encode is still out: a GPU-decoded batch's
 		// streams start for the host
@@ -1379,6 +1394,24 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 		}
 		// kick the next batch when its half is free: the batch before it on that
 		// half has been harvested and (host decode) its streams copied out
+		if (fwd_ahead && kicked == 0 && nbatch >= 2) {
+			// the step's start: the first host groups' and both coder batches'
+			// forward levels, then both coder launches (level 0 runs alone on
+			// the CUs, not beside the coder waves)
+			while (rc == RIC_OK && fl.size() < 2 && !ready_host.empty()) {
+				const HGroup g = ready_host.front();
+				ready_host.pop_front();
+				rc = launch_group(g);
+			}
+			if (rc == RIC_OK) rc = kick_fwd(0);
+			if (rc == RIC_OK) rc = kick_fwd(1);
+			for (int j = 0; j < 2 && rc == RIC_OK; j++) {
+				rc = kick_coder(j, j == 0);
+				running[j] = rc == RIC_OK;
+				kicked++;
+			}
+			if (rc) break;
+		}
 		while (rc == RIC_OK && kicked < nbatch && kicked - finished < 2 &&
 		       (kicked < 2 || copied[kicked - 2].wait_for_ms(0))) {
 			rc = kick(kicked);
