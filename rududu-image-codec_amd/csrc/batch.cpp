@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <map>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -221,6 +222,7 @@ struct ric_batch {
 		hipStream_t st[2] = {nullptr, nullptr};    // coder stream of each half
 		hipEvent_t ev_fwd[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr};
 		hipEvent_t ev_enc[2] = {nullptr, nullptr};   // a half's encode (and its result words) done
+		uint64_t* d_ts = nullptr;                  // RIC_GC_TSTAMP: per half, the waves' start / end stamps
 	} cp;
 
 	int nslot() const { return 2 * slots; }
@@ -709,6 +711,7 @@ void ric_batch_destroy(ric_batch* b)
 		if (c.d_dargs) (void)hipFree(c.d_dargs);
 		if (c.d_res) (void)hipFree(c.d_res);
 		if (c.h_res) (void)hipHostFree(c.h_res);
+		if (c.d_ts) (void)hipFree(c.d_ts);
 		for (int h = 0; h < 2; h++) {
 			if (c.ev_fwd[h]) (void)hipEventDestroy(c.ev_fwd[h]);
 			if (c.ev_done[h]) (void)hipEventDestroy(c.ev_done[h]);
@@ -907,6 +910,7 @@ int ric_batch_encode_gpu(ric_batch* b, const uint8_t* const* pix, int n, int q, 
 		BCHK(hipHostMalloc(&b->h_res, sizeof(uint32_t) * 2 * b->nslot(), 0));
 	}
 	GEncArgs& a = b->genc;
+	a.ts = nullptr;
 	a.arena = b->arena(0); a.astride = (size_t)C * b->astride;
 	a.pstride = b->astride; a.nplanes = C;
 	a.out = out; a.ostride = ostride; a.cap = cap;
@@ -985,6 +989,7 @@ int ric_batch_decode_gpu(ric_batch* b, const uint8_t* in, size_t istride, const 
 	a.lens = b->d_res; a.lens_stride = 2;
 	a.res = b->d_res + 2 * b->slots;          // after the lengths (2 words per frame)
 	a.dbg = (uint32_t*)g_gdec_dbg;
+	a.ts = nullptr;
 	a.w = b->w; a.h = b->h;
 	gc_bands(b->P, a.ll, a.b, a.nb);
 	BCHK(hipMemcpyAsync(b->d_gdec, &a, sizeof(GDecArgs), hipMemcpyHostToDevice, b->st));
@@ -1045,6 +1050,7 @@ int ric_batch_hybrid_config(ric_batch* b, int pool_frames, size_t stream_cap)
 	if (c.d_out) { BCHK(hipFree(c.d_out)); c.d_out = nullptr; }
 	if (c.d_res) { BCHK(hipFree(c.d_res)); c.d_res = nullptr; }
 	if (c.h_res) { BCHK(hipHostFree(c.h_res)); c.h_res = nullptr; }
+	if (c.d_ts) { BCHK(hipFree(c.d_ts)); c.d_ts = nullptr; }
 	c.n = pool_frames;
 	c.abstride = (b->P.b_end + 65535) / 65536 * 65536;
 	c.ocap = stream_cap;
@@ -1107,9 +1113,14 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 	const int S = b->slots;
 	auto res_enc = [&](int h) { return (size_t)h * 3 * c.n; };           // word offsets into d_res / h_res
 	auto res_dec = [&](int h) { return (size_t)h * 3 * c.n + 2 * (size_t)c.n; };
+	// RIC_GC_TSTAMP=1: every coder wave's start and end, summarised per launch
+	// on stderr at its harvest (when the waves end: the launch's tail)
+	static const bool tstamp = [] { const char* e = getenv("RIC_GC_TSTAMP"); return e && atoi(e) > 0; }();
+	if (tstamp && c.d_ab && !c.d_ts) BCHK(hipMalloc(&c.d_ts, sizeof(uint64_t) * 16 * (size_t)c.n));
 	if (c.d_ab) {
 		for (int h = 0; h < 2; h++) {
 			GEncArgs& a = c.args[h];
+			a.ts = tstamp ? c.d_ts + (size_t)h * 8 * c.n : nullptr;
 			a.arena = c.d_ab + (size_t)h * c.n * c.abstride; a.astride = c.abstride;
 			a.pstride = c.abstride; a.nplanes = 1;                        // gray (checked above)
 			a.out = c.d_out + (size_t)h * c.n * c.ocap; a.ostride = c.ocap; a.cap = c.ocap;
@@ -1124,6 +1135,7 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 			d.lens = a.res; d.lens_stride = 2;
 			d.res = c.d_res + res_dec(h);
 			d.dbg = nullptr;
+			d.ts = tstamp ? c.d_ts + (size_t)h * 8 * c.n + 4 * (size_t)c.n : nullptr;
 			d.w = b->w; d.h = b->h;
 			gc_bands(P, d.ll, d.b, d.nb);
 		}
@@ -1248,6 +1260,68 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 		const uint32_t* rd = c.h_res + res_dec(h);
 		if (copier[j].joinable()) copier[j].join();
 		if (copy_rc[j]) return copy_rc[j];
+		if (tstamp) {
+			// per kernel: waves' end times from the kernel's first start, ms (p0 p10 p50 p90 p100),
+			// the mean wave duration, and the waves per SIMD they ran beside (this launch's own)
+			std::vector<uint64_t> t(8 * (size_t)m);
+			BCHK(hipMemcpy(t.data(), c.d_ts + (size_t)h * 8 * c.n, sizeof(uint64_t) * 4 * m, hipMemcpyDeviceToHost));
+			BCHK(hipMemcpy(t.data() + 4 * m, c.d_ts + (size_t)h * 8 * c.n + 4 * (size_t)c.n, sizeof(uint64_t) * 4 * m,
+			               hipMemcpyDeviceToHost));
+			static std::mutex ts_mu;
+			std::lock_guard<std::mutex> g(ts_mu);
+			// RIC_GC_TSTAMP_FILE: every wave as a line (call, batch, kernel, frame, start, end, HW_ID, XCC_ID)
+			static FILE* tsf = [] { const char* e = getenv("RIC_GC_TSTAMP_FILE"); return e ? fopen(e, "a") : (FILE*)nullptr; }();
+			static int ts_call = 0;
+			if (j == 0) ts_call++;
+			if (tsf) {
+				for (int kk = 0; kk < (bgpu[j] ? 2 : 1); kk++)
+					for (int k = 0; k < m; k++) {
+						const uint64_t* w = t.data() + (size_t)kk * 4 * m + 4 * (size_t)k;
+						fprintf(tsf, "%d %d %d %d %llu %llu %llu %llu\n", ts_call, j, kk, k, (unsigned long long)w[0],
+						        (unsigned long long)w[1], (unsigned long long)(w[2] & 0xFFFFFFFFu), (unsigned long long)(w[2] >> 32));
+					}
+				fflush(tsf);
+			}
+			for (int kk = 0; kk < (bgpu[j] ? 2 : 1); kk++) {
+				const uint64_t* w = t.data() + (size_t)kk * 4 * m;
+				uint64_t t0 = ~0ull;
+				double dur = 0;
+				std::vector<double> e(m);
+				std::map<uint64_t, int> simd, cu;
+				for (int k = 0; k < m; k++) t0 = std::min(t0, w[4 * k]);
+				for (int k = 0; k < m; k++) {
+					e[k] = (double)(w[4 * k + 1] - t0) * 1e-5;
+					dur += (double)(w[4 * k + 1] - w[4 * k]) * 1e-5;
+					const uint64_t hw = w[4 * k + 2];
+					const uint64_t where = (hw >> 32) << 16 | ((hw >> 8) & 0xFF) | ((hw >> 13) & 7) << 8;   // xcc, se, cu
+					cu[where]++;
+					simd[where << 2 | ((hw >> 4) & 3)]++;
+				}
+				std::sort(e.begin(), e.end());
+				auto pc = [&](double q) { return e[std::min((size_t)(q * (m - 1) + 0.5), (size_t)m - 1)]; };
+				int hs[17] = {0}, hc[33] = {0};
+				for (auto& x : simd) hs[std::min(x.second, 16)]++;
+				for (auto& x : cu) hc[std::min(x.second, 32)]++;
+				fprintf(stderr, "[tstamp] batch %d %s: wave ends (ms from first start) p0 %.0f p10 %.0f p50 %.0f p90 %.0f p100 %.0f; mean wave %.0f; CUs %zu SIMDs %zu\n",
+				        j, kk ? "decode" : "encode", pc(0), pc(0.1), pc(0.5), pc(0.9), pc(1.0), dur / m, cu.size(), simd.size());
+				fprintf(stderr, "[tstamp]   SIMDs by waves:");
+				for (int i = 1; i <= 16; i++) if (hs[i]) fprintf(stderr, " %d:%d", i, hs[i]);
+				fprintf(stderr, "   CUs by waves:");
+				for (int i = 1; i <= 32; i++) if (hc[i]) fprintf(stderr, " %d:%d", i, hc[i]);
+				fprintf(stderr, "\n");
+				// mean duration by the waves on the same SIMD
+				std::map<int, std::pair<double, int>> by;
+				for (int k = 0; k < m; k++) {
+					const uint64_t hw = w[4 * k + 2];
+					const uint64_t where = (hw >> 32) << 16 | ((hw >> 8) & 0xFF) | ((hw >> 13) & 7) << 8;
+					auto& q = by[simd[where << 2 | ((hw >> 4) & 3)]];
+					q.first += (double)(w[4 * k + 1] - w[4 * k]) * 1e-5; q.second++;
+				}
+				fprintf(stderr, "[tstamp]   mean wave ms by waves on its SIMD:");
+				for (auto& x : by) fprintf(stderr, " %d:%.0f(%d)", x.first, x.second.first / x.second.second, x.second.second);
+				fprintf(stderr, "\n");
+			}
+		}
 		for (int k = 0; k < m; k++) {
 			if (re[2 * k + 1] == 2) {
 				clear_status(b);

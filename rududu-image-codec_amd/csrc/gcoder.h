@@ -33,6 +33,7 @@ struct GEncArgs {
 	size_t cap;                      // bytes available at each out
 	uint32_t* res;                   // per frame: file length, status (0 ok, 1 capacity, 2 ring timeout)
 	uint32_t status_off;
+	uint64_t* ts;                    // diagnostics: 4 words per frame: the wave's start, end (s_memrealtime, 100 MHz), HW_ID | XCC_ID << 32; or null
 	int w, h, q, trans;
 	int nb;
 	GBandDesc ll;
@@ -54,6 +55,7 @@ struct GDecArgs {
 	int lens_stride;
 	uint32_t* res;
 	uint32_t* dbg;                   // diagnostics: 8 words of coder state after the LL and each band, per frame (or null)
+	uint64_t* ts;                    // diagnostics: as GEncArgs::ts
 	int w, h;
 	int nb;
 	GBandDesc ll;

@@ -67,6 +67,17 @@ struct GTabs {
 	}
 };
 
+// diagnostics (GEncArgs::ts): the wave's start and end (s_memrealtime, 100
+// MHz), and where it ran: HW_ID (wave, SIMD, CU, SE) | XCC_ID << 32
+GC_DI void ts_put(uint64_t* ts, int f, uint64_t t_start)
+{
+	const uint64_t hw = (uint64_t)__builtin_amdgcn_s_getreg(0xF804) | (uint64_t)__builtin_amdgcn_s_getreg(0xF814) << 32;
+	GAS uint64_t* o = gst(ts) + 4 * (size_t)f;
+	o[0] = t_start;
+	o[1] = __builtin_amdgcn_s_memrealtime();
+	o[2] = hw;
+}
+
 // ------------------------------------------------------------ the encoder
 // Coded bytes go to a ring in LDS and leave for HBM in 1 KiB pieces (all 64
 // lanes, 16-byte stores) once no reservation slot points into them: single
@@ -531,6 +542,7 @@ __global__ void __launch_bounds__(64) k_gc_encode(const GEncArgs* __restrict__ a
 {
 	const GEncArgs& a = *ap;
 	const int f = blockIdx.x;
+	const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
 	const char* arena = a.arena + (size_t)f * a.astride;
 	uint8_t* out = a.out + (size_t)f * a.ostride;
 	for (int i = (int)threadIdx.x; i < 16 * 16 + 17 * 17; i += 64)
@@ -559,6 +571,7 @@ __global__ void __launch_bounds__(64) k_gc_encode(const GEncArgs* __restrict__ a
 	if (lane_id() == 0) {
 		gst(a.res)[2 * f] = rc ? 0u : end;               // file length = 9 + (end - 7) - 2
 		gst(a.res)[2 * f + 1] = rc;
+		if (a.ts) ts_put(a.ts, f, t_start);
 	}
 }
 
@@ -1135,6 +1148,7 @@ __global__ void __launch_bounds__(64) k_gc_decode(const GDecArgs* __restrict__ a
 {
 	const GDecArgs& a = *ap;
 	const int f = blockIdx.x;
+	const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
 	char* arena = a.arena + (size_t)f * a.astride;
 	const uint8_t* file = a.in + (size_t)f * a.istride;
 	const uint32_t len = gld(a.lens)[(size_t)f * a.lens_stride];
@@ -1199,7 +1213,10 @@ __global__ void __launch_bounds__(64) k_gc_decode(const GDecArgs* __restrict__ a
 			o += cnt;
 		}
 	}
-	if (l == 0) gst(a.res)[f] = d.ovf & 2 ? 3u | (d.p < (1u << 27) ? d.p << 4 : 0xFFFFFFF0u) : (d.ovf ? 1u : 0u);
+	if (l == 0) {
+		gst(a.res)[f] = d.ovf & 2 ? 3u | (d.p < (1u << 27) ? d.p << 4 : 0xFFFFFFF0u) : (d.ovf ? 1u : 0u);
+		if (a.ts) ts_put(a.ts, f, t_start);
+	}
 }
 }  // namespace
 
