@@ -445,9 +445,13 @@ def main():
         pw = b.prof_read()
         per_warm = n_host // threads
         per, t_host, t_gpu, t_eff, th, tg = per_warm, 0.0, 0.0, 0.0, 0.0, 0.0
-        if pw["host_enc"][1] and pw["gpu_enc"][2] and pw["gpu_dec"][2]:
+        coded = (pw["gpu_enc"][2] and pw["gpu_dec"][2]) or pw["gpu_rt"][2]
+        if pw["host_enc"][1] and coded:
             t_host = (pw["host_enc"][0] + pw["host_dec"][0]) / pw["host_enc"][1]     # ms per round trip per thread
-            t_gpu = pw["gpu_enc"][0] / pw["gpu_enc"][2] + pw["gpu_dec"][0] / pw["gpu_dec"][2]
+            if pw["gpu_rt"][2]:                    # encode + decode as one kernel (k_gc_roundtrip)
+                t_gpu = pw["gpu_rt"][0] / pw["gpu_rt"][2]
+            else:
+                t_gpu = pw["gpu_enc"][0] / pw["gpu_enc"][2] + pw["gpu_dec"][0] / pw["gpu_dec"][2]
             # the warmup step's own timeline: when the host side (its last round
             # trip group) and the GPU side (its last coder batch) finished; the
             # host share is scaled so both end together (a little before the GPU)
@@ -580,7 +584,7 @@ def main():
                                "source": "profiles/r03_stream_coder_salu.json"}}
         if balance:
             coder["balance"] = balance
-        for k, name in (("gpu_enc", "encode"), ("gpu_dec", "decode")):
+        for k, name in (("gpu_enc", "encode"), ("gpu_dec", "decode"), ("gpu_rt", "encode_then_decode")):
             if k in per_launch:
                 ms, fr, ln = prof[k]
                 coder[name] = {"launches": ln, "streams": fr, "ms_per_launch": round(ms / ln, 1),

@@ -90,7 +90,7 @@ private:
 // time, frames = streams).
 // B_D2HV: the compacted values of host-coded frames, written into the host mirrors by k_cmp_to_host
 enum { B_PIXIN = 0, B_FWD = 1, B_D2H = 9, B_HENC = 10, B_HDEC = 11, B_H2D = 12, B_INV = 13, B_PIXOUT = 21, B_GENC = 22, B_GDEC = 23,
-       B_D2HV = 24, B_COUNT = 25 };
+       B_D2HV = 24, B_GRT = 25, B_DEXP = 26, B_COUNT = 27 };   // B_DEXP: k_dcmp_expand (part of B_H2D)   // B_GRT: the stream coder's encode + decode as one kernel
 
 struct BProf {
 	bool on = false;
@@ -223,6 +223,10 @@ struct ric_batch {
 		hipEvent_t ev_fwd[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr};
 		hipEvent_t ev_enc[2] = {nullptr, nullptr};   // a half's encode (and its result words) done
 		uint64_t* d_ts = nullptr;                  // RIC_GC_TSTAMP: per half, the waves' start / end stamps
+		// k_gc_roundtrip: per frame of both halves, the encoder's end offset and
+		// status | 0x100, posted by the kernel into coherent host memory
+		uint32_t* h_post = nullptr;
+		uint32_t* d_post = nullptr;
 	} cp;
 
 	int nslot() const { return 2 * slots; }
@@ -385,7 +389,9 @@ int gpu_decode_plane(ric_batch* b, int set, int n, int p, const int* qs, int tra
 			}
 			a.chunk0[3] = ch;
 			a.vals_off = (uint32_t)b->dl.vals_off;
+			auto sx = b->prof.begin(B_DEXP, n, b->st);
 			if (launch_dcmp_expand(a, n, b->st)) return bfail(hipGetLastError(), "k_dcmp_expand") ? RIC_E_HIP : RIC_E_HIP;
+			b->prof.end(sx);
 		} else {
 			BCHK(hipMemcpy2DAsync(b->arena(s0), b->astride, b->harena(s0), b->hstride, P.a_end, n, hipMemcpyHostToDevice, b->st));
 		}
@@ -709,9 +715,9 @@ void ric_batch_destroy(ric_batch* b)
 		if (c.d_out) (void)hipFree(c.d_out);
 		if (c.d_args) (void)hipFree(c.d_args);
 		if (c.d_dargs) (void)hipFree(c.d_dargs);
-		if (c.d_res) (void)hipFree(c.d_res);
 		if (c.h_res) (void)hipHostFree(c.h_res);
 		if (c.d_ts) (void)hipFree(c.d_ts);
+		if (c.h_post) (void)hipHostFree(c.h_post);
 		for (int h = 0; h < 2; h++) {
 			if (c.ev_fwd[h]) (void)hipEventDestroy(c.ev_fwd[h]);
 			if (c.ev_done[h]) (void)hipEventDestroy(c.ev_done[h]);
@@ -1048,9 +1054,9 @@ int ric_batch_hybrid_config(ric_batch* b, int pool_frames, size_t stream_cap)
 		if (c.st[h]) BCHK(hipStreamSynchronize(c.st[h]));
 	if (c.d_ab) { BCHK(hipFree(c.d_ab)); c.d_ab = nullptr; }
 	if (c.d_out) { BCHK(hipFree(c.d_out)); c.d_out = nullptr; }
-	if (c.d_res) { BCHK(hipFree(c.d_res)); c.d_res = nullptr; }
-	if (c.h_res) { BCHK(hipHostFree(c.h_res)); c.h_res = nullptr; }
+	if (c.h_res) { BCHK(hipHostFree(c.h_res)); c.h_res = c.d_res = nullptr; }
 	if (c.d_ts) { BCHK(hipFree(c.d_ts)); c.d_ts = nullptr; }
+	if (c.h_post) { BCHK(hipHostFree(c.h_post)); c.h_post = c.d_post = nullptr; }
 	c.n = pool_frames;
 	c.abstride = (b->P.b_end + 65535) / 65536 * 65536;
 	c.ocap = stream_cap;
@@ -1065,10 +1071,15 @@ int ric_batch_hybrid_config(ric_batch* b, int pool_frames, size_t stream_cap)
 		               " frames: " + hipGetErrorString(e));
 		return e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation ? RIC_E_CAPACITY : RIC_E_HIP;
 	}
-	BCHK(hipMalloc(&c.d_res, sizeof(uint32_t) * 6 * c.n));          // per half: 2 n encoder words, n decoder words
-	BCHK(hipHostMalloc(&c.h_res, sizeof(uint32_t) * 6 * c.n, 0));
-	if (!c.d_args) BCHK(hipMalloc(&c.d_args, 2 * sizeof(GEncArgs)));
-	if (!c.d_dargs) BCHK(hipMalloc(&c.d_dargs, 2 * sizeof(GDecArgs)));
+	// the coder kernels write their result words straight into host memory: a
+	// copy queued behind a coder kernel on its stream held up the batch
+	// stream's own copies until the kernel ended (seconds)
+	BCHK(hipHostMalloc(&c.h_res, sizeof(uint32_t) * 6 * c.n, hipHostMallocMapped | hipHostMallocCoherent));
+	BCHK(hipHostGetDevicePointer((void**)&c.d_res, c.h_res, 0));
+	BCHK(hipHostMalloc(&c.h_post, sizeof(uint32_t) * 4 * c.n, hipHostMallocCoherent | hipHostMallocMapped));
+	BCHK(hipHostGetDevicePointer((void**)&c.d_post, c.h_post, 0));
+	if (!c.d_args) BCHK(hipMalloc(&c.d_args, 3 * sizeof(GEncArgs)));   // the halves, then both as one launch
+	if (!c.d_dargs) BCHK(hipMalloc(&c.d_dargs, 3 * sizeof(GDecArgs)));
 	for (int h = 0; h < 2; h++) {
 		if (!c.st[h]) BCHK(hipStreamCreateWithFlags(&c.st[h], hipStreamNonBlocking));
 		if (!c.ev_fwd[h]) BCHK(hipEventCreateWithFlags(&c.ev_fwd[h], hipEventDisableTiming));
@@ -1111,8 +1122,11 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 	auto& c = b->cp;
 	Pyramid& P = b->P;
 	const int S = b->slots;
-	auto res_enc = [&](int h) { return (size_t)h * 3 * c.n; };           // word offsets into d_res / h_res
-	auto res_dec = [&](int h) { return (size_t)h * 3 * c.n + 2 * (size_t)c.n; };
+	// word offsets into d_res / h_res: the encoder's 2 words per frame of both
+	// halves, then the decoder's word per frame of both (so the two halves can
+	// also run as one launch over 2 n frames)
+	auto res_enc = [&](int h) { return (size_t)h * 2 * c.n; };
+	auto res_dec = [&](int h) { return (size_t)4 * c.n + (size_t)h * c.n; };
 	// RIC_GC_TSTAMP=1: every coder wave's start and end, summarised per launch
 	// on stderr at its harvest (when the waves end: the launch's tail)
 	static const bool tstamp = [] { const char* e = getenv("RIC_GC_TSTAMP"); return e && atoi(e) > 0; }();
@@ -1120,7 +1134,7 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 	if (c.d_ab) {
 		for (int h = 0; h < 2; h++) {
 			GEncArgs& a = c.args[h];
-			a.ts = tstamp ? c.d_ts + (size_t)h * 8 * c.n : nullptr;
+			a.ts = tstamp ? c.d_ts + (size_t)h * 4 * c.n : nullptr;
 			a.arena = c.d_ab + (size_t)h * c.n * c.abstride; a.astride = c.abstride;
 			a.pstride = c.abstride; a.nplanes = 1;                        // gray (checked above)
 			a.out = c.d_out + (size_t)h * c.n * c.ocap; a.ostride = c.ocap; a.cap = c.ocap;
@@ -1135,16 +1149,20 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 			d.lens = a.res; d.lens_stride = 2;
 			d.res = c.d_res + res_dec(h);
 			d.dbg = nullptr;
-			d.ts = tstamp ? c.d_ts + (size_t)h * 8 * c.n + 4 * (size_t)c.n : nullptr;
+			d.ts = tstamp ? c.d_ts + (size_t)8 * c.n + (size_t)h * 4 * c.n : nullptr;
 			d.w = b->w; d.h = b->h;
 			gc_bands(P, d.ll, d.b, d.nb);
 		}
-		BCHK(hipMemcpy(c.d_args, c.args, sizeof(c.args), hipMemcpyHostToDevice));
-		BCHK(hipMemcpy(c.d_dargs, c.dargs, sizeof(c.dargs), hipMemcpyHostToDevice));
+		// entry 2: both halves as one launch (frames 0 .. 2 n - 1 of the pool;
+		// the arenas, streams and result words of the halves are contiguous)
+		GEncArgs ea[3] = {c.args[0], c.args[1], c.args[0]};
+		GDecArgs da[3] = {c.dargs[0], c.dargs[1], c.dargs[0]};
+		BCHK(hipMemcpy(c.d_args, ea, sizeof(ea), hipMemcpyHostToDevice));
+		BCHK(hipMemcpy(c.d_dargs, da, sizeof(da), hipMemcpyHostToDevice));
 	}
 	// RIC_HYBRID_TRACE=1: the step's timeline on stderr (kicks, encode ends,
 	// harvests, host groups, the end), ms from entry
-	static const bool trace = [] { const char* e = getenv("RIC_HYBRID_TRACE"); return e && atoi(e) > 0; }();
+	static const int trace = [] { const char* e = getenv("RIC_HYBRID_TRACE"); return e ? atoi(e) : 0; }();   // 2: every group
 	const double t_entry = now_ms();
 	auto tr = [&](const char* what, int j) {
 		if (trace) fprintf(stderr, "[hybrid] %9.1f ms %s %d\n", now_ms() - t_entry, what, j);
@@ -1172,6 +1190,60 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 	auto batch_f0 = [&](int j) { return n_host + j * c.n; };
 	auto batch_m = [&](int j) { return std::min(c.n, n - batch_f0(j)); };
 	auto abslot = [&](int h, int k) { return c.d_ab + ((size_t)h * c.n + k) * c.abstride; };
+	// RIC_FWD_AHEAD=0: each batch's coder launch starts after its own forward
+	// levels (the second batch's then run beside the first batch's coder waves)
+	static const bool fwd_ahead = [] { const char* e = getenv("RIC_FWD_AHEAD"); return !e || atoi(e) != 0; }();
+	// RIC_GC_MERGE=0: the two halves' coder kernels as two launches side by side
+	static const bool merge = [] { const char* e = getenv("RIC_GC_MERGE"); return !e || atoi(e) != 0; }();
+	// RIC_GC_FUSE=0: the merged launch as an encode kernel, then a decode kernel
+	// (1: k_gc_roundtrip, each wave goes on to decode its stream as soon as it
+	// is encoded)
+	static const bool fuse = [] { const char* e = getenv("RIC_GC_FUSE"); return !e || atoi(e) != 0; }();
+	bool fused = false;                                     // this call's first two batches ran as k_gc_roundtrip
+	// batch j's coder launches are done: (host decode) its decode groups become
+	// ready; (gpu_decode) its frames go through the inverse levels right away
+	// A GPU-decoded batch's .ric files leave for the host as soon as its encode
+	// is done, from a thread of their own (the host buffers are pageable: the
+	// copies block their caller), while the batch decodes on the GPU.
+	std::vector<std::thread> copier(nbatch > 0 ? nbatch : 1);
+	std::vector<int> copy_rc(nbatch > 0 ? nbatch : 1, RIC_OK);
+	int enc_seen = 0;                                      // batches whose encode event was handled
+	auto copy_out = [&](int j) {
+		if (copier[j].joinable()) return;                          // (fused: started at the kick)
+		const int f0 = batch_f0(j), m = batch_m(j), h = j & 1;
+		const uint32_t* re = c.h_res + res_enc(h);
+		const uint32_t* po = c.h_post + res_enc(h);
+		const bool poll = fused;
+		hipEvent_t done = c.ev_done[h];
+		copier[j] = std::thread([=, &copy_rc, &c] {
+			int r = set_dev(b->device);
+			for (int k = 0; k < m && !r; k++) {
+				uint32_t len_k, st_k;
+				if (poll) {
+					// the kernel posts each stream once it is in HBM; the kernel's
+					// end (normal or not) stops the wait
+					while (!((st_k = __atomic_load_n(po + 2 * k + 1, __ATOMIC_ACQUIRE)) & 0x100u)) {
+						if (hipEventQuery(done) != hipErrorNotReady) {
+							st_k = __atomic_load_n(po + 2 * k + 1, __ATOMIC_ACQUIRE);
+							break;
+						}
+						std::this_thread::sleep_for(std::chrono::microseconds(500));
+					}
+					if (!(st_k & 0x100u)) break;                         // harvest reports it
+					len_k = __atomic_load_n(po + 2 * k, __ATOMIC_RELAXED);
+					st_k &= 0xFFu;
+				} else {
+					len_k = re[2 * k];
+					st_k = re[2 * k + 1];
+				}
+				if (st_k || len_k > cap[f0 + k]) break;   // harvest reports it
+				if (bfail(hipMemcpy(out[f0 + k], c.d_out + ((size_t)h * c.n + k) * c.ocap, len_k, hipMemcpyDeviceToHost),
+				          "hipMemcpy stream"))
+					r = RIC_E_HIP;
+			}
+			copy_rc[j] = r;
+		});
+	};
 	// batch j: forward levels in groups of S (slot set 0; stream order keeps it
 	// clear of the groups using the arenas), bands + records into pool half
 	// j & 1, then the coder launches on that half's stream
@@ -1197,8 +1269,6 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 		auto sp = b->prof.begin(B_GENC, m, c.st[h]);
 		if (launch_gc_encode(c.d_args + h, m, q == 0, c.st[h])) return bfail(hipGetLastError(), "k_gc_encode") ? RIC_E_HIP : RIC_E_HIP;
 		b->prof.end(sp);
-		BCHK(hipMemcpyAsync(c.h_res + res_enc(h), c.d_res + res_enc(h), sizeof(uint32_t) * 2 * c.n, hipMemcpyDeviceToHost,
-		                    c.st[h]));
 		BCHK(hipEventRecord(c.ev_enc[h], c.st[h]));
 		if (gpu_decode == 1) bgpu[j] = 1;
 		else if (gpu_decode == 2) {
@@ -1221,38 +1291,61 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 				return bfail(hipGetLastError(), "k_gc_decode") ? RIC_E_HIP : RIC_E_HIP;
 			b->prof.end(sd);
 		}
-		if (bgpu[j])
-			BCHK(hipMemcpyAsync(c.h_res + res_dec(h), c.d_res + res_dec(h), sizeof(uint32_t) * c.n, hipMemcpyDeviceToHost,
-			                    c.st[h]));
 		BCHK(hipEventRecord(c.ev_done[h], c.st[h]));
 		copied[j].reset(bgpu[j] ? 0 : m);
+		return RIC_OK;
+	};
+	// batches 0 and 1 (both GPU-decoded) as one launch of both pool halves:
+	// dispatched at once onto an idle chip, the waves spread evenly over the
+	// SIMDs (two launches side by side each spread on their own, so SIMDs
+	// held two to four coder waves, and the four-wave ones set each phase's end)
+	auto kick_both = [&]() -> int {
+		const int m = batch_m(0) + batch_m(1);
+		BCHK(hipStreamWaitEvent(c.st[0], c.ev_fwd[0], 0));
+		BCHK(hipStreamWaitEvent(c.st[0], c.ev_fwd[1], 0));
+		if (fuse && q != 0) {
+			// one kernel: each wave encodes its frame, posts the stream (the
+			// copiers take it from there at once) and decodes it
+			for (size_t i = 0; i < 4 * (size_t)c.n; i++) __atomic_store_n(c.h_post + i, 0u, __ATOMIC_RELAXED);
+			__atomic_thread_fence(__ATOMIC_SEQ_CST);
+			fused = true;
+			auto sp = b->prof.begin(B_GRT, m, c.st[0]);
+			if (launch_gc_roundtrip(c.d_args + 2, c.d_dargs + 2, c.d_post, m, c.st[0]))
+				return bfail(hipGetLastError(), "k_gc_roundtrip") ? RIC_E_HIP : RIC_E_HIP;
+			b->prof.end(sp);
+			for (int j = 0; j < 2; j++) {
+				BCHK(hipEventRecord(c.ev_enc[j], c.st[0]));
+				BCHK(hipEventRecord(c.ev_done[j], c.st[0]));
+				bgpu[j] = 1;
+				t_kick[j] = now_ms();
+				tr("kick", j);
+				copied[j].reset(0);
+				copy_out(j);
+			}
+			return RIC_OK;
+		}
+		auto sp = b->prof.begin(B_GENC, m, c.st[0]);
+		if (launch_gc_encode(c.d_args + 2, m, q == 0, c.st[0])) return bfail(hipGetLastError(), "k_gc_encode") ? RIC_E_HIP : RIC_E_HIP;
+		b->prof.end(sp);
+		BCHK(hipEventRecord(c.ev_enc[0], c.st[0]));
+		BCHK(hipEventRecord(c.ev_enc[1], c.st[0]));
+		for (int j = 0; j < 2; j++) {
+			bgpu[j] = 1;
+			t_kick[j] = now_ms();
+			tr("kick", j);
+		}
+		auto sd = b->prof.begin(B_GDEC, m, c.st[0]);
+		if (launch_gc_decode(c.d_dargs + 2, m, c.st[0])) return bfail(hipGetLastError(), "k_gc_decode") ? RIC_E_HIP : RIC_E_HIP;
+		b->prof.end(sd);
+		BCHK(hipEventRecord(c.ev_done[0], c.st[0]));
+		BCHK(hipEventRecord(c.ev_done[1], c.st[0]));
+		copied[0].reset(0);
+		copied[1].reset(0);
 		return RIC_OK;
 	};
 	auto kick = [&](int j) -> int {
 		const int r = kick_fwd(j);
 		return r ? r : kick_coder(j, false);
-	};
-	// batch j's coder launches are done: (host decode) its decode groups become
-	// ready; (gpu_decode) its frames go through the inverse levels right away
-	// A GPU-decoded batch's .ric files leave for the host as soon as its encode
-	// is done, from a thread of their own (the host buffers are pageable: the
-	// copies block their caller), while the batch decodes on the GPU.
-	std::vector<std::thread> copier(nbatch > 0 ? nbatch : 1);
-	std::vector<int> copy_rc(nbatch > 0 ? nbatch : 1, RIC_OK);
-	int enc_seen = 0;                                      // batches whose encode event was handled
-	auto copy_out = [&](int j) {
-		const int f0 = batch_f0(j), m = batch_m(j), h = j & 1;
-		const uint32_t* re = c.h_res + res_enc(h);
-		copier[j] = std::thread([=, &copy_rc, &c] {
-			int r = set_dev(b->device);
-			for (int k = 0; k < m && !r; k++) {
-				if (re[2 * k + 1] || re[2 * k] > cap[f0 + k]) break;   // harvest reports it
-				if (bfail(hipMemcpy(out[f0 + k], c.d_out + ((size_t)h * c.n + k) * c.ocap, re[2 * k], hipMemcpyDeviceToHost),
-				          "hipMemcpy stream"))
-					r = RIC_E_HIP;
-			}
-			copy_rc[j] = r;
-		});
 	};
 	auto harvest = [&](int j) -> int {
 		const int f0 = batch_f0(j), m = batch_m(j), h = j & 1;
@@ -1264,8 +1357,8 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 			// per kernel: waves' end times from the kernel's first start, ms (p0 p10 p50 p90 p100),
 			// the mean wave duration, and the waves per SIMD they ran beside (this launch's own)
 			std::vector<uint64_t> t(8 * (size_t)m);
-			BCHK(hipMemcpy(t.data(), c.d_ts + (size_t)h * 8 * c.n, sizeof(uint64_t) * 4 * m, hipMemcpyDeviceToHost));
-			BCHK(hipMemcpy(t.data() + 4 * m, c.d_ts + (size_t)h * 8 * c.n + 4 * (size_t)c.n, sizeof(uint64_t) * 4 * m,
+			BCHK(hipMemcpy(t.data(), c.d_ts + (size_t)h * 4 * c.n, sizeof(uint64_t) * 4 * m, hipMemcpyDeviceToHost));
+			BCHK(hipMemcpy(t.data() + 4 * m, c.d_ts + (size_t)8 * c.n + (size_t)h * 4 * c.n, sizeof(uint64_t) * 4 * m,
 			               hipMemcpyDeviceToHost));
 			static std::mutex ts_mu;
 			std::lock_guard<std::mutex> g(ts_mu);
@@ -1379,14 +1472,17 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 			int r = gpu_encode_plane(b, set, g.m, 0, pix + g.f0, q, trans);
 			if (r) return r;
 			BCHK(hipEventRecord(F.ev, b->st));
+			if (trace > 2) tr("  forward issued", g.f0);
 		}
 		F.done.reset(g.m);
+		if (trace > 1) tr(g.gpu ? "decode group launched" : "host group launched", g.f0);
 		for (int i = 0; i < g.m; i++) {
 			const int slot = set * S + i, f = g.f0 + i;
 			Flight* pf = &F;
 			if (!g.gpu) {
 				b->pool->submit([=] {
 					int r1 = bfail(hipEventSynchronize(pf->ev), "hipEventSynchronize") ? RIC_E_HIP : RIC_OK;
+					if (trace > 2 && i == 0) tr("  task: forward passed", f);
 					if (!r1) r1 = host_encode_plane(b, slot, 0, q, trans, out[f], cap[f], &len[f]);
 					if (!r1) r1 = host_decode_plane(b, slot, 0, out[f], len[f]);
 					pf->err.put(r1);
@@ -1423,19 +1519,20 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 		stream_err |= r == RIC_E_STREAM;
 		if (!F.g.gpu) {
 			b->hyb_host_ms = now_ms() - t_entry;
-			if (++host_groups_done == 1 || host_groups_done == (n_host + S - 1) / S) tr("host group done", host_groups_done);
+			if (++host_groups_done == 1 || host_groups_done == (n_host + S - 1) / S || trace > 1) tr("host group done", host_groups_done);
+		} else if (trace > 1) {
+			tr("decode group done", F.g.f0);
 		}
 		if (!r2) r2 = gpu_decode_plane(b, F.set, F.g.m, 0, qs.data(), trans);
+		if (trace > 2) tr("  inverse issued", F.g.f0);
 		if (!r2) r2 = gpu_pix_out(b, F.set, F.g.m, qs.data(), pix_out + F.g.f0, 1, F.g.f0);
+		if (trace > 2) tr("  pix out issued", F.g.f0);
 		if (!r2) BCHK(hipEventRecord(F.ev, b->st));   // the set's mirrors are free once this passes
 		set_busy[F.set] = false;
 		fl.pop_front();
 		return r2;
 	};
 	bool running[2] = {false, false};
-	// RIC_FWD_AHEAD=0: each batch's coder launch starts after its own forward
-	// levels (the second batch's then run beside the first batch's coder waves)
-	static const bool fwd_ahead = [] { const char* e = getenv("RIC_FWD_AHEAD"); return !e || atoi(e) != 0; }();
 	while (rc == RIC_OK && (finished < nbatch || !ready_host.empty() || !ready_dec.empty() || !fl.empty())) {
 		// the oldest batch whose encode is still out: a GPU-decoded batch's
 		// streams start for the host
@@ -1479,7 +1576,12 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 			}
 			if (rc == RIC_OK) rc = kick_fwd(0);
 			if (rc == RIC_OK) rc = kick_fwd(1);
-			for (int j = 0; j < 2 && rc == RIC_OK; j++) {
+			if (rc == RIC_OK && merge && gpu_decode == 1) {
+				rc = kick_both();
+				running[0] = running[1] = rc == RIC_OK;
+				kicked = 2;
+			}
+			for (int j = kicked; j < 2 && rc == RIC_OK; j++) {
 				rc = kick_coder(j, j == 0);
 				running[j] = rc == RIC_OK;
 				kicked++;

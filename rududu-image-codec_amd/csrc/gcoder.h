@@ -68,6 +68,12 @@ int launch_gc_decode(const GDecArgs* dev_args, int nframes, hipStream_t st);
 // lossless: q == 0 (the 8 KiB byte ring; lossy streams take a 4 KiB one).
 int launch_gc_encode(const GEncArgs* dev_args, int nframes, int lossless, hipStream_t st);
 
+// k_gc_roundtrip over n lossy frames: each wave encodes its frame (as
+// k_gc_encode), posts the stream's end offset and status | 0x100 to
+// posted[2 f], posted[2 f + 1] (host-visible memory, written once the stream is
+// in HBM), then decodes it (as k_gc_decode, lens from the encoder).
+int launch_gc_roundtrip(const GEncArgs* dev_eargs, const GDecArgs* dev_dargs, uint32_t* posted, int nframes, hipStream_t st);
+
 // Fill the band descriptors (coding order) of a pyramid.
 inline void gc_bands(const Pyramid& P, GBandDesc& ll, GBandDesc* b, int& nb)
 {

@@ -537,17 +537,21 @@ GC_DI void tree_enc(E& e, const GTabs& T, const GBandDesc& B, const char* arena)
 // fine, V, H, D.  The .ric file goes to out + f * ostride: the 9-byte header
 // (ric.cpp:142-152) then the payload; the coder buffer starts at out + 7 and
 // the header overwrites its two dropped leading bytes (as ric_codec).
-template <uint32_t RING>
-__global__ void __launch_bounds__(64) k_gc_encode(const GEncArgs* __restrict__ ap)
+GC_DI void load_huff()
 {
-	const GEncArgs& a = *ap;
-	const int f = blockIdx.x;
-	const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
-	const char* arena = a.arena + (size_t)f * a.astride;
-	uint8_t* out = a.out + (size_t)f * a.ostride;
 	for (int i = (int)threadIdx.x; i < 16 * 16 + 17 * 17; i += 64)
 		g_huff[i] = i < 256 ? kHuff_HIGH[i >> 4][i & 15] : kHuff_LOW[(i - 256) / 17][(i - 256) % 17];
 	__syncthreads();
+}
+
+// frame f's whole stream; *end: the coder's end offset (file length 9 + end -
+// 9), the status: 0 ok, 1 capacity, 2 a fused level kernel's ring timeout, 3
+// the LDS ring overran / a guard
+template <uint32_t RING>
+GC_DI uint32_t enc_frame(const GEncArgs& a, int f, uint32_t& end_out)
+{
+	const char* arena = a.arena + (size_t)f * a.astride;
+	uint8_t* out = a.out + (size_t)f * a.ostride;
 	int32_t status = 0;
 	for (int p = 0; p < a.nplanes; p++) status |= *gld((const int32_t*)(arena + p * a.pstride + a.status_off));
 	GTabs T;
@@ -568,6 +572,19 @@ __global__ void __launch_bounds__(64) k_gc_encode(const GEncArgs* __restrict__ a
 	if (status) rc = 2;                                  // a fused kernel's ring timeout
 	else if (e.ovf & 6) rc = 3;                          // the LDS ring overran (pathological stream) / guard
 	else if (e.ovf) rc = 1;
+	end_out = end;
+	return rc;
+}
+
+template <uint32_t RING>
+__global__ void __launch_bounds__(64) k_gc_encode(const GEncArgs* __restrict__ ap)
+{
+	const GEncArgs& a = *ap;
+	const int f = blockIdx.x;
+	const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+	load_huff();
+	uint32_t end;
+	const uint32_t rc = enc_frame<RING>(a, f, end);
 	if (lane_id() == 0) {
 		gst(a.res)[2 * f] = rc ? 0u : end;               // file length = 9 + (end - 7) - 2
 		gst(a.res)[2 * f + 1] = rc;
@@ -586,8 +603,12 @@ __global__ void __launch_bounds__(64) k_gc_encode(const GEncArgs* __restrict__ a
 constexpr uint32_t kDRing = 4096;
 constexpr uint32_t kDAhead = 2048;     // bytes staged past the read position at each refill
 constexpr uint32_t kDMargin = 512;     // staged bytes kept ahead of a block / a unary run's bin
-__shared__ __attribute__((aligned(16))) uint8_t g_dring[kDRing];
-__shared__ int32_t g_blk[64 * 16];     // the current chunk's decoded blocks, 16 values each
+// The decoder's LDS is the lossy encoder's: its byte ring is the encoder's 4
+// KiB ring and its chunk of decoded blocks the encoder's coefficient chunk, so a
+// wave that encodes and then decodes (k_gc_roundtrip) holds 9.3 KiB, as either.
+#define g_dring g_ring4
+#define g_blk ((int32_t*)g_coef)
+static_assert(kDRing == sizeof(g_ring4), "the decoder's ring is the lossy encoder's");
 
 // enumDecode<16> patterns for k = 1..8 (filled once per device by
 // launch_gc_decode): g_enum16[g_enum16_off[k] + code]
@@ -1143,17 +1164,13 @@ GC_DI void tree_dec(GDec& d, const GTabs& T, const GBandDesc& B, const GBandDesc
 // order (src/ric/ric.cpp:207-225 -> CWavelet2D::DecodeBand,
 // src/lib/wavelet2d.cpp:179-222): the coarsest LL, then coarse to fine V, H, D.
 // The bands land in the frame's arena, ready for the inverse kernels.
+// frame f's stream of len bytes decoded into its arena; the result word (0
+// ok, 1 the stream ran past its end, 3 | position << 4 a staging overrun)
 template <bool ETAB>
-__global__ void __launch_bounds__(64) k_gc_decode(const GDecArgs* __restrict__ ap)
+GC_DI uint32_t dec_frame(const GDecArgs& a, int f, uint32_t len)
 {
-	const GDecArgs& a = *ap;
-	const int f = blockIdx.x;
-	const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
 	char* arena = a.arena + (size_t)f * a.astride;
 	const uint8_t* file = a.in + (size_t)f * a.istride;
-	const uint32_t len = gld(a.lens)[(size_t)f * a.lens_stride];
-	for (int i = (int)threadIdx.x; i < 16 * 16 + 17 * 17; i += 64)
-		g_huff[i] = i < 256 ? kHuff_HIGH[i >> 4][i & 15] : kHuff_LOW[(i - 256) / 17][(i - 256) % 17];
 	const uint32_t l = lane_id();
 	uint32_t cnk[2], binom[2];
 	for (int h = 0; h < 2; h++) {
@@ -1165,7 +1182,6 @@ __global__ void __launch_bounds__(64) k_gc_decode(const GDecArgs* __restrict__ a
 		else for (uint32_t t = 1; t <= r; t++) cb = cb * (nn - r + t) / t;
 		binom[h] = cb;
 	}
-	__syncthreads();
 	GTabs T;
 	T.init();
 	GDec d;
@@ -1213,9 +1229,57 @@ __global__ void __launch_bounds__(64) k_gc_decode(const GDecArgs* __restrict__ a
 			o += cnt;
 		}
 	}
-	if (l == 0) {
-		gst(a.res)[f] = d.ovf & 2 ? 3u | (d.p < (1u << 27) ? d.p << 4 : 0xFFFFFFF0u) : (d.ovf ? 1u : 0u);
+	return d.ovf & 2 ? 3u | (d.p < (1u << 27) ? d.p << 4 : 0xFFFFFFF0u) : (d.ovf ? 1u : 0u);
+}
+
+template <bool ETAB>
+__global__ void __launch_bounds__(64) k_gc_decode(const GDecArgs* __restrict__ ap)
+{
+	const GDecArgs& a = *ap;
+	const int f = blockIdx.x;
+	const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+	load_huff();
+	const uint32_t r = dec_frame<ETAB>(a, f, gld(a.lens)[(size_t)f * a.lens_stride]);
+	if (lane_id() == 0) {
+		gst(a.res)[f] = r;
 		if (a.ts) ts_put(a.ts, f, t_start);
+	}
+}
+
+// Encode and then decode frame f's stream on one wave (lossy streams: the
+// 4 KiB ring).  Once the stream is in HBM, its length and status go to
+// `posted` (host memory the caller polls, so the stream can leave for the host
+// while the wave decodes): posted[2 f] = the coder's end offset, posted[2 f +
+// 1] = status | 0x100.  ea.res / da.res get the words k_gc_encode /
+// k_gc_decode write.  A stream that failed is not decoded (result word 0).
+template <bool ETAB>
+__global__ void __launch_bounds__(64) k_gc_roundtrip(const GEncArgs* __restrict__ eap, const GDecArgs* __restrict__ dap,
+                                                    uint32_t* posted)
+{
+	const GEncArgs& ea = *eap;
+	const GDecArgs& da = *dap;
+	const int f = blockIdx.x;
+	const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+	load_huff();
+	uint32_t end;
+	const uint32_t rc = enc_frame<4096>(ea, f, end);
+	// the stream's stores reach memory (system scope: the host's copy engine
+	// reads it) before the words that announce it; the acquire half lets this
+	// wave's decoder read them back
+	__threadfence_system();
+	if (lane_id() == 0) {
+		gst(ea.res)[2 * f] = rc ? 0u : end;
+		gst(ea.res)[2 * f + 1] = rc;
+		if (ea.ts) ts_put(ea.ts, f, t_start);
+		__hip_atomic_store(posted + 2 * f, rc ? 0u : end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+		__hip_atomic_store(posted + 2 * f + 1, rc | 0x100u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+	}
+	__threadfence();
+	const uint64_t t_dec = __builtin_amdgcn_s_memrealtime();
+	const uint32_t r = rc ? 0u : dec_frame<ETAB>(da, f, end);
+	if (lane_id() == 0) {
+		gst(da.res)[f] = r;
+		if (da.ts) ts_put(da.ts, f, t_dec);
 	}
 }
 }  // namespace
@@ -1281,6 +1345,14 @@ static int enum16_upload(hipStream_t st)
 		return -1;
 	done |= 1ull << dev;
 	return 0;
+}
+
+int launch_gc_roundtrip(const GEncArgs* dev_eargs, const GDecArgs* dev_dargs, uint32_t* posted, int nframes, hipStream_t st)
+{
+	if (nframes <= 0) return 0;
+	if (enum16_upload(st)) return -1;
+	hipLaunchKernelGGL(k_gc_roundtrip<true>, dim3(nframes), dim3(64), 0, st, dev_eargs, dev_dargs, posted);
+	return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int launch_gc_decode(const GDecArgs* dev_args, int nframes, hipStream_t st)

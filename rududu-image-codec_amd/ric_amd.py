@@ -337,7 +337,7 @@ class Wavelet2D:
 
 
 BATCH_STAGES = (["pix_in"] + ["fwd_l%d" % l for l in range(8)] + ["d2h", "host_enc", "host_dec", "h2d"] +
-                ["inv_l%d" % l for l in range(8)] + ["pix_out", "gpu_enc", "gpu_dec", "d2h_values"])
+                ["inv_l%d" % l for l in range(8)] + ["pix_out", "gpu_enc", "gpu_dec", "d2h_values", "gpu_rt", "dcmp_expand"])
 
 
 def _ptrs(xs):
