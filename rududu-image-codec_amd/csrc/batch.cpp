@@ -244,6 +244,14 @@ struct ric_batch {
 
 namespace {
 
+// RIC_GC_PRIO: the stream coder waves' issue priority by progress (prio_band, gcoder.hip):
+// 0 one priority, 1 steps at the finest H band of each phase, 2 (default) steps through the decode's finest bands
+int gc_prio()
+{
+	static const int mode = [] { const char* e = getenv("RIC_GC_PRIO"); return e ? atoi(e) : 2; }();
+	return mode;
+}
+
 int set_dev(int device) { return bfail(hipSetDevice(device), "hipSetDevice") ? RIC_E_HIP : RIC_OK; }
 
 int quant_of(int q, int p) { return q ? quants(q + 20 + (p ? 8 : 0)) : 0; }    // Y, then chroma +C_Q_BOOST (ric.cpp:164-168)
@@ -917,6 +925,7 @@ int ric_batch_encode_gpu(ric_batch* b, const uint8_t* const* pix, int n, int q, 
 	}
 	GEncArgs& a = b->genc;
 	a.ts = nullptr;
+	a.prio = gc_prio();
 	a.arena = b->arena(0); a.astride = (size_t)C * b->astride;
 	a.pstride = b->astride; a.nplanes = C;
 	a.out = out; a.ostride = ostride; a.cap = cap;
@@ -996,6 +1005,9 @@ int ric_batch_decode_gpu(ric_batch* b, const uint8_t* in, size_t istride, const 
 	a.res = b->d_res + 2 * b->slots;          // after the lengths (2 words per frame)
 	a.dbg = (uint32_t*)g_gdec_dbg;
 	a.ts = nullptr;
+	a.prio = gc_prio();
+	a.etab = gc_enum16_table(b->st);
+	if (!a.etab) return set_last_error("GPU stream decoder: enumDecode table upload failed"), RIC_E_HIP;
 	a.w = b->w; a.h = b->h;
 	gc_bands(b->P, a.ll, a.b, a.nb);
 	BCHK(hipMemcpyAsync(b->d_gdec, &a, sizeof(GDecArgs), hipMemcpyHostToDevice, b->st));
@@ -1135,6 +1147,7 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 		for (int h = 0; h < 2; h++) {
 			GEncArgs& a = c.args[h];
 			a.ts = tstamp ? c.d_ts + (size_t)h * 4 * c.n : nullptr;
+			a.prio = gc_prio();
 			a.arena = c.d_ab + (size_t)h * c.n * c.abstride; a.astride = c.abstride;
 			a.pstride = c.abstride; a.nplanes = 1;                        // gray (checked above)
 			a.out = c.d_out + (size_t)h * c.n * c.ocap; a.ostride = c.ocap; a.cap = c.ocap;
@@ -1149,6 +1162,9 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 			d.lens = a.res; d.lens_stride = 2;
 			d.res = c.d_res + res_dec(h);
 			d.dbg = nullptr;
+			d.prio = gc_prio();
+			d.etab = gc_enum16_table(b->st);
+			if (!d.etab) return set_last_error("GPU stream decoder: enumDecode table upload failed"), RIC_E_HIP;
 			d.ts = tstamp ? c.d_ts + (size_t)8 * c.n + (size_t)h * 4 * c.n : nullptr;
 			d.w = b->w; d.h = b->h;
 			gc_bands(P, d.ll, d.b, d.nb);

@@ -33,6 +33,7 @@ struct GEncArgs {
 	size_t cap;                      // bytes available at each out
 	uint32_t* res;                   // per frame: file length, status (0 ok, 1 capacity, 2 ring timeout)
 	uint32_t status_off;
+	int prio;                        // issue priority by progress: 0 off, 1 or 2 (prio_band, gcoder.hip)
 	uint64_t* ts;                    // diagnostics: 4 words per frame: the wave's start, end (s_memrealtime, 100 MHz), HW_ID | XCC_ID << 32; or null
 	int w, h, q, trans;
 	int nb;
@@ -56,12 +57,17 @@ struct GDecArgs {
 	uint32_t* res;
 	uint32_t* dbg;                   // diagnostics: 8 words of coder state after the LL and each band, per frame (or null)
 	uint64_t* ts;                    // diagnostics: as GEncArgs::ts
+	int prio;                        // as GEncArgs::prio
+	const uint32_t* etab;            // the enumDecode<16> pattern table (gc_enum16_table())
 	int w, h;
 	int nb;
 	GBandDesc ll;
 	GBandDesc b[3 * kMaxLevels];
 };
 int launch_gc_decode(const GDecArgs* dev_args, int nframes, hipStream_t st);
+// the device address of the decoder's enumDecode<16> table (GDecArgs::etab),
+// uploaded on first use on the current device; null on failure
+const uint32_t* gc_enum16_table(hipStream_t st);
 
 // k_gc_encode over n frames: the whole .ric file of each (gray, one plane).
 // dev_args: the argument block in device memory.

@@ -58,14 +58,47 @@ struct GTabs {
 	uint32_t geo_ks;     // lane i < 25: kGeoK[i] | kGeoShift[i] << 8
 	uint32_t geo_thr;    // lane s in 1..10: kGeoThres[s - 1] | kGeoThres[s] << 16
 	uint32_t bit_thr;    // lane s in 0..9: kBitThres[s] | kBitThres[s + 1] << 16
+	uint32_t e16;        // enumDecode<16> table: lane k in 1..8 its offset (sum of C(16, j), j < k), lane 16 + k C(16, k)
 	GC_DI void init()
 	{
 		const uint32_t l = lane_id();
+		{
+			uint32_t c = 1, off = 0, ck = 0;                 // C(16, j) for j = 0, 1, ...
+			for (uint32_t j = 1; j <= 8; j++) {
+				c = c * (17 - j) / j;
+				if (j == (l & 15)) ck = c;
+				if (j < (l & 15)) off += c;
+			}
+			e16 = l < 16 ? off : ck;
+		}
 		geo_ks = l < 25 ? (uint32_t)kGeoK[l] | (uint32_t)kGeoShift[l] << 8 : 0;
 		geo_thr = (l >= 1 && l <= 10) ? (uint32_t)kGeoThres[l - 1] | (uint32_t)kGeoThres[l] << 16 : 0;
 		bit_thr = l <= 9 ? (uint32_t)kBitThres[l] | (uint32_t)kBitThres[l + 1] << 16 : 0;
 	}
 };
+
+// Issue priority by progress (GEncArgs::prio).  The SIMDs pick among their
+// waves by priority, then by age, so with equal priorities the oldest coder
+// wave of a SIMD runs ahead and its waves finish one after another, the last
+// ones alone on their SIMD (the slowest way to run them).  A wave lowers its
+// priority as it advances -- encode up to the finest level's H band 3, the rest
+// of the encode 2, then the decode 1 and 0 -- so the waves of a SIMD keep
+// level with each other.
+// prio 2 (the default) keeps the encode and the decode's coarse levels at 3
+// and steps down at the decode's finest V, H and D bands (2, 1, 0): the last
+// step, where the waves of a SIMD finish by age again, is the shortest.
+template <int P> GC_DI void set_prio(int on) { if (on) __builtin_amdgcn_s_setprio(P); }
+// the priority a wave takes at band b (of nb, coding order) of its last plane
+GC_DI void prio_band(int mode, bool dec, int b, int nb)
+{
+	if (mode == 1) {                                   // encode 3 / 2, decode 1 / 0, stepping at the finest H band
+		if (b == nb - 2) { if (dec) set_prio<0>(1); else set_prio<2>(1); }
+	} else if (mode == 2 && dec) {
+		if (b == nb - 3) set_prio<2>(1);
+		else if (b == nb - 2) set_prio<1>(1);
+		else if (b == nb - 1) set_prio<0>(1);
+	}
+}
 
 // diagnostics (GEncArgs::ts): the wave's start and end (s_memrealtime, 100
 // MHz), and where it ran: HW_ID (wave, SIMD, CU, SE) | XCC_ID << 32
@@ -565,7 +598,10 @@ GC_DI uint32_t enc_frame(const GEncArgs& a, int f, uint32_t& end_out)
 		const char* pa = arena + p * a.pstride;
 		if (a.ll.is_int) pred_enc<int32_t>(e, T, a.ll, pa);
 		else pred_enc<int16_t>(e, T, a.ll, pa);
-		for (int b = 0; b < a.nb; b++) tree_enc(e, T, a.b[b], pa);
+		for (int b = 0; b < a.nb; b++) {
+			if (p + 1 == a.nplanes) prio_band(a.prio, false, b, a.nb);
+			tree_enc(e, T, a.b[b], pa);
+		}
 	}
 	const uint32_t end = e.end();
 	uint32_t rc = 0;
@@ -582,6 +618,7 @@ __global__ void __launch_bounds__(64) k_gc_encode(const GEncArgs* __restrict__ a
 	const GEncArgs& a = *ap;
 	const int f = blockIdx.x;
 	const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+	set_prio<3>(a.prio);
 	load_huff();
 	uint32_t end;
 	const uint32_t rc = enc_frame<RING>(a, f, end);
@@ -611,13 +648,12 @@ constexpr uint32_t kDMargin = 512;     // staged bytes kept ahead of a block / a
 static_assert(kDRing == sizeof(g_ring4), "the decoder's ring is the lossy encoder's");
 
 // enumDecode<16> patterns for k = 1..8 (filled once per device by
-// launch_gc_decode): g_enum16[g_enum16_off[k] + code]
+// launch_gc_decode): g_enum16[offset of k + code], the offsets in GTabs::e16
 // Constant memory: the index is wave-uniform, so the load is a scalar one
 // (s_load_dword through the scalar cache, counted on lgkmcnt), which does not
 // wait on the walk's vector prefetch loads the way a vector load would.
 constexpr int kEnum16N = 39202;
 __constant__ uint32_t g_enum16[(kEnum16N + 1) / 2];       // two patterns per word, low half first
-__constant__ uint32_t g_enum16_off[9];
 
 struct GDec {
 	// Staging-only values, held in VGPRs (the lanes use them; the scalar walk
@@ -841,18 +877,17 @@ struct GDec {
 	// enumDecode<16> by table (the host decoder's decoder.cpp enum16): the
 	// pattern of (k, code) for k <= 8, complemented above 8.  One load from a
 	// 78 KB table in HBM (L2 / scalar-cache resident) instead of k ballot rows.
-	GC_DI uint32_t enum16(const uint32_t (&cnk)[2], const uint32_t (&binom)[2], uint32_t k)
+	// etab: the table (GDecArgs::etab); the offset of k's patterns and C(16,
+	// k) come from the lane table T.e16
+	GC_DI uint32_t enum16(const uint32_t (&cnk)[2], const GTabs& T, const uint32_t* etab, uint32_t k)
 	{
 		const bool comp = k > 8;
 		const uint32_t kk = comp ? 16 - k : k;
+		const uint32_t off = lget(T.e16, kk), lim = lget(T.e16, 16 + kk);
 		uint32_t c = enum_code(cnk, kk, 16);
-		// C(16, kk) = C(15, kk) + C(15, kk - 1): the host reads code 0 past it (corrupt streams)
-		const uint32_t i1 = (kk - 1) * 16 + 15, i0 = (kk - 2) * 16 + 15;
-		const uint32_t a1 = i1 < 64 ? lget(binom[0], i1) : lget(binom[1], i1 - 64);
-		const uint32_t a0 = kk < 2 ? 1u : (i0 < 64 ? lget(binom[0], i0) : lget(binom[1], i0 - 64));
-		if (c >= a1 + a0) c = 0;
-		const uint32_t i = g_enum16_off[kk] + c;
-		const uint32_t m = (g_enum16[i >> 1] >> ((i & 1) * 16)) & 0xFFFFu;
+		if (c >= lim) c = 0;                                 // the host reads code 0 past C(16, k) (corrupt streams)
+		const uint32_t i = off + c;
+		const uint32_t m = (etab[i >> 1] >> ((i & 1) * 16)) & 0xFFFFu;
 		return comp ? ~m & 0xFFFFu : m;
 	}
 	GC_DI uint32_t max_dec(uint32_t max)                 // maxDecode, muxcodec.cpp:526-534
@@ -1069,7 +1104,7 @@ GC_DI uint32_t block_info(const GBandDesc& B, const GBandDesc* P, const char* ar
 // parent anchors the chunk consumed are cleared by the lanes too.
 template <bool ETAB>
 GC_DI void tree_dec(GDec& d, const GTabs& T, const GBandDesc& B, const GBandDesc* P, char* arena,
-                    const uint32_t (&cnk)[2], const uint32_t (&binom)[2])
+                    const uint32_t (&cnk)[2], const uint32_t (&binom)[2], const uint32_t* etab)
 {
 	const bool high = B.high;
 	char* band = arena + B.off;
@@ -1114,7 +1149,7 @@ GC_DI void tree_dec(GDec& d, const GTabs& T, const GBandDesc& B, const GBandDesc
 				const uint32_t hrow = l < hn ? (uint32_t)g_huff[hbase + idx * hn + l] : 0u;
 				const uint32_t k = d.huff(hrow, hn) + (high ? 1u : 0u);
 				if (high || k != 0) {
-					uint32_t sig = k == 16 ? 0xFFFFu : ETAB ? d.enum16(cnk, binom, k) : d.enum_n(cnk, binom, k, 16, true);
+					uint32_t sig = k == 16 ? 0xFFFFu : ETAB ? d.enum16(cnk, T, etab, k) : d.enum_n(cnk, binom, k, 16, true);
 					GGeoD g;
 					g.load(geo, k - 1, T);
 					while (sig) {
@@ -1199,7 +1234,7 @@ GC_DI uint32_t dec_frame(const GDecArgs& a, int f, uint32_t len)
 		pred_dec(d, T, a.ll, pa);
 		for (int b = 0; b < a.nb; b++) {
 			const GBandDesc& B = a.b[b];
-			tree_dec<ETAB>(d, T, B, B.par >= 0 ? &a.b[B.par] : nullptr, pa, cnk, binom);
+			tree_dec<ETAB>(d, T, B, B.par >= 0 ? &a.b[B.par] : nullptr, pa, cnk, binom, a.etab);
 		}
 	}
 	arena += (a.nplanes - 1) * a.pstride;              // the last (or only) plane, with the diagnostics
@@ -1212,7 +1247,8 @@ GC_DI uint32_t dec_frame(const GDecArgs& a, int f, uint32_t len)
 	}
 	for (int b = 0; b < a.nb; b++) {
 		const GBandDesc& B = a.b[b];
-		tree_dec<ETAB>(d, T, B, B.par >= 0 ? &a.b[B.par] : nullptr, arena, cnk, binom);
+		prio_band(a.prio, true, b, a.nb);
+		tree_dec<ETAB>(d, T, B, B.par >= 0 ? &a.b[B.par] : nullptr, arena, cnk, binom, a.etab);
 		dump(b + 1);
 	}
 	// status in bits 0-3; on a staging overrun, the read position (diagnostic)
@@ -1238,6 +1274,8 @@ __global__ void __launch_bounds__(64) k_gc_decode(const GDecArgs* __restrict__ a
 	const GDecArgs& a = *ap;
 	const int f = blockIdx.x;
 	const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+	if (a.prio == 1) set_prio<1>(1);
+	else set_prio<3>(a.prio);
 	load_huff();
 	const uint32_t r = dec_frame<ETAB>(a, f, gld(a.lens)[(size_t)f * a.lens_stride]);
 	if (lane_id() == 0) {
@@ -1260,6 +1298,7 @@ __global__ void __launch_bounds__(64) k_gc_roundtrip(const GEncArgs* __restrict_
 	const GDecArgs& da = *dap;
 	const int f = blockIdx.x;
 	const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+	set_prio<3>(ea.prio);
 	load_huff();
 	uint32_t end;
 	const uint32_t rc = enc_frame<4096>(ea, f, end);
@@ -1276,6 +1315,7 @@ __global__ void __launch_bounds__(64) k_gc_roundtrip(const GEncArgs* __restrict_
 	}
 	__threadfence();
 	const uint64_t t_dec = __builtin_amdgcn_s_memrealtime();
+	if (da.prio == 1) set_prio<1>(1);
 	const uint32_t r = rc ? 0u : dec_frame<ETAB>(da, f, end);
 	if (lane_id() == 0) {
 		gst(da.res)[f] = r;
@@ -1315,6 +1355,7 @@ int launch_gc_encode(const GEncArgs* dev_args, int nframes, int lossless, hipStr
 // code = sum over set bits of C(position, rank + 1))
 static int enum16_upload(hipStream_t st)
 {
+	// (the kernels take the table's address from GDecArgs::etab: ric_gc_enum16_table)
 	static std::mutex mu;
 	static uint64_t done = 0;                        // devices 0..63
 	int dev = 0;
@@ -1340,11 +1381,20 @@ static int enum16_upload(hipStream_t st)
 	pat.resize((n + 1) & ~1u, 0);
 	if (hipMemcpyToSymbolAsync(HIP_SYMBOL(g_enum16), pat.data(), pat.size() * sizeof(uint16_t), 0, hipMemcpyHostToDevice, st) !=
 	        hipSuccess ||
-	    hipMemcpyToSymbolAsync(HIP_SYMBOL(g_enum16_off), off, sizeof(off), 0, hipMemcpyHostToDevice, st) != hipSuccess ||
 	    hipStreamSynchronize(st) != hipSuccess)
 		return -1;
 	done |= 1ull << dev;
 	return 0;
+}
+
+// the device address of the enumDecode<16> table (GDecArgs::etab), uploaded
+// on first use on the current device
+const uint32_t* gc_enum16_table(hipStream_t st)
+{
+	if (enum16_upload(st)) return nullptr;
+	void* p = nullptr;
+	if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_enum16)) != hipSuccess) return nullptr;
+	return (const uint32_t*)p;
 }
 
 int launch_gc_roundtrip(const GEncArgs* dev_eargs, const GDecArgs* dev_dargs, uint32_t* posted, int nframes, hipStream_t st)
