@@ -245,7 +245,8 @@ struct ric_batch {
 namespace {
 
 // RIC_GC_PRIO: the stream coder waves' issue priority by progress (prio_band, gcoder.hip):
-// 0 one priority, 1 steps at the finest H band of each phase, 2 (default) steps through the decode's finest bands
+// 0 one priority, 1 steps at the finest H band of each phase, 2 (default) steps through the decode's finest
+// bands, 3 steps at the decode's finest H and D bands and half-way through D
 int gc_prio()
 {
 	static const int mode = [] { const char* e = getenv("RIC_GC_PRIO"); return e ? atoi(e) : 2; }();

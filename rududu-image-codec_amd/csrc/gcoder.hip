@@ -97,6 +97,9 @@ GC_DI void prio_band(int mode, bool dec, int b, int nb)
 		if (b == nb - 3) set_prio<2>(1);
 		else if (b == nb - 2) set_prio<1>(1);
 		else if (b == nb - 1) set_prio<0>(1);
+	} else if (mode == 3 && dec) {                     // 2 at H, 1 at D, 0 half-way through D (tree_dec)
+		if (b == nb - 2) set_prio<2>(1);
+		else if (b == nb - 1) set_prio<1>(1);
 	}
 }
 
@@ -1104,7 +1107,7 @@ GC_DI uint32_t block_info(const GBandDesc& B, const GBandDesc* P, const char* ar
 // parent anchors the chunk consumed are cleared by the lanes too.
 template <bool ETAB>
 GC_DI void tree_dec(GDec& d, const GTabs& T, const GBandDesc& B, const GBandDesc* P, char* arena,
-                    const uint32_t (&cnk)[2], const uint32_t (&binom)[2], const uint32_t* etab)
+                    const uint32_t (&cnk)[2], const uint32_t (&binom)[2], const uint32_t* etab, bool prio_half = false)
 {
 	const bool high = B.high;
 	char* band = arena + B.off;
@@ -1122,7 +1125,9 @@ GC_DI void tree_dec(GDec& d, const GTabs& T, const GBandDesc& B, const GBandDesc
 	                       : 15u << 10;
 	const uint32_t hbase = high ? 0u : 256u, hn = high ? 16u : 17u;
 	const uint32_t lmax = is_int ? (1u << 20) : (1u << 15);
+	const int s_half = prio_half ? (nblk / 2) & ~63 : -1;
 	for (int s0 = 0; s0 < nblk; s0 += 64) {
+		if (s0 == s_half) set_prio<0>(1);
 		int bx, by;
 		const uint32_t info = block_info(B, P, arena, nblk, s0 + (int)l, bx, by);
 		// the chunk's blocks: zeros, and the marks of the propagated ones
@@ -1248,7 +1253,7 @@ GC_DI uint32_t dec_frame(const GDecArgs& a, int f, uint32_t len)
 	for (int b = 0; b < a.nb; b++) {
 		const GBandDesc& B = a.b[b];
 		prio_band(a.prio, true, b, a.nb);
-		tree_dec<ETAB>(d, T, B, B.par >= 0 ? &a.b[B.par] : nullptr, arena, cnk, binom, a.etab);
+		tree_dec<ETAB>(d, T, B, B.par >= 0 ? &a.b[B.par] : nullptr, arena, cnk, binom, a.etab, a.prio == 3 && b == a.nb - 1);
 		dump(b + 1);
 	}
 	// status in bits 0-3; on a staging overrun, the read position (diagnostic)
