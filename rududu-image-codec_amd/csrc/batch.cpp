@@ -227,6 +227,7 @@ struct ric_batch {
 		// status | 0x100, posted by the kernel into coherent host memory
 		uint32_t* h_post = nullptr;
 		uint32_t* d_post = nullptr;
+		uint32_t* d_yield = nullptr;               // raised while the batch stream runs host frames' level kernels
 	} cp;
 
 	int nslot() const { return 2 * slots; }
@@ -265,9 +266,12 @@ int lambda_of(int q, int p) { return q ? quants(q + 13 + (p ? 8 : 0)) : 0; }
 // abase / amul: frame i's arena is arena(abase + i * amul) (default: the
 // set's slots, abase = set * slots, amul 1); the GPU stream coder of colour
 // frames keeps a frame's three plane pyramids side by side (amul 3).
+// yflag: the GPU stream coder's yield flag (coder_yield, gcoder.hip), raised
+// around the level kernels only (not the copies), or null
 int gpu_encode_plane(ric_batch* b, int set, int n, int p, const uint8_t* const* pix, int q, int trans, bool d2h = true,
-                     int abase = -1, int amul = 1)
+                     int abase = -1, int amul = 1, uint32_t* yflag = nullptr)
 {
+	if (yflag && launch_gc_flag(yflag, 1, b->st)) return RIC_E_HIP;
 	Pyramid& P = b->P;
 	const int s0 = set * b->slots;
 	if (abase < 0) abase = s0;
@@ -328,6 +332,7 @@ int gpu_encode_plane(ric_batch* b, int set, int n, int p, const uint8_t* const* 
 				launch_blocks_level(P, l, !fused[l], l + 1 < P.nlev && !fused[l + 1], ar, b->st);
 	}
 	BCHK(hipGetLastError());
+	if (yflag && launch_gc_flag(yflag, 0, b->st)) return RIC_E_HIP;
 	if (!d2h) return RIC_OK;
 	if (abase != s0 || amul != 1) return RIC_E_ARG;      // the host mirrors follow the slots
 	if (b->compact) {
@@ -362,7 +367,7 @@ int gpu_encode_plane(ric_batch* b, int set, int n, int p, const uint8_t* const* 
 // host-decoded bands to the device (one strided copy), then every inverse
 // level with the fused TSUQi factors of each frame, as one launch per level.
 int gpu_decode_plane(ric_batch* b, int set, int n, int p, const int* qs, int trans, bool h2d = true, int abase = -1,
-                     int amul = 1)
+                     int amul = 1, uint32_t* yflag = nullptr)
 {
 	Pyramid& P = b->P;
 	const int s0 = set * b->slots;
@@ -407,6 +412,7 @@ int gpu_decode_plane(ric_batch* b, int set, int n, int p, const int* qs, int tra
 		b->prof.end(sp);
 	}
 	P.set_weight(trans);
+	if (yflag && launch_gc_flag(yflag, 1, b->st)) return RIC_E_HIP;      // (after the copies)
 	std::vector<int> qf(4 * n);
 	for (int l = P.nlev - 1; l >= 0; l--) {
 		const Level& L = P.L[l];
@@ -433,6 +439,7 @@ int gpu_decode_plane(ric_batch* b, int set, int n, int p, const int* qs, int tra
 		if (launch_inv_level_z(L, L.b[BL], fr, out_int, trans, qf.data(), b->zi[set][l], b->st)) return RIC_E_HIP;
 		b->prof.end(si);
 	}
+	if (yflag && launch_gc_flag(yflag, 0, b->st)) return RIC_E_HIP;
 	BCHK(hipGetLastError());
 	return RIC_OK;
 }
@@ -727,6 +734,7 @@ void ric_batch_destroy(ric_batch* b)
 		if (c.h_res) (void)hipHostFree(c.h_res);
 		if (c.d_ts) (void)hipFree(c.d_ts);
 		if (c.h_post) (void)hipHostFree(c.h_post);
+		if (c.d_yield) (void)hipFree(c.d_yield);
 		for (int h = 0; h < 2; h++) {
 			if (c.ev_fwd[h]) (void)hipEventDestroy(c.ev_fwd[h]);
 			if (c.ev_done[h]) (void)hipEventDestroy(c.ev_done[h]);
@@ -926,6 +934,7 @@ int ric_batch_encode_gpu(ric_batch* b, const uint8_t* const* pix, int n, int q, 
 	}
 	GEncArgs& a = b->genc;
 	a.ts = nullptr;
+	a.yield = nullptr;
 	a.prio = gc_prio();
 	a.arena = b->arena(0); a.astride = (size_t)C * b->astride;
 	a.pstride = b->astride; a.nplanes = C;
@@ -1006,6 +1015,7 @@ int ric_batch_decode_gpu(ric_batch* b, const uint8_t* in, size_t istride, const 
 	a.res = b->d_res + 2 * b->slots;          // after the lengths (2 words per frame)
 	a.dbg = (uint32_t*)g_gdec_dbg;
 	a.ts = nullptr;
+	a.yield = nullptr;
 	a.prio = gc_prio();
 	a.etab = gc_enum16_table(b->st);
 	if (!a.etab) return set_last_error("GPU stream decoder: enumDecode table upload failed"), RIC_E_HIP;
@@ -1070,6 +1080,10 @@ int ric_batch_hybrid_config(ric_batch* b, int pool_frames, size_t stream_cap)
 	if (c.h_res) { BCHK(hipHostFree(c.h_res)); c.h_res = c.d_res = nullptr; }
 	if (c.d_ts) { BCHK(hipFree(c.d_ts)); c.d_ts = nullptr; }
 	if (c.h_post) { BCHK(hipHostFree(c.h_post)); c.h_post = c.d_post = nullptr; }
+	if (!c.d_yield) {
+		BCHK(hipMalloc(&c.d_yield, 256));
+		BCHK(hipMemset(c.d_yield, 0, 256));
+	}
 	c.n = pool_frames;
 	c.abstride = (b->P.b_end + 65535) / 65536 * 65536;
 	c.ocap = stream_cap;
@@ -1140,6 +1154,11 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 	// also run as one launch over 2 n frames)
 	auto res_enc = [&](int h) { return (size_t)h * 2 * c.n; };
 	auto res_dec = [&](int h) { return (size_t)4 * c.n + (size_t)h * c.n; };
+	// RIC_GC_YIELD=0: the coder waves do not pause for the host frames' level
+	// kernels (coder_yield, gcoder.hip)
+	static const bool yield_on = [] { const char* e = getenv("RIC_GC_YIELD"); return !e || atoi(e) != 0; }();
+	if (c.d_yield) BCHK(hipMemsetAsync(c.d_yield, 0, 4, b->st));
+	uint32_t* yflag = yield_on ? c.d_yield : nullptr;   // host frames' level kernels raise it
 	// RIC_GC_TSTAMP=1: every coder wave's start and end, summarised per launch
 	// on stderr at its harvest (when the waves end: the launch's tail)
 	static const bool tstamp = [] { const char* e = getenv("RIC_GC_TSTAMP"); return e && atoi(e) > 0; }();
@@ -1149,6 +1168,7 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 			GEncArgs& a = c.args[h];
 			a.ts = tstamp ? c.d_ts + (size_t)h * 4 * c.n : nullptr;
 			a.prio = gc_prio();
+			a.yield = yield_on ? c.d_yield : nullptr;
 			a.arena = c.d_ab + (size_t)h * c.n * c.abstride; a.astride = c.abstride;
 			a.pstride = c.abstride; a.nplanes = 1;                        // gray (checked above)
 			a.out = c.d_out + (size_t)h * c.n * c.ocap; a.ostride = c.ocap; a.cap = c.ocap;
@@ -1164,6 +1184,7 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 			d.res = c.d_res + res_dec(h);
 			d.dbg = nullptr;
 			d.prio = gc_prio();
+			d.yield = yield_on ? c.d_yield : nullptr;
 			d.etab = gc_enum16_table(b->st);
 			if (!d.etab) return set_last_error("GPU stream decoder: enumDecode table upload failed"), RIC_E_HIP;
 			d.ts = tstamp ? c.d_ts + (size_t)8 * c.n + (size_t)h * 4 * c.n : nullptr;
@@ -1486,7 +1507,7 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 		Flight& F = fl.back();
 		F.g = g; F.set = set; F.ev = evs[set];
 		if (!g.gpu) {
-			int r = gpu_encode_plane(b, set, g.m, 0, pix + g.f0, q, trans);
+			int r = gpu_encode_plane(b, set, g.m, 0, pix + g.f0, q, trans, true, -1, 1, yflag);
 			if (r) return r;
 			BCHK(hipEventRecord(F.ev, b->st));
 			if (trace > 2) tr("  forward issued", g.f0);
@@ -1540,7 +1561,7 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 		} else if (trace > 1) {
 			tr("decode group done", F.g.f0);
 		}
-		if (!r2) r2 = gpu_decode_plane(b, F.set, F.g.m, 0, qs.data(), trans);
+		if (!r2) r2 = gpu_decode_plane(b, F.set, F.g.m, 0, qs.data(), trans, true, -1, 1, yflag);
 		if (trace > 2) tr("  inverse issued", F.g.f0);
 		if (!r2) r2 = gpu_pix_out(b, F.set, F.g.m, qs.data(), pix_out + F.g.f0, 1, F.g.f0);
 		if (trace > 2) tr("  pix out issued", F.g.f0);

@@ -34,6 +34,7 @@ struct GEncArgs {
 	uint32_t* res;                   // per frame: file length, status (0 ok, 1 capacity, 2 ring timeout)
 	uint32_t status_off;
 	int prio;                        // issue priority by progress: 0 off, 1 or 2 (prio_band, gcoder.hip)
+	const uint32_t* yield;           // the batch stream's level-kernel flag (coder_yield), or null
 	uint64_t* ts;                    // diagnostics: 4 words per frame: the wave's start, end (s_memrealtime, 100 MHz), HW_ID | XCC_ID << 32; or null
 	int w, h, q, trans;
 	int nb;
@@ -58,6 +59,7 @@ struct GDecArgs {
 	uint32_t* dbg;                   // diagnostics: 8 words of coder state after the LL and each band, per frame (or null)
 	uint64_t* ts;                    // diagnostics: as GEncArgs::ts
 	int prio;                        // as GEncArgs::prio
+	const uint32_t* yield;           // as GEncArgs::yield
 	const uint32_t* etab;            // the enumDecode<16> pattern table (gc_enum16_table())
 	int w, h;
 	int nb;
@@ -65,6 +67,8 @@ struct GDecArgs {
 	GBandDesc b[3 * kMaxLevels];
 };
 int launch_gc_decode(const GDecArgs* dev_args, int nframes, hipStream_t st);
+// *flag = v in stream order (a one-wave kernel; the coder waves poll it)
+int launch_gc_flag(uint32_t* flag, uint32_t v, hipStream_t st);
 // the device address of the decoder's enumDecode<16> table (GDecArgs::etab),
 // uploaded on first use on the current device; null on failure
 const uint32_t* gc_enum16_table(hipStream_t st);

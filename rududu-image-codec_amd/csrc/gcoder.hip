@@ -103,6 +103,18 @@ GC_DI void prio_band(int mode, bool dec, int b, int nb)
 	}
 }
 
+// Yielding to the level kernels (GEncArgs::yield): while the batch stream
+// runs the host-coded frames' level kernels it raises a flag in device memory;
+// a coder wave that finds it raised at a chunk boundary sleeps (at most ~0.25
+// ms per check, so a flag left raised only slows the coder), leaving the CU's
+// issue slots to the level kernel's waves.
+GC_DI void coder_yield(const uint32_t* flag)
+{
+	if (!flag) return;
+	for (int n = 0; n < 64 && __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); n++)
+		__builtin_amdgcn_s_sleep(127);
+}
+
 // diagnostics (GEncArgs::ts): the wave's start and end (s_memrealtime, 100
 // MHz), and where it ran: HW_ID (wave, SIMD, CU, SE) | XCC_ID << 32
 GC_DI void ts_put(uint64_t* ts, int f, uint64_t t_start)
@@ -491,7 +503,7 @@ GC_DI void code_coefs(E& e, const GTabs& T, uint32_t& geo, uint32_t gc, uint32_t
 // tree_rec_fast; bandcodec.cpp:484-589 with block_enum :346-478).  high: the
 // finest level (HIGH tables); par: the band has a parent level.
 template <typename E>
-GC_DI void tree_enc(E& e, const GTabs& T, const GBandDesc& B, const char* arena)
+GC_DI void tree_enc(E& e, const GTabs& T, const GBandDesc& B, const char* arena, const uint32_t* yield)
 {
 	const bool high = B.high, par = B.has_pin;
 	const uint64_t* rec = (const uint64_t*)(arena + B.rec_off);
@@ -521,6 +533,7 @@ GC_DI void tree_enc(E& e, const GTabs& T, const GBandDesc& B, const char* arena)
 	RIC_UNROLL
 	for (int g = 0; g < 16; g++) cn[g] = fetch_group(band, is_int, st, dx, dy, nblk, 4 * g, g, half);
 	for (int s0 = 0; s0 < nblk; s0 += 64) {
+		coder_yield(yield);
 		const RecChunk rc = rn;
 		RIC_UNROLL
 		for (int g = 0; g < 16; g++) g_coef[g * 64 + l] = unpack_coef(cn[g], is_int, half, g);
@@ -603,7 +616,7 @@ GC_DI uint32_t enc_frame(const GEncArgs& a, int f, uint32_t& end_out)
 		else pred_enc<int16_t>(e, T, a.ll, pa);
 		for (int b = 0; b < a.nb; b++) {
 			if (p + 1 == a.nplanes) prio_band(a.prio, false, b, a.nb);
-			tree_enc(e, T, a.b[b], pa);
+			tree_enc(e, T, a.b[b], pa, a.yield);
 		}
 	}
 	const uint32_t end = e.end();
@@ -1107,7 +1120,8 @@ GC_DI uint32_t block_info(const GBandDesc& B, const GBandDesc* P, const char* ar
 // parent anchors the chunk consumed are cleared by the lanes too.
 template <bool ETAB>
 GC_DI void tree_dec(GDec& d, const GTabs& T, const GBandDesc& B, const GBandDesc* P, char* arena,
-                    const uint32_t (&cnk)[2], const uint32_t (&binom)[2], const uint32_t* etab, bool prio_half = false)
+                    const uint32_t (&cnk)[2], const uint32_t (&binom)[2], const uint32_t* etab, const uint32_t* yield,
+                    bool prio_half = false)
 {
 	const bool high = B.high;
 	char* band = arena + B.off;
@@ -1127,6 +1141,7 @@ GC_DI void tree_dec(GDec& d, const GTabs& T, const GBandDesc& B, const GBandDesc
 	const uint32_t lmax = is_int ? (1u << 20) : (1u << 15);
 	const int s_half = prio_half ? (nblk / 2) & ~63 : -1;
 	for (int s0 = 0; s0 < nblk; s0 += 64) {
+		coder_yield(yield);
 		if (s0 == s_half) set_prio<0>(1);
 		int bx, by;
 		const uint32_t info = block_info(B, P, arena, nblk, s0 + (int)l, bx, by);
@@ -1239,7 +1254,7 @@ GC_DI uint32_t dec_frame(const GDecArgs& a, int f, uint32_t len)
 		pred_dec(d, T, a.ll, pa);
 		for (int b = 0; b < a.nb; b++) {
 			const GBandDesc& B = a.b[b];
-			tree_dec<ETAB>(d, T, B, B.par >= 0 ? &a.b[B.par] : nullptr, pa, cnk, binom, a.etab);
+			tree_dec<ETAB>(d, T, B, B.par >= 0 ? &a.b[B.par] : nullptr, pa, cnk, binom, a.etab, a.yield);
 		}
 	}
 	arena += (a.nplanes - 1) * a.pstride;              // the last (or only) plane, with the diagnostics
@@ -1253,7 +1268,8 @@ GC_DI uint32_t dec_frame(const GDecArgs& a, int f, uint32_t len)
 	for (int b = 0; b < a.nb; b++) {
 		const GBandDesc& B = a.b[b];
 		prio_band(a.prio, true, b, a.nb);
-		tree_dec<ETAB>(d, T, B, B.par >= 0 ? &a.b[B.par] : nullptr, arena, cnk, binom, a.etab, a.prio == 3 && b == a.nb - 1);
+		tree_dec<ETAB>(d, T, B, B.par >= 0 ? &a.b[B.par] : nullptr, arena, cnk, binom, a.etab, a.yield,
+		               a.prio == 3 && b == a.nb - 1);
 		dump(b + 1);
 	}
 	// status in bits 0-3; on a staging overrun, the read position (diagnostic)
@@ -1400,6 +1416,17 @@ const uint32_t* gc_enum16_table(hipStream_t st)
 	void* p = nullptr;
 	if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_enum16)) != hipSuccess) return nullptr;
 	return (const uint32_t*)p;
+}
+
+__global__ void k_gc_flag(uint32_t* flag, uint32_t v)
+{
+	if (threadIdx.x == 0) __hip_atomic_store(flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+int launch_gc_flag(uint32_t* flag, uint32_t v, hipStream_t st)
+{
+	hipLaunchKernelGGL(k_gc_flag, dim3(1), dim3(64), 0, st, flag, v);
+	return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int launch_gc_roundtrip(const GEncArgs* dev_eargs, const GDecArgs* dev_dargs, uint32_t* posted, int nframes, hipStream_t st)
