@@ -1251,7 +1251,7 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 		const int f0 = batch_f0(j), m = batch_m(j), h = j & 1;
 		const uint32_t* re = c.h_res + res_enc(h);
 		const uint32_t* po = c.h_post + res_enc(h);
-		const bool poll = fused;
+		const bool poll = fused && j < 2;                      // (batches 2.. take per-half launches)
 		hipEvent_t done = c.ev_done[h];
 		copier[j] = std::thread([=, &copy_rc, &c] {
 			int r = set_dev(b->device);
