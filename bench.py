@@ -581,7 +581,10 @@ def main():
                  # inside this process): SALU instructions per CU per cycle at 1920 1080p streams in flight
                  "salu_frac": {"encode": 0.489, "decode": 0.488, "decode_first_launch": 0.649,
                                "issue_frac_all_types": {"encode": 0.564, "decode": 0.586},
-                               "source": "profiles/r03_stream_coder_salu.json"}}
+                               "source": "profiles/r03_stream_coder_salu.json",
+                               "note": "k_gc_encode / k_gc_decode over 1920 1080p streams in two side-by-side "
+                                       "launches (scripts/gc_probe.py), before the merged launch, the priority "
+                                       "schedule and the enumDecode table fix"}}
         if balance:
             coder["balance"] = balance
         for k, name in (("gpu_enc", "encode"), ("gpu_dec", "decode"), ("gpu_rt", "encode_then_decode")):
