@@ -24,6 +24,11 @@ resident in HBM before the timed region; decoded frames land in HBM.
                     [--frames F] [--threads T] [--slots S]
 
 Multi-GPU: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+(one process per GPU; barrier and max-over-ranks timing over gloo on the CPU;
+the stream gather to rank 0 over the library's RCCL communicator, overlapped
+with the step).  Device memory comes from the library itself
+(ric_amd.DeviceArray): torch is imported only for torch.distributed's CPU
+process group, and never touches the GPU.
 """
 import argparse
 import hashlib
@@ -282,31 +287,48 @@ def workload_frames(a, rank, world, threads):
 def main():
     t_start = time.perf_counter()
     a = parse()
-    import torch
-    import torch.distributed as dist
-
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # the library (and its HIP runtime) first; torch only for the CPU process group
+    import ric_amd
+    import shard
+    ndev = ric_amd.lib().ric_device_count()
+    if ndev < 1:
+        raise SystemExit("bench.py: no HIP device visible")
     # one process per GPU; a rehearsal with more ranks than GPUs (gloo) wraps
-    ndev = torch.cuda.device_count()
-    local = local % max(ndev, 1)
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    # barrier, max-over-ranks timing and the stream gather go over RCCL
-    # ("nccl" is RCCL on ROCm; RIC_BENCH_BACKEND=gloo for a CPU-side rehearsal)
-    backend = os.environ.get("RIC_BENCH_BACKEND", "nccl")
-    cdev = dev if backend == "nccl" else torch.device("cpu")
+    local = local % ndev
+    # the gather's transport: RCCL (the library's communicator, xGMI) or, for a
+    # rehearsal with several ranks on one GPU, gloo on the CPU
+    backend = os.environ.get("RIC_BENCH_BACKEND", "rccl")
+    dist = None
+    transport = None
     if world > 1:
-        dist.init_process_group(backend, init_method="env://")
+        import torch
+        import torch.distributed as dist
+        dist.init_process_group("gloo", init_method="env://")
+        if backend == "gloo":
+            transport = shard.GlooTransport(dist)
+        else:
+            backend = "rccl"
+            uid = [ric_amd.Comm.unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            transport = shard.RcclTransport(ric_amd.Comm(uid[0], world, rank, local), local)
 
     def barrier():
         if world > 1:
-            t = torch.ones(1, device=cdev)
-            dist.all_reduce(t)
+            dist.barrier()
 
-    import ric_amd
-    import shard
+    def allreduce(v, op):
+        if world == 1:
+            return v
+        t = torch.tensor([float(v)], dtype=torch.float64)
+        dist.all_reduce(t, op={"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op])
+        return float(t[0])
+
+    def dsync():
+        ric_amd.device_sync(local)
+
     threads = a.threads or default_threads(world)
     W, H, CH, mine, scaling = workload_frames(a, rank, world, threads)
     nfr = len(mine)
@@ -329,7 +351,7 @@ def main():
                 rgb = ric_amd.synth(7680, 4320, 3, 0)
             _, _, x0, y0, w, h = crop
             host = np.ascontiguousarray(rgb[:, y0:y0 + h, x0:x0 + w])
-        frames.append(torch.from_numpy(host).to(dev))
+        frames.append(ric_amd.DeviceArray.from_numpy(host, local))
     # decoded-frame buffers cycled over the distinct inputs (frames k and
     # k + distinct decode the same input); every frame's output is checked
     # after the timed region through its digest, taken by the library in
@@ -338,10 +360,10 @@ def main():
     # nothing.  (One buffer per frame would take ~100 GB of HBM at C3, which
     # the stream coder's pool uses instead.)
     nout = min(nfr, a.distinct)
-    outs_d = [torch.empty((CH, H, W), dtype=torch.uint8, device=dev) for _ in range(nout)]
+    outs_d = [ric_amd.DeviceArray((CH, H, W), np.uint8, local) for _ in range(nout)]
     outs = [outs_d[k % nout] for k in range(nfr)]
-    digests = torch.zeros(max(nfr, 1), dtype=torch.int64, device=dev)
-    torch.cuda.synchronize()
+    digests = ric_amd.DeviceArray(max(nfr, 1), np.uint64, local, zero=True)
+    dsync()
 
     b = ric_amd.Batch(W, H, CH, slots=slots, threads=threads, device=local) if nfr else None
     if b is not None:
@@ -349,6 +371,17 @@ def main():
     gather = world > 1 and not a.no_gather
     gathered = [0]
     container = [None]
+    # the path's one exchange: every stream this rank codes
+    # goes to rank 0 in bounded chunks while the step runs (shard.StreamGather):
+    # a stream leaves as soon as its .ric file is complete (ric_batch_set_ready)
+    ready = np.zeros(max(nfr, 1), np.uint32)
+    gath = None
+    gstats = {"rounds": 0, "streams": 0, "bytes": 0, "digest_mismatches": 0, "tail_ms": []}
+    if gather and a.workload != "C4":
+        # allocated before the stream coder's pool, which takes the rest of HBM
+        gath = shard.StreamGather(transport, rank, world, chunk_bytes=64 << 20)
+        if b is not None:
+            b.set_ready(ready, nfr)
 
     hybrid = a.coder in ("hybrid", "gpu", "mix") and CH == 1 and b is not None
     gpu_dec = {"hybrid": 0, "gpu": 1, "mix": 2}.get(a.coder, 0)
@@ -382,20 +415,59 @@ def main():
         # buffers: host coders and the stream copier write them concurrently)
         sbufs = [np.empty(scap, np.uint8) for _ in range(nfr)]
 
+    def host_stream(i, ln):
+        return (sbufs[i] if hybrid else b._outs[i])[:ln]
+
     def step():
-        if b is not None:
-            if hybrid:
-                m = n_host + n_gpu
-                b.roundtrip_hybrid(frames[:m], outs[:m], n_host, q=a.q, trans=a.trans, gpu_decode=gpu_dec,
-                                   streams=sbufs[:m])
-            else:
-                b.roundtrip(frames, outs, q=a.q, trans=a.trans)
+        th, gres, failed = None, {}, [False]
+        if gath is not None:
+            ready[:] = 0
+            m = (n_host + n_gpu) if hybrid else nfr
+
+            def stop():
+                if failed[0]:
+                    raise RuntimeError("the step failed")
+
+            def run():
+                try:
+                    if rank == 0:
+                        gres.update(gath.receive())
+                    else:
+                        gres.update(gath.send(m if b is not None else 0, ready, host_stream, stop=stop))
+                    gres["t_end"] = time.perf_counter()
+                except Exception as e:           # reported by the main thread
+                    gres["error"] = repr(e)
+            th = threading.Thread(target=run)
+            th.start()
+        try:
+            if b is not None:
+                if hybrid:
+                    m = n_host + n_gpu
+                    b.roundtrip_hybrid(frames[:m], outs[:m], n_host, q=a.q, trans=a.trans, gpu_decode=gpu_dec,
+                                       streams=sbufs[:m])
+                else:
+                    b.roundtrip(frames, outs, q=a.q, trans=a.trans)
+        except Exception:
+            failed[0] = True
+            raise
+        t_coded = time.perf_counter()
+        if th is not None:
+            th.join()
+            if "error" in gres:
+                raise RuntimeError("rank %d: stream gather failed: %s" % (rank, gres["error"]))
+            gstats["rounds"] += gres["rounds"]
+            gstats["tail_ms"].append(round((gres["t_end"] - t_coded) * 1e3, 1))
+            if rank == 0:
+                gstats["streams"] += sum(gres["streams"]) + (n_host + n_gpu if hybrid else nfr)
+                gstats["bytes"] += sum(gres["bytes"]) + (sum(b._lens) if b is not None else 0)
+                gstats["digest_mismatches"] += len(gres["digest_mismatches"])
+                gathered[0] = gstats["bytes"]
         if gather and a.workload == "C4":
             # C4: the tile streams to rank 0 into one RTL1 container, and the
             # decode side of the exchange: the container's tiles scattered
             # back to the ranks that decode them (shard.scatter_streams)
             streams = [b.stream(i) for i in range(nfr)] if b is not None else []
-            got = shard.gather_streams(streams, dist, device=cdev)
+            got = shard.gather_streams(streams, transport, rank, world)
             per_rank = None
             if rank == 0:
                 tiles = [None] * 4
@@ -406,19 +478,9 @@ def main():
                 gathered[0] = len(container[0])
                 _, _, _, _, back = shard.unpack_tiles(container[0])
                 per_rank = [[back[i] for i in shard.tiles_of_rank(world, r)] for r in range(world)]
-            mine_back = shard.scatter_streams(per_rank, dist, device=cdev)
+            mine_back = shard.scatter_streams(per_rank, transport, rank, world)
             if mine_back != streams:
                 raise RuntimeError("rank %d: scattered tile streams differ from the encoded ones" % rank)
-        elif gather:
-            # the path's one exchange: every rank's .ric streams to rank 0
-            # (SURVEY.md §8(e)); rank 0 keeps them on the device.  With the
-            # stream coder a step holds ~1800 frames per rank (13 GB of
-            # streams): the distinct ones (--distinct, the rest repeat them) go
-            ng = min(nstep, a.distinct) if hybrid else nfr
-            streams = [b.stream(i) for i in range(ng)] if b is not None else []
-            got = shard.gather_streams(streams, dist, device=cdev, to_host=False)
-            if rank == 0:
-                gathered[0] = int(sum(int(s[1:1 + int(s[0])].sum()) for s in got[1]))
 
     def progress(what):
         # a line on stderr per step: a step with the stream coder takes seconds
@@ -463,10 +525,7 @@ def main():
                 t_eff = 1.08 * t_host
                 per = int(t_gpu / t_eff)
             per = max(1, min(per, host_frames_room(a, threads) // threads))
-        if world > 1:                          # one split for every rank: the slowest rank's
-            t = torch.tensor([per], dtype=torch.float64, device=cdev)
-            dist.all_reduce(t, op=dist.ReduceOp.MIN)
-            per = int(t[0])
+        per = int(allreduce(per, "min"))      # one split for every rank: the slowest rank's
         n_host = min(per * threads, nfr - n_gpu)
         nstep = n_host + n_gpu
         balance = {"host_round_trip_ms": round(t_host, 1), "host_wall_ms_per_frame": round(t_eff, 1),
@@ -478,19 +537,18 @@ def main():
     if b is not None:
         b.prof_enable(True)
 
+    # the warmup steps' gather statistics are not the timed ones
+    gstats.update(rounds=0, streams=0, bytes=0, digest_mismatches=0, tail_ms=[])
     barrier()
-    torch.cuda.synchronize()
+    dsync()
     t0 = time.perf_counter()
     for i in range(a.steps):
         step()
         progress("step %d/%d" % (i + 1, a.steps))
-    torch.cuda.synchronize()
+    dsync()
     dt = time.perf_counter() - t0
     barrier()
-    if world > 1:
-        tt = torch.tensor([dt], dtype=torch.float64, device=cdev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt[0])
+    dt = allreduce(dt, "max")
 
     # ---- verification (outside the timed region): EVERY frame of the last
     # step -- its .ric file and its decoded pixels -- against the reference
@@ -502,12 +560,12 @@ def main():
         notes = []
         if b is not None:
             nd = min(nstep, a.distinct)
-            exp, t_or, kind = oracle_expectations([frames[d].cpu().numpy() for d in range(nd)], a.q, a.trans, threads)
+            exp, t_or, kind = oracle_expectations([frames[d].numpy() for d in range(nd)], a.q, a.trans, threads)
             bad = []
-            got_dig = digests.cpu().numpy().view(np.uint64)
+            got_dig = digests.numpy()
             for d in range(nd):
                 want_dig = pixel_digest(exp[d][1])
-                if not torch.equal(outs_d[d % nout], torch.from_numpy(exp[d][1]).to(dev)):
+                if not np.array_equal(outs_d[d % nout].numpy(), exp[d][1].reshape(CH, H, W)):
                     bad.append(d)                  # the buffer's last writer, compared in full
                 for k in range(d, nstep, a.distinct):
                     if b.stream(k) != exp[d][0] or got_dig[k] != want_dig:
@@ -533,15 +591,15 @@ def main():
             if want:
                 e = [g for g in gold if g["name"] == want][0]
                 ok &= hashlib.sha256(b.stream(0)).hexdigest() == e["ric_sha256"]
-                ok &= hashlib.sha256(outs[0].cpu().numpy().tobytes()).hexdigest() == e["decoded_sha256"]
+                ok &= hashlib.sha256(outs[0].numpy().tobytes()).hexdigest() == e["decoded_sha256"]
                 notes.append("frame 0: %s golden sha256" % want)
+        if gath is not None and rank == 0:
+            ok &= gstats["digest_mismatches"] == 0
+            notes.append("gather: %d streams (%d bytes) at rank 0 over the timed steps, %d digest mismatches"
+                         % (gstats["streams"], gstats["bytes"], gstats["digest_mismatches"]))
         if world > 1:
-            t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=cdev)
-            dist.all_reduce(t, op=dist.ReduceOp.MIN)
-            ok = bool(int(t[0]))
-            t = torch.tensor([nstep], dtype=torch.int64, device=cdev)
-            dist.all_reduce(t)
-            notes.append("%d ranks, %d frames in all" % (world, int(t[0])))
+            ok = bool(allreduce(1 if ok else 0, "min"))
+            notes.append("%d ranks, %d frames in all" % (world, int(allreduce(nstep, "sum"))))
         verified, vnote = bool(ok), "; ".join(notes)
         if not ok:
             print(json.dumps({"error": "bench output mismatch", "rank": rank, "checked": vnote}), file=sys.stderr)
@@ -620,7 +678,7 @@ def main():
             c.set_host_threads(nt)
             ts = []
             for _ in range(4):
-                torch.cuda.synchronize()
+                dsync()
                 t0 = time.perf_counter()
                 r = c.compress(frames[0], a.q, a.trans, on_device=True)
                 ts.append(time.perf_counter() - t0)
@@ -628,10 +686,10 @@ def main():
             enc[str(nt)] = round(float(np.median(ts[1:])) * 1e3, 2)
         td = []
         for _ in range(4):
-            torch.cuda.synchronize()
+            dsync()
             t0 = time.perf_counter()
             c.decompress(want, pix_out=outs[0])
-            torch.cuda.synchronize()
+            dsync()
             td.append(time.perf_counter() - t0)
         lat = {"encode_ms_by_host_threads": enc, "decode_ms": round(float(np.median(td[1:])) * 1e3, 2),
                "bytes_equal_step_frame0": bool(same),
@@ -648,7 +706,7 @@ def main():
     split = None
     if rank == 0 and b is not None and not a.no_split and not hybrid:
         streams = [b.stream(i) for i in range(nfr)]
-        torch.cuda.synchronize()
+        dsync()
         te = time.perf_counter()
         for g in range(0, nfr, slots):
             b.compress(frames[g:g + slots], a.q, a.trans, on_device=True)
@@ -656,17 +714,14 @@ def main():
         td = time.perf_counter()
         for g in range(0, nfr, slots):
             b.decompress(streams[g:g + slots], pix_out=outs[g:g + slots])
-        torch.cuda.synchronize()
+        dsync()
         td = time.perf_counter() - td
         mpx = nfr * W * H / 1e6
         split = {"encode_mpix_s": round(mpx / te, 2), "decode_mpix_s": round(mpx / td, 2),
                  "note": "rank 0, %d frames in groups of %d, groups not pipelined" % (nfr, slots)}
 
-    total_px = sum_px = nstep * W * H
-    if world > 1:
-        t = torch.tensor([total_px], dtype=torch.float64, device=cdev)
-        dist.all_reduce(t)
-        sum_px = float(t[0])
+    total_px = nstep * W * H
+    sum_px = allreduce(total_px, "sum")
     value = sum_px * a.steps / 1e6 / dt
     wl = {"C3": "C3: 7680x4320 gray, 5-level cdf97, q=%d, .ric encode+decode round trip, bit-exact" % a.q,
           "C5": "C5: %d x 4096x4096 gray frames per step, 5-level cdf97, q=%d, encode+decode, frame f on rank f mod N"
@@ -733,7 +788,19 @@ def main():
     if lat:
         out["latency"] = lat
     if gather:
-        out["gather"] = {"backend": backend, "bytes_to_rank0_per_step": gathered[0]}
+        out["gather"] = {"backend": backend, "bytes_to_rank0_per_step": gathered[0] // max(a.steps, 1)
+                         if a.workload != "C4" else gathered[0]}
+        if gath is not None:
+            out["gather"].update({
+                "streams_to_rank0_per_step": gstats["streams"] // max(a.steps, 1),
+                "rounds_per_step": gstats["rounds"] / max(a.steps, 1),
+                "digest_mismatches": gstats["digest_mismatches"],
+                "chunk_bytes": gath.chunk,
+                "rank0_gather_buffers_bytes": (world - 1) * gath.chunk,
+                "finish_after_coding_ms": gstats["tail_ms"],
+                "note": "every stream of every rank, shipped in chunks of at most chunk_bytes while the step runs "
+                        "(a stream leaves once its .ric file is complete), digest-checked at rank 0; "
+                        "finish_after_coding_ms: how long after this rank's coding the gather ended, per timed step"})
         if a.workload == "C4":
             out["gather"]["container"] = "RTL1, 4 tiles, %d bytes; tiles scattered back per step" % gathered[0]
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

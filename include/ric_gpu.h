@@ -104,6 +104,13 @@ int ric_band_write(ric_wavelet* w, int index, const int32_t* host_in);
  * from the device; the mirror stays authoritative -- what the caller writes
  * there is what the next GPU stage reads -- until a stage rewrites the bands. */
 int ric_band_host(ric_wavelet* w, int index, void** ptr, int* pitch);
+/* CBand::pBand in the reference's own layout: a stable host buffer holding
+ * band `index` with row stride *stride samples = DimXAlign of CBand::Init
+ * (DimX * sample size rounded up to 32 bytes, src/lib/band.cpp:57), synced
+ * from the mirror on this call and whenever the mirror is rewritten
+ * (CodeBand's host half, DecodeBand); what the caller writes there goes to the
+ * device with the mirror at the next GPU stage, as through ric_band_host. */
+int ric_band_host_ref(ric_wavelet* w, int index, void** ptr, int* stride);
 /* CBand's operations on one band (band index as ric_band_info), run on the
  * device (bands written through ric_band_host go to the device first; the host
  * mirror is stale afterwards):
@@ -250,8 +257,18 @@ int ric_batch_hybrid_config(ric_batch* b, int pool_frames, size_t stream_cap);
  * write, for frame i of the call (i < n), the 64-bit digest of its decoded
  * pixels, sum over byte k of pix[k] * (k * 0x9E3779B97F4A7C15 + 1) mod 2^64,
  * to dev_digests[i] (device memory), in stream order right after the pixels.
- * n = 0 turns it off. */
+ * n = 0 turns it off.  The library keeps the pointer across calls: the buffer
+ * must stay allocated until the digests are turned off (or the batch is
+ * destroyed). */
 int ric_batch_set_digests(ric_batch* b, unsigned long long* dev_digests, long n);
+/* Stream-ready words (no reference counterpart; they let a caller ship the
+ * .ric files while the call still runs, e.g. the multi-GPU gather): while set,
+ * ric_batch_roundtrip and ric_batch_roundtrip_hybrid store, for frame i of
+ * the call (i < n), the file's length into host_words[i] (release order) as
+ * soon as out[i] holds the complete file; the caller zeroes the words before
+ * each call and polls them.  The words must stay allocated until turned off
+ * (n = 0). */
+int ric_batch_set_ready(ric_batch* b, uint32_t* host_words, long n);
 /* As ric_batch_roundtrip (device pixels in and out, .ric files to host
  * out[i]): frames [0, n_host) encoded and decoded on the host; frames
  * [n_host, n) encoded by the GPU stream coder and decoded by the GPU stream
@@ -330,6 +347,50 @@ int ric_video_output(ric_video* v, int16_t* planes, int border, int on_device);
  * vectors in quarter pel, x in the low 16 bits, y in the high 16, MV_INTRA =
  * 0x80008000 (COBMC::pMV, obmc.h:29-57) */
 int ric_video_motion(ric_video* v, uint32_t* mv);
+
+/* ------------------------------------------------------- device memory */
+/* HBM buffers from this library's own HIP runtime (no reference counterpart:
+ * the reference is host-only).  Callers that have no HIP runtime of their own
+ * (the ctypes binding, the tests, the benchmark) use these, so only this
+ * library's runtime is ever mapped into the process.  Copies are synchronous. */
+#define RIC_COPY_H2D 1
+#define RIC_COPY_D2H 2
+#define RIC_COPY_D2D 3
+int ric_device_alloc(int device, size_t bytes, void** out);   /* RIC_E_CAPACITY when HBM is exhausted */
+int ric_device_free(void* p);
+int ric_device_copy(int device, void* dst, const void* src, size_t bytes, int kind);
+int ric_device_memset(int device, void* p, int value, size_t bytes);
+int ric_device_sync(int device);
+/* pinned (page-locked) host memory */
+int ric_host_alloc(size_t bytes, void** out);
+int ric_host_free(void* p);
+/* the 64-bit digest of ric_batch_set_digests over n device byte runs
+ * base + off[i], len[i] bytes each (position 0 = the run's first byte), to
+ * host_out[i] */
+int ric_device_digests(int device, const uint8_t* base, int n, const size_t* off, const size_t* len,
+                       unsigned long long* host_out);
+
+/* ------------------------------------------------------------ ric_comm */
+/* The path's one exchange across GPUs: the .ric streams
+ * of every rank gathered to rank 0, over RCCL (xGMI).  One communicator per
+ * process (one process per GPU).  No reference counterpart: the reference
+ * writes one file per image (src/ric/ric.cpp:174-176).  The chunked gather
+ * protocol runs on the host (shard.py StreamGather) over these primitives. */
+typedef struct ric_comm ric_comm;
+#define RIC_COMM_ID_BYTES 128
+#define RIC_RED_SUM 0
+#define RIC_RED_MAX 1
+#define RIC_RED_MIN 2
+/* rank 0 makes the id; every rank passes the same bytes to ric_comm_create */
+int ric_comm_unique_id(uint8_t* id, size_t len);
+int ric_comm_create(ric_comm** out, const uint8_t* id, int nranks, int rank, int device);
+void ric_comm_destroy(ric_comm* c);
+/* all-reduce of n host doubles in place (op RIC_RED_*); also the barrier */
+int ric_comm_allreduce_f64(ric_comm* c, double* vals, int n, int op);
+/* one group of point-to-point operations, completed before return: op i sends
+ * (is_send[i]) or receives bytes[i] bytes of DEVICE buffer buf[i] to / from
+ * rank peer[i]; sends and receives between two ranks match in issue order */
+int ric_comm_sendrecv(ric_comm* c, int nops, const int* peer, const int* is_send, void* const* buf, const size_t* bytes);
 
 /* .ric header fields (src/ric/ric.cpp:114-121, 187-200) */
 int ric_read_header(const uint8_t* ric, size_t len, int* w, int* h, int* channels, int* q, int* trans);

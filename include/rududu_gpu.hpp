@@ -18,12 +18,13 @@
 //
 // What differs, and why:
 //   * the pyramid lives in GPU memory.  CBand::pBand converts (C-style cast,
-//     `(short*) band.pBand`) to a pointer into a host mirror of the band, with
-//     row stride DimXAlign, synced from the device on that conversion; writes
-//     through it are what the next GPU operation on the pyramid reads.  The
-//     pointer is valid until the next CWavelet2D call.
-//   * DimXAlign is this pyramid's row pitch (64 samples), not the reference's
-//     32-byte rounding: it is the stride of pBand, as in the reference.
+//     `(short*) band.pBand`) to a pointer into a host copy of the band in the
+//     reference's layout -- row stride DimXAlign = DimX rounded up to 32 bytes
+//     (CBand::Init, src/lib/band.cpp:57) -- synced from the device on that
+//     conversion (ric_band_host_ref); writes through it are what the next GPU
+//     operation on the pyramid reads.  The pointer stays the band's (stable);
+//     its contents are current after the conversion and after CodeBand /
+//     DecodeBand, not after a device-side band operation (convert again).
 //   * every failure (HIP error, no GPU, stream capacity) throws
 //     rududu::RicError: there is no CPU fallback.
 //   * the sub-level CWavelet2D objects of the pLow chain are views of the one
@@ -155,8 +156,8 @@ public:
 	{
 		if (!w_) return nullptr;
 		void* p = nullptr;
-		int pitch = 0;
-		ric_check(ric_band_host(w_, index_, &p, &pitch), "CBand::pBand");
+		int stride = 0;
+		ric_check(ric_band_host_ref(w_, index_, &p, &stride), "CBand::pBand");
 		return (T*)p;
 	}
 	explicit operator bool() const { return w_ != nullptr; }
@@ -369,8 +370,9 @@ private:
 		float wt;
 		ric_check(ric_band_info(w_, index, &dx, &dy, &isint, &wt), "band_info");
 		b.DimX = dx; b.DimY = dy; b.type = isint ? sint : sshort; b.Weight = wt;
-		b.DimXAlign = (dx + 63) / 64 * 64;
-		if (b.DimXAlign == 0) b.DimXAlign = 64;
+		// CBand::Init (src/lib/band.cpp:57): DimX * sample size rounded up to ALIGN (32) bytes
+		const int ss = isint ? 4 : 2;
+		b.DimXAlign = (unsigned int)(((dx * ss + 31) & -32) / ss);
 		b.BandSize = b.DimXAlign * dy;
 		b.pBand.w_ = w_;
 		b.pBand.index_ = index;
@@ -553,6 +555,10 @@ public:
 		const int rc = ric_video_decode(v_, pBuffer, 0, &size);
 		if (rc != RIC_OK && rc != RIC_E_STREAM) ric_check(rc, "CRududuCodec::decode");
 		if (outImage) *outImage = sync_out();
+		// a stream that ran past its end (the reference has no error channel and
+		// returns garbage silently): the frame is still decoded and *outImage set,
+		// then the caller is told
+		if (rc == RIC_E_STREAM) throw RicError(rc, "CRududuCodec::decode: the decoder ran past the end of the stream");
 		return size;
 	}
 	ric_video* handle() { return v_; }

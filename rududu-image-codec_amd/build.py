@@ -56,7 +56,8 @@ def build(jobs=8, verbose=False):
     if os.path.exists(OUT) and os.path.getmtime(OUT) >= max(os.path.getmtime(o) for o in objs):
         _build_cli()
         return OUT
-    cmd = [os.path.join(ROCM, "bin", "hipcc"), "--offload-arch=" + ARCH, "-shared", "-fPIC"] + objs + ["-o", OUT]
+    cmd = [os.path.join(ROCM, "bin", "hipcc"), "--offload-arch=" + ARCH, "-shared", "-fPIC"] + objs + [
+        "-L" + os.path.join(ROCM, "lib"), "-lrccl", "-Wl,-rpath," + os.path.join(ROCM, "lib"), "-o", OUT]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError("link failed: %s\n%s" % (" ".join(cmd), r.stderr))

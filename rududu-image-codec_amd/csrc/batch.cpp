@@ -185,6 +185,10 @@ struct ric_batch {
 	// ric_batch_set_digests: per frame of a call, the digest of its decoded pixels
 	unsigned long long* digest = nullptr;
 	long ndigest = 0;
+	// ric_batch_set_ready: per frame of a call, its .ric file's length once the
+	// file is complete in out[i] (host words the caller polls)
+	uint32_t* ready = nullptr;
+	long nready = 0;
 	int device = 0, w = 0, h = 0, channels = 1, slots = 0;
 	double hyb_host_ms = 0, hyb_gpu_ms = 0;        // last hybrid call: when each side finished (ms from entry)
 	Pyramid P;
@@ -228,6 +232,7 @@ struct ric_batch {
 		uint32_t* h_post = nullptr;
 		uint32_t* d_post = nullptr;
 		uint32_t* d_yield = nullptr;               // raised while the batch stream runs host frames' level kernels
+		uint32_t epoch = 0;                        // the last coder launch's tag (posted words, k_gc_*)
 	} cp;
 
 	int nslot() const { return 2 * slots; }
@@ -256,6 +261,30 @@ int gc_prio()
 
 int set_dev(int device) { return bfail(hipSetDevice(device), "hipSetDevice") ? RIC_E_HIP : RIC_OK; }
 
+// The coder's yield flag (coder_yield, gcoder.hip) raised around a run of
+// level kernels: lowered on every path out, errors included (a flag left up
+// would make the coder waves sleep at every chunk until the next call)
+struct YieldFlag {
+	uint32_t* f;
+	hipStream_t st;
+	bool up = false;
+	YieldFlag(uint32_t* flag, hipStream_t s) : f(flag), st(s) {}
+	int raise()
+	{
+		if (!f || up) return RIC_OK;
+		if (launch_gc_flag(f, 1, st)) return RIC_E_HIP;
+		up = true;
+		return RIC_OK;
+	}
+	int lower()
+	{
+		if (!f || !up) return RIC_OK;
+		up = false;
+		return launch_gc_flag(f, 0, st) ? RIC_E_HIP : RIC_OK;
+	}
+	~YieldFlag() { (void)lower(); }
+};
+
 int quant_of(int q, int p) { return q ? quants(q + 20 + (p ? 8 : 0)) : 0; }    // Y, then chroma +C_Q_BOOST (ric.cpp:164-168)
 int lambda_of(int q, int p) { return q ? quants(q + 13 + (p ? 8 : 0)) : 0; }
 
@@ -271,7 +300,8 @@ int lambda_of(int q, int p) { return q ? quants(q + 13 + (p ? 8 : 0)) : 0; }
 int gpu_encode_plane(ric_batch* b, int set, int n, int p, const uint8_t* const* pix, int q, int trans, bool d2h = true,
                      int abase = -1, int amul = 1, uint32_t* yflag = nullptr)
 {
-	if (yflag && launch_gc_flag(yflag, 1, b->st)) return RIC_E_HIP;
+	YieldFlag yf(yflag, b->st);
+	if (yf.raise()) return RIC_E_HIP;
 	Pyramid& P = b->P;
 	const int s0 = set * b->slots;
 	if (abase < 0) abase = s0;
@@ -332,7 +362,7 @@ int gpu_encode_plane(ric_batch* b, int set, int n, int p, const uint8_t* const* 
 				launch_blocks_level(P, l, !fused[l], l + 1 < P.nlev && !fused[l + 1], ar, b->st);
 	}
 	BCHK(hipGetLastError());
-	if (yflag && launch_gc_flag(yflag, 0, b->st)) return RIC_E_HIP;
+	if (yf.lower()) return RIC_E_HIP;
 	if (!d2h) return RIC_OK;
 	if (abase != s0 || amul != 1) return RIC_E_ARG;      // the host mirrors follow the slots
 	if (b->compact) {
@@ -412,7 +442,8 @@ int gpu_decode_plane(ric_batch* b, int set, int n, int p, const int* qs, int tra
 		b->prof.end(sp);
 	}
 	P.set_weight(trans);
-	if (yflag && launch_gc_flag(yflag, 1, b->st)) return RIC_E_HIP;      // (after the copies)
+	YieldFlag yf(yflag, b->st);
+	if (yf.raise()) return RIC_E_HIP;                                    // (after the copies)
 	std::vector<int> qf(4 * n);
 	for (int l = P.nlev - 1; l >= 0; l--) {
 		const Level& L = P.L[l];
@@ -439,7 +470,7 @@ int gpu_decode_plane(ric_batch* b, int set, int n, int p, const int* qs, int tra
 		if (launch_inv_level_z(L, L.b[BL], fr, out_int, trans, qf.data(), b->zi[set][l], b->st)) return RIC_E_HIP;
 		b->prof.end(si);
 	}
-	if (yflag && launch_gc_flag(yflag, 0, b->st)) return RIC_E_HIP;
+	if (yf.lower()) return RIC_E_HIP;
 	BCHK(hipGetLastError());
 	return RIC_OK;
 }
@@ -452,13 +483,15 @@ int gpu_pix_out(ric_batch* b, int set, int n, const int* qs, uint8_t* const* pix
 	const int s0 = set * b->slots;
 	auto sp = b->prof.begin(B_PIXOUT, n, b->st);
 	const size_t npix = (size_t)b->w * b->h * b->channels;
-	const bool dig = b->digest && idx0 >= 0 && idx0 + n <= b->ndigest;
-	if (dig) BCHK(hipMemsetAsync(b->digest + idx0, 0, sizeof(unsigned long long) * n, b->st));
+	// every frame of the group below ndigest gets its digest (a group may
+	// straddle the limit)
+	const long ndig = b->digest && idx0 >= 0 ? std::max(0L, std::min((long)n, b->ndigest - idx0)) : 0;
+	if (ndig) BCHK(hipMemsetAsync(b->digest + idx0, 0, sizeof(unsigned long long) * ndig, b->st));
 	for (int i = 0; i < n; i++) {
 		if (!pix_out[i]) continue;
 		uint8_t* dst = on_device ? pix_out[i] : b->stage(s0 + i);
 		launch_pix_out(b->plane(s0 + i, 0), b->pitch, b->w, b->h, b->channels, qs[i], dst, nullptr, b->st);
-		if (dig) launch_digest(dst, npix, b->digest + idx0 + i, b->st);
+		if (i < ndig) launch_digest(dst, npix, b->digest + idx0 + i, b->st);
 	}
 	b->prof.end(sp);
 	BCHK(hipGetLastError());
@@ -588,6 +621,12 @@ bool outputs_distinct(uint8_t* const* out, int n)
 	std::vector<uint8_t*> v(out, out + n);
 	std::sort(v.begin(), v.end());
 	return std::adjacent_find(v.begin(), v.end()) == v.end();
+}
+
+// frame f's .ric file is complete in its host buffer (ric_batch_set_ready)
+void mark_ready(ric_batch* b, long f, size_t len)
+{
+	if (b->ready && f < b->nready) __atomic_store_n(b->ready + f, (uint32_t)len, __ATOMIC_RELEASE);
 }
 
 int check_header(ric_batch* b, const uint8_t* ric, size_t len, int* q, int* trans)
@@ -833,6 +872,7 @@ int ric_batch_roundtrip(ric_batch* b, const uint8_t* const* pix, int n, int q, i
 			const int f0 = g * S, m = std::min(S, n - f0);
 			int rc = ric_batch_encode(b, pix + f0, m, 1, q, trans, out + f0, cap + f0, len + f0);
 			if (rc) return rc;
+			for (int i = 0; i < m; i++) mark_ready(b, f0 + i, len[f0 + i]);
 			std::vector<const uint8_t*> rics(out + f0, out + f0 + m);
 			// the group's digests are frames f0.. of this call
 			unsigned long long* const dg = b->digest;
@@ -867,6 +907,7 @@ int ric_batch_roundtrip(ric_batch* b, const uint8_t* const* pix, int n, int q, i
 			b->pool->submit([=, &ev, &err, &done] {
 				int r1 = bfail(hipEventSynchronize(ev[g]), "hipEventSynchronize") ? RIC_E_HIP : RIC_OK;
 				if (!r1) r1 = host_encode_plane(b, slot, 0, q, trans, out[f], cap[f], &len[f]);
+				if (!r1) mark_ready(b, f, len[f]);
 				if (!r1) r1 = host_decode_plane(b, slot, 0, out[f], len[f]);
 				err[g].put(r1);
 				done[g].done();
@@ -1066,6 +1107,14 @@ int ric_batch_set_digests(ric_batch* b, unsigned long long* dev_digests, long n)
 	return RIC_OK;
 }
 
+int ric_batch_set_ready(ric_batch* b, uint32_t* host_words, long n)
+{
+	if (!b || n < 0 || (n > 0 && !host_words)) return RIC_E_ARG;
+	b->ready = n ? host_words : nullptr;
+	b->nready = n;
+	return RIC_OK;
+}
+
 int ric_batch_hybrid_config(ric_batch* b, int pool_frames, size_t stream_cap)
 {
 	if (!b || pool_frames < 1 || pool_frames > 65536 || stream_cap < 64 || (stream_cap & 15) || stream_cap > 0xFFFFFFF0u)
@@ -1098,22 +1147,40 @@ int ric_batch_hybrid_config(ric_batch* b, int pool_frames, size_t stream_cap)
 		               " frames: " + hipGetErrorString(e));
 		return e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation ? RIC_E_CAPACITY : RIC_E_HIP;
 	}
-	// the coder kernels write their result words straight into host memory: a
-	// copy queued behind a coder kernel on its stream held up the batch
-	// stream's own copies until the kernel ended (seconds)
-	BCHK(hipHostMalloc(&c.h_res, sizeof(uint32_t) * 6 * c.n, hipHostMallocMapped | hipHostMallocCoherent));
-	BCHK(hipHostGetDevicePointer((void**)&c.d_res, c.h_res, 0));
-	BCHK(hipHostMalloc(&c.h_post, sizeof(uint32_t) * 4 * c.n, hipHostMallocCoherent | hipHostMallocMapped));
-	BCHK(hipHostGetDevicePointer((void**)&c.d_post, c.h_post, 0));
-	if (!c.d_args) BCHK(hipMalloc(&c.d_args, 3 * sizeof(GEncArgs)));   // the halves, then both as one launch
-	if (!c.d_dargs) BCHK(hipMalloc(&c.d_dargs, 3 * sizeof(GDecArgs)));
-	for (int h = 0; h < 2; h++) {
-		if (!c.st[h]) BCHK(hipStreamCreateWithFlags(&c.st[h], hipStreamNonBlocking));
-		if (!c.ev_fwd[h]) BCHK(hipEventCreateWithFlags(&c.ev_fwd[h], hipEventDisableTiming));
-		if (!c.ev_done[h]) BCHK(hipEventCreateWithFlags(&c.ev_done[h], hipEventDisableTiming));
-		if (!c.ev_enc[h]) BCHK(hipEventCreateWithFlags(&c.ev_enc[h], hipEventDisableTiming));
+	// the rest; on any failure the pool is released again (a half-configured
+	// pool would let ric_batch_roundtrip_hybrid launch coder kernels that post
+	// through null result pointers)
+	auto rest = [&]() -> int {
+		// the coder kernels write their result words straight into host memory: a
+		// copy queued behind a coder kernel on its stream held up the batch
+		// stream's own copies until the kernel ended (seconds)
+		BCHK(hipHostMalloc(&c.h_res, sizeof(uint32_t) * 6 * c.n, hipHostMallocMapped | hipHostMallocCoherent));
+		BCHK(hipHostGetDevicePointer((void**)&c.d_res, c.h_res, 0));
+		BCHK(hipHostMalloc(&c.h_post, sizeof(uint32_t) * 4 * c.n, hipHostMallocCoherent | hipHostMallocMapped));
+		BCHK(hipHostGetDevicePointer((void**)&c.d_post, c.h_post, 0));
+		memset(c.h_post, 0, sizeof(uint32_t) * 4 * c.n);
+		if (!c.d_args) BCHK(hipMalloc(&c.d_args, 3 * sizeof(GEncArgs)));   // the halves, then both as one launch
+		if (!c.d_dargs) BCHK(hipMalloc(&c.d_dargs, 3 * sizeof(GDecArgs)));
+		for (int h = 0; h < 2; h++) {
+			if (!c.st[h]) BCHK(hipStreamCreateWithFlags(&c.st[h], hipStreamNonBlocking));
+			if (!c.ev_fwd[h]) BCHK(hipEventCreateWithFlags(&c.ev_fwd[h], hipEventDisableTiming));
+			if (!c.ev_done[h]) BCHK(hipEventCreateWithFlags(&c.ev_done[h], hipEventDisableTiming));
+			if (!c.ev_enc[h]) BCHK(hipEventCreateWithFlags(&c.ev_enc[h], hipEventDisableTiming));
+		}
+		return RIC_OK;
+	};
+	const int rc = rest();
+	if (rc) {
+		(void)hipFree(c.d_ab);
+		(void)hipFree(c.d_out);
+		c.d_ab = nullptr;
+		c.d_out = nullptr;
+		if (c.h_res) (void)hipHostFree(c.h_res);
+		if (c.h_post) (void)hipHostFree(c.h_post);
+		c.h_res = c.d_res = c.h_post = c.d_post = nullptr;
+		c.n = 0;
 	}
-	return RIC_OK;
+	return rc;
 }
 
 namespace {
@@ -1135,7 +1202,7 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 	    trans < 0 || trans > 2)
 		return RIC_E_ARG;
 	if (b->channels != 1) return RIC_E_ARG;
-	if (n_host < n && !b->cp.d_ab) return RIC_E_ARG;    // ric_batch_hybrid_config first
+	if (n_host < n && (!b->cp.d_ab || !b->cp.h_res || !b->cp.d_post)) return RIC_E_ARG;    // ric_batch_hybrid_config first
 	if (n == 0) return RIC_OK;
 	if (!outputs_distinct(out, n))
 		return set_last_error("ric_batch_roundtrip_hybrid: out[] buffers must be distinct"), RIC_E_ARG;
@@ -1237,7 +1304,13 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 	// (1: k_gc_roundtrip, each wave goes on to decode its stream as soon as it
 	// is encoded)
 	static const bool fuse = [] { const char* e = getenv("RIC_GC_FUSE"); return !e || atoi(e) != 0; }();
-	bool fused = false;                                     // this call's first two batches ran as k_gc_roundtrip
+	// each coder launch's tag (launch_gc_encode): its posted result words carry it
+	std::vector<uint32_t> tagj(nbatch > 0 ? nbatch : 1, 0);
+	auto next_tag = [&]() {
+		c.epoch = (c.epoch + 1) & 0xFFFFFu;
+		if (!c.epoch) c.epoch = 1;
+		return c.epoch;
+	};
 	// batch j's coder launches are done: (host decode) its decode groups become
 	// ready; (gpu_decode) its frames go through the inverse levels right away
 	// A GPU-decoded batch's .ric files leave for the host as soon as its encode
@@ -1249,35 +1322,32 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 	auto copy_out = [&](int j) {
 		if (copier[j].joinable()) return;                          // (fused: started at the kick)
 		const int f0 = batch_f0(j), m = batch_m(j), h = j & 1;
-		const uint32_t* re = c.h_res + res_enc(h);
+		// the launch posts each stream's result once the stream is in HBM, tagged
+		// with the launch's tag (k_gc_encode / k_gc_roundtrip): a word is this
+		// launch's only if it carries the tag, whatever an earlier launch left
 		const uint32_t* po = c.h_post + res_enc(h);
-		const bool poll = fused && j < 2;                      // (batches 2.. take per-half launches)
-		hipEvent_t done = c.ev_done[h];
+		const uint32_t want = 0x100u | tagj[j] << 12;
+		hipEvent_t done = c.ev_enc[h];                         // the encoding kernel's end
 		copier[j] = std::thread([=, &copy_rc, &c] {
 			int r = set_dev(b->device);
 			for (int k = 0; k < m && !r; k++) {
-				uint32_t len_k, st_k;
-				if (poll) {
-					// the kernel posts each stream once it is in HBM; the kernel's
-					// end (normal or not) stops the wait
-					while (!((st_k = __atomic_load_n(po + 2 * k + 1, __ATOMIC_ACQUIRE)) & 0x100u)) {
-						if (hipEventQuery(done) != hipErrorNotReady) {
-							st_k = __atomic_load_n(po + 2 * k + 1, __ATOMIC_ACQUIRE);
-							break;
-						}
-						std::this_thread::sleep_for(std::chrono::microseconds(500));
+				uint32_t st_k;
+				// the kernel's end (normal or not) stops the wait
+				while (((st_k = __atomic_load_n(po + 2 * k + 1, __ATOMIC_ACQUIRE)) & ~0xFFu) != want) {
+					if (hipEventQuery(done) != hipErrorNotReady) {
+						st_k = __atomic_load_n(po + 2 * k + 1, __ATOMIC_ACQUIRE);
+						break;
 					}
-					if (!(st_k & 0x100u)) break;                         // harvest reports it
-					len_k = __atomic_load_n(po + 2 * k, __ATOMIC_RELAXED);
-					st_k &= 0xFFu;
-				} else {
-					len_k = re[2 * k];
-					st_k = re[2 * k + 1];
+					std::this_thread::sleep_for(std::chrono::microseconds(500));
 				}
-				if (st_k || len_k > cap[f0 + k]) break;   // harvest reports it
+				if ((st_k & ~0xFFu) != want) break;                  // harvest reports it
+				const uint32_t len_k = __atomic_load_n(po + 2 * k, __ATOMIC_RELAXED);
+				if ((st_k & 0xFFu) || len_k > cap[f0 + k]) break;   // harvest reports it
 				if (bfail(hipMemcpy(out[f0 + k], c.d_out + ((size_t)h * c.n + k) * c.ocap, len_k, hipMemcpyDeviceToHost),
 				          "hipMemcpy stream"))
 					r = RIC_E_HIP;
+				else
+					mark_ready(b, f0 + k, len_k);
 			}
 			copy_rc[j] = r;
 		});
@@ -1304,8 +1374,10 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 		const int m = batch_m(j), h = j & 1;
 		BCHK(hipStreamWaitEvent(c.st[h], c.ev_fwd[h], 0));
 		if (wait_other) BCHK(hipStreamWaitEvent(c.st[h], c.ev_fwd[h ^ 1], 0));
+		tagj[j] = next_tag();
 		auto sp = b->prof.begin(B_GENC, m, c.st[h]);
-		if (launch_gc_encode(c.d_args + h, m, q == 0, c.st[h])) return bfail(hipGetLastError(), "k_gc_encode") ? RIC_E_HIP : RIC_E_HIP;
+		if (launch_gc_encode(c.d_args + h, m, q == 0, c.st[h], c.d_post + res_enc(h), tagj[j]))
+			return bfail(hipGetLastError(), "k_gc_encode") ? RIC_E_HIP : RIC_E_HIP;
 		b->prof.end(sp);
 		BCHK(hipEventRecord(c.ev_enc[h], c.st[h]));
 		if (gpu_decode == 1) bgpu[j] = 1;
@@ -1341,14 +1413,12 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 		const int m = batch_m(0) + batch_m(1);
 		BCHK(hipStreamWaitEvent(c.st[0], c.ev_fwd[0], 0));
 		BCHK(hipStreamWaitEvent(c.st[0], c.ev_fwd[1], 0));
+		tagj[0] = tagj[1] = next_tag();
 		if (fuse && q != 0) {
 			// one kernel: each wave encodes its frame, posts the stream (the
 			// copiers take it from there at once) and decodes it
-			for (size_t i = 0; i < 4 * (size_t)c.n; i++) __atomic_store_n(c.h_post + i, 0u, __ATOMIC_RELAXED);
-			__atomic_thread_fence(__ATOMIC_SEQ_CST);
-			fused = true;
 			auto sp = b->prof.begin(B_GRT, m, c.st[0]);
-			if (launch_gc_roundtrip(c.d_args + 2, c.d_dargs + 2, c.d_post, m, c.st[0]))
+			if (launch_gc_roundtrip(c.d_args + 2, c.d_dargs + 2, c.d_post, tagj[0], m, c.st[0]))
 				return bfail(hipGetLastError(), "k_gc_roundtrip") ? RIC_E_HIP : RIC_E_HIP;
 			b->prof.end(sp);
 			for (int j = 0; j < 2; j++) {
@@ -1363,7 +1433,8 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 			return RIC_OK;
 		}
 		auto sp = b->prof.begin(B_GENC, m, c.st[0]);
-		if (launch_gc_encode(c.d_args + 2, m, q == 0, c.st[0])) return bfail(hipGetLastError(), "k_gc_encode") ? RIC_E_HIP : RIC_E_HIP;
+		if (launch_gc_encode(c.d_args + 2, m, q == 0, c.st[0], c.d_post, tagj[0]))
+			return bfail(hipGetLastError(), "k_gc_encode") ? RIC_E_HIP : RIC_E_HIP;
 		b->prof.end(sp);
 		BCHK(hipEventRecord(c.ev_enc[0], c.st[0]));
 		BCHK(hipEventRecord(c.ev_enc[1], c.st[0]));
@@ -1522,6 +1593,7 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 					int r1 = bfail(hipEventSynchronize(pf->ev), "hipEventSynchronize") ? RIC_E_HIP : RIC_OK;
 					if (trace > 2 && i == 0) tr("  task: forward passed", f);
 					if (!r1) r1 = host_encode_plane(b, slot, 0, q, trans, out[f], cap[f], &len[f]);
+					if (!r1) mark_ready(b, f, len[f]);
 					if (!r1) r1 = host_decode_plane(b, slot, 0, out[f], len[f]);
 					pf->err.put(r1);
 					pf->done.done();
@@ -1535,6 +1607,7 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 					int r1 = set_dev(b->device);
 					if (!r1) r1 = bfail(hipMemcpy(out[f], src, len[f], hipMemcpyDeviceToHost), "hipMemcpy stream") ? RIC_E_HIP
 					                                                                                            : RIC_OK;
+					if (!r1) mark_ready(b, f, len[f]);
 					cl->done();
 					// the set's mirrors: the previous group's H2D from them has passed
 					if (!r1) r1 = bfail(hipEventSynchronize(pf->ev), "hipEventSynchronize") ? RIC_E_HIP : RIC_OK;

@@ -105,6 +105,12 @@ struct ric_wavelet {
 	// a device block and its pinned mirror, allocated with the arena
 	char* d_small = nullptr;
 	char* h_small = nullptr;
+	// ric_band_host_ref: bands handed out in the reference's layout (row stride
+	// DimXAlign: DimX rounded up to 32 bytes, src/lib/band.cpp:57), each a
+	// stable host buffer; active ones are written back into the mirror before
+	// the mirror goes to the device, and refreshed when the mirror is rewritten
+	std::vector<std::vector<char>> ref_buf;
+	std::vector<char> ref_active;
 };
 
 struct ric_mux {
@@ -148,6 +154,29 @@ int take_status(ric_wavelet* w, bool in_copy)
 	return RIC_E_HIP;
 }
 
+// the reference's row stride of band B in samples (CBand::Init, src/lib/band.cpp:57, ALIGN 32)
+int ref_stride(const Band& B)
+{
+	const int ss = B.is_int ? 4 : 2;
+	return ((B.dx * ss + 31) & ~31) / ss;
+}
+
+// active reference-layout views <-> the host mirror (rows of dx samples)
+void ref_copy(ric_wavelet* w, bool to_mirror)
+{
+	for (size_t i = 0; i < w->ref_active.size(); i++) {
+		if (!w->ref_active[i]) continue;
+		const Band& B = w->P.band((int)i);
+		const size_t ss = B.is_int ? 4 : 2, rs = (size_t)ref_stride(B) * ss, ms = (size_t)B.pitch * ss;
+		char* m = w->h_arena + B.off;
+		char* r = w->ref_buf[i].data();
+		for (int y = 0; y < B.dy; y++) {
+			if (to_mirror) memcpy(m + y * ms, r + y * rs, (size_t)B.dx * ss);
+			else memcpy(r + y * rs, m + y * ms, (size_t)B.dx * ss);
+		}
+	}
+}
+
 // region A (+ B with records): see Pyramid in ric_types.h
 int to_host(ric_wavelet* w, bool records = false)
 {
@@ -163,6 +192,7 @@ int to_host(ric_wavelet* w, bool records = false)
 int to_device(ric_wavelet* w)
 {
 	if (!w->host_valid) return RIC_OK;
+	ref_copy(w, true);            // what the caller wrote through reference-layout pBand views
 	const size_t lo = 0, hi = w->P.a_end;
 	w->prof.begin(S_H2D, w->st);
 	HIPCHK(hipMemcpyAsync(w->d_arena + lo, w->h_arena + lo, hi - lo, hipMemcpyHostToDevice, w->st));
@@ -371,6 +401,7 @@ int code_band_host(ric_wavelet* w, Mux& m, bool copy = true, bool state = false)
 	// the host mirror is now the reference: CodeBand's final state with
 	// `state`, else buildTree's (the codec path never reads it back)
 	w->host_valid = true;
+	ref_copy(w, false);
 	return RIC_OK;
 }
 
@@ -392,6 +423,7 @@ int decode_band(ric_wavelet* w, Mux& m)
 	}
 	w->prof.host(S_HDEC, now_ms() - t0);
 	w->host_valid = true;
+	ref_copy(w, false);
 	return m.overflow() ? RIC_E_STREAM : RIC_OK;
 }
 
@@ -863,6 +895,8 @@ int ric_band_read(ric_wavelet* w, int index, int32_t* out)
 	if (!w->host_valid) {
 		HIPCHK(hipMemcpyAsync(w->h_arena + B.off, w->d_arena + B.off, B.bytes(), hipMemcpyDeviceToHost, w->st));
 		HIPCHK(hipStreamSynchronize(w->st));
+	} else {
+		ref_copy(w, true);
 	}
 	for (int y = 0; y < B.dy; y++)
 		for (int x = 0; x < B.dx; x++) {
@@ -881,10 +915,40 @@ int ric_band_host(ric_wavelet* w, int index, void** ptr, int* pitch)
 		int rc = to_host(w, false);
 		if (rc) return rc;
 		w->host_valid = true;   // the mirror is authoritative until the next GPU stage
+		ref_copy(w, false);
+	} else {
+		ref_copy(w, true);
 	}
 	const Band& B = w->P.band(index);
 	*ptr = w->h_arena + B.off;
 	if (pitch) *pitch = B.pitch;
+	return RIC_OK;
+}
+
+int ric_band_host_ref(ric_wavelet* w, int index, void** ptr, int* stride)
+{
+	if (!w || !ptr || index < 0 || index >= w->P.nbands()) return RIC_E_ARG;
+	if (set_dev(w->device)) return RIC_E_HIP;
+	if (flush_pending(w)) return RIC_E_HIP;
+	if ((int)w->ref_buf.size() < w->P.nbands()) {
+		w->ref_buf.resize(w->P.nbands());
+		w->ref_active.resize(w->P.nbands(), 0);
+	}
+	if (!w->host_valid) {
+		int rc = to_host(w, false);
+		if (rc) return rc;
+		w->host_valid = true;
+	} else {
+		ref_copy(w, true);              // other views' writes first
+	}
+	const Band& B = w->P.band(index);
+	const int rs = ref_stride(B);
+	auto& buf = w->ref_buf[index];
+	if (buf.empty()) buf.assign((size_t)rs * B.dy * (B.is_int ? 4 : 2) + 32, 0);
+	w->ref_active[index] = 1;
+	ref_copy(w, false);
+	*ptr = buf.data();
+	if (stride) *stride = rs;
 	return RIC_OK;
 }
 

@@ -1,0 +1,228 @@
+// device.cpp -- device memory and the stream gather's transport (include/ric_gpu.h).
+//
+// Device memory: callers (the Python binding, the tests, bench.py, the CLI)
+// get HBM buffers from the product's own HIP runtime, so no second runtime
+// (e.g. one bundled with a framework) is ever mapped into the process beside
+// it.
+//
+// ric_comm: the path's one exchange -- the .ric streams of
+// every rank to rank 0 -- over RCCL (xGMI between the GPUs of a node), one
+// communicator per process, point-to-point send / receive of device buffers.
+// The chunked gather protocol itself (which streams go in which round) is
+// host logic in shard.py, shared with the CPU (gloo) transport of the tests.
+// The reference has no multi-process path (src/ric/ric.cpp:174-176 writes one
+// file per image); this is the drop-in's scale-out.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "ric_gpu.h"
+#include "codec_params.h"
+#include "ric_image.h"
+
+using namespace ric;
+
+namespace {
+
+bool dfail(hipError_t e, const char* what)
+{
+	if (e == hipSuccess) return false;
+	set_last_error(std::string(what) + ": " + hipGetErrorString(e));
+	(void)hipGetLastError();
+	return true;
+}
+#define DCHK(x) do { if (dfail((x), #x)) return RIC_E_HIP; } while (0)
+
+bool nfail(ncclResult_t r, const char* what)
+{
+	if (r == ncclSuccess) return false;
+	set_last_error(std::string(what) + ": " + ncclGetErrorString(r));
+	return true;
+}
+#define NCHK(x) do { if (nfail((x), #x)) return RIC_E_HIP; } while (0)
+
+int on_device(int device)
+{
+	int n = 0;
+	if (hipGetDeviceCount(&n) != hipSuccess || n < 1) return set_last_error("no HIP device visible"), RIC_E_HIP;
+	if (device < 0 || device >= n) return RIC_E_ARG;
+	DCHK(hipSetDevice(device));
+	return RIC_OK;
+}
+
+}  // namespace
+
+struct ric_comm {
+	ncclComm_t comm = nullptr;
+	hipStream_t st = nullptr;
+	int device = 0, nranks = 1, rank = 0;
+	double* d_red = nullptr;                        // allreduce scratch
+	int red_n = 0;
+};
+
+extern "C" {
+
+int ric_device_alloc(int device, size_t bytes, void** out)
+{
+	if (!out) return RIC_E_ARG;
+	*out = nullptr;
+	if (int rc = on_device(device)) return rc;
+	if (bytes == 0) bytes = 16;
+	const hipError_t e = hipMalloc(out, bytes);
+	if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) {
+		(void)hipGetLastError();
+		set_last_error("hipMalloc: out of device memory (" + std::to_string(bytes) + " bytes)");
+		*out = nullptr;
+		return RIC_E_CAPACITY;
+	}
+	DCHK(e);
+	return RIC_OK;
+}
+
+int ric_device_free(void* p)
+{
+	if (p) DCHK(hipFree(p));
+	return RIC_OK;
+}
+
+int ric_host_alloc(size_t bytes, void** out)
+{
+	if (!out) return RIC_E_ARG;
+	*out = nullptr;
+	DCHK(hipHostMalloc(out, bytes ? bytes : 16, 0));
+	return RIC_OK;
+}
+
+int ric_host_free(void* p)
+{
+	if (p) DCHK(hipHostFree(p));
+	return RIC_OK;
+}
+
+int ric_device_copy(int device, void* dst, const void* src, size_t bytes, int kind)
+{
+	if ((!dst || !src) && bytes) return RIC_E_ARG;
+	if (kind != RIC_COPY_H2D && kind != RIC_COPY_D2H && kind != RIC_COPY_D2D) return RIC_E_ARG;
+	if (!bytes) return RIC_OK;
+	if (int rc = on_device(device)) return rc;
+	const hipMemcpyKind k = kind == RIC_COPY_H2D ? hipMemcpyHostToDevice
+	                        : kind == RIC_COPY_D2H ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
+	DCHK(hipMemcpy(dst, src, bytes, k));
+	return RIC_OK;
+}
+
+int ric_device_memset(int device, void* p, int value, size_t bytes)
+{
+	if (!p && bytes) return RIC_E_ARG;
+	if (!bytes) return RIC_OK;
+	if (int rc = on_device(device)) return rc;
+	DCHK(hipMemset(p, value, bytes));
+	return RIC_OK;
+}
+
+int ric_device_sync(int device)
+{
+	if (int rc = on_device(device)) return rc;
+	DCHK(hipDeviceSynchronize());
+	return RIC_OK;
+}
+
+int ric_device_digests(int device, const uint8_t* base, int n, const size_t* off, const size_t* len,
+                       unsigned long long* host_out)
+{
+	if (n < 0 || (n && (!base || !off || !len || !host_out))) return RIC_E_ARG;
+	if (!n) return RIC_OK;
+	if (int rc = on_device(device)) return rc;
+	unsigned long long* d = nullptr;
+	DCHK(hipMalloc(&d, sizeof(unsigned long long) * (size_t)n));
+	int rc = RIC_OK;
+	if (dfail(hipMemset(d, 0, sizeof(unsigned long long) * (size_t)n), "hipMemset")) rc = RIC_E_HIP;
+	for (int i = 0; i < n && !rc; i++) launch_digest(base + off[i], len[i], d + i, nullptr);
+	if (!rc && dfail(hipGetLastError(), "k_digest")) rc = RIC_E_HIP;
+	if (!rc && dfail(hipMemcpy(host_out, d, sizeof(unsigned long long) * (size_t)n, hipMemcpyDeviceToHost), "hipMemcpy"))
+		rc = RIC_E_HIP;
+	(void)hipFree(d);
+	return rc;
+}
+
+// ------------------------------------------------------------------ ric_comm
+int ric_comm_unique_id(uint8_t* id, size_t len)
+{
+	if (!id || len < NCCL_UNIQUE_ID_BYTES) return RIC_E_ARG;
+	ncclUniqueId u;
+	NCHK(ncclGetUniqueId(&u));
+	memcpy(id, u.internal, NCCL_UNIQUE_ID_BYTES);
+	return RIC_OK;
+}
+
+int ric_comm_create(ric_comm** out, const uint8_t* id, int nranks, int rank, int device)
+{
+	if (!out || !id || nranks < 1 || rank < 0 || rank >= nranks) return RIC_E_ARG;
+	*out = nullptr;
+	if (int rc = on_device(device)) return rc;
+	ric_comm* c = new ric_comm;
+	c->device = device; c->nranks = nranks; c->rank = rank;
+	ncclUniqueId u;
+	memcpy(u.internal, id, NCCL_UNIQUE_ID_BYTES);
+	if (dfail(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking), "hipStreamCreate") ||
+	    nfail(ncclCommInitRank(&c->comm, nranks, u, rank), "ncclCommInitRank")) {
+		ric_comm_destroy(c);
+		return RIC_E_HIP;
+	}
+	*out = c;
+	return RIC_OK;
+}
+
+void ric_comm_destroy(ric_comm* c)
+{
+	if (!c) return;
+	(void)hipSetDevice(c->device);
+	if (c->st) (void)hipStreamSynchronize(c->st);
+	if (c->comm) (void)ncclCommDestroy(c->comm);
+	if (c->d_red) (void)hipFree(c->d_red);
+	if (c->st) (void)hipStreamDestroy(c->st);
+	delete c;
+}
+
+int ric_comm_allreduce_f64(ric_comm* c, double* vals, int n, int op)
+{
+	if (!c || !vals || n < 1 || op < 0 || op > 2) return RIC_E_ARG;
+	DCHK(hipSetDevice(c->device));
+	if (c->red_n < n) {
+		if (c->d_red) DCHK(hipFree(c->d_red));
+		c->d_red = nullptr;
+		DCHK(hipMalloc(&c->d_red, sizeof(double) * (size_t)n));
+		c->red_n = n;
+	}
+	DCHK(hipMemcpyAsync(c->d_red, vals, sizeof(double) * (size_t)n, hipMemcpyHostToDevice, c->st));
+	const ncclRedOp_t o = op == RIC_RED_SUM ? ncclSum : op == RIC_RED_MAX ? ncclMax : ncclMin;
+	NCHK(ncclAllReduce(c->d_red, c->d_red, (size_t)n, ncclFloat64, o, c->comm, c->st));
+	DCHK(hipMemcpyAsync(vals, c->d_red, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost, c->st));
+	DCHK(hipStreamSynchronize(c->st));
+	return RIC_OK;
+}
+
+int ric_comm_sendrecv(ric_comm* c, int nops, const int* peer, const int* is_send, void* const* buf, const size_t* bytes)
+{
+	if (!c || nops < 0 || (nops && (!peer || !is_send || !buf || !bytes))) return RIC_E_ARG;
+	for (int i = 0; i < nops; i++)
+		if (peer[i] < 0 || peer[i] >= c->nranks || (bytes[i] && !buf[i])) return RIC_E_ARG;
+	if (!nops) return RIC_OK;
+	DCHK(hipSetDevice(c->device));
+	NCHK(ncclGroupStart());
+	ncclResult_t r = ncclSuccess;
+	for (int i = 0; i < nops && r == ncclSuccess; i++) {
+		if (!bytes[i]) continue;
+		r = is_send[i] ? ncclSend(buf[i], bytes[i], ncclUint8, peer[i], c->comm, c->st)
+		               : ncclRecv(buf[i], bytes[i], ncclUint8, peer[i], c->comm, c->st);
+	}
+	const ncclResult_t r2 = ncclGroupEnd();
+	if (nfail(r, "ncclSend/ncclRecv") || nfail(r2, "ncclGroupEnd")) return RIC_E_HIP;
+	DCHK(hipStreamSynchronize(c->st));
+	return RIC_OK;
+}
+
+}  // extern "C"

@@ -76,13 +76,17 @@ const uint32_t* gc_enum16_table(hipStream_t st);
 // k_gc_encode over n frames: the whole .ric file of each (gray, one plane).
 // dev_args: the argument block in device memory.
 // lossless: q == 0 (the 8 KiB byte ring; lossy streams take a 4 KiB one).
-int launch_gc_encode(const GEncArgs* dev_args, int nframes, int lossless, hipStream_t st);
+// posted (or null): each frame's result as soon as its stream is in HBM,
+// host-visible: posted[2 f] = the coder's end offset, posted[2 f + 1] = status |
+// 0x100 | (tag & 0xFFFFF) << 12 -- the caller accepts only its launch's tag.
+int launch_gc_encode(const GEncArgs* dev_args, int nframes, int lossless, hipStream_t st, uint32_t* posted = nullptr,
+                     uint32_t tag = 0);
 
 // k_gc_roundtrip over n lossy frames: each wave encodes its frame (as
-// k_gc_encode), posts the stream's end offset and status | 0x100 to
-// posted[2 f], posted[2 f + 1] (host-visible memory, written once the stream is
-// in HBM), then decodes it (as k_gc_decode, lens from the encoder).
-int launch_gc_roundtrip(const GEncArgs* dev_eargs, const GDecArgs* dev_dargs, uint32_t* posted, int nframes, hipStream_t st);
+// k_gc_encode), posts its result tagged as launch_gc_encode does, then decodes
+// the stream (as k_gc_decode, lens from the encoder).
+int launch_gc_roundtrip(const GEncArgs* dev_eargs, const GDecArgs* dev_dargs, uint32_t* posted, uint32_t tag, int nframes,
+                        hipStream_t st);
 
 // Fill the band descriptors (coding order) of a pyramid.
 inline void gc_bands(const Pyramid& P, GBandDesc& ll, GBandDesc* b, int& nb)

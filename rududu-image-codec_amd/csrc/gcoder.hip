@@ -628,8 +628,25 @@ GC_DI uint32_t enc_frame(const GEncArgs& a, int f, uint32_t& end_out)
 	return rc;
 }
 
+// The posted result of frame f (host-visible memory the caller polls while
+// the launch runs): posted[2 f] = the coder's end offset, posted[2 f + 1] =
+// status | 0x100 | tag << 12.  The tag is the launch's (a 20-bit counter the
+// caller keeps): a word left from an earlier launch over the same frames never
+// carries it, so the caller needs no reset between launches.  The stream's
+// stores reach memory (system scope: the host's copy engine reads it) before
+// the words that announce it.
+GC_DI void post_result(uint32_t* posted, uint32_t tag, int f, uint32_t rc, uint32_t end)
+{
+	if (!posted) return;
+	__threadfence_system();
+	if (lane_id() == 0) {
+		__hip_atomic_store(posted + 2 * f, rc ? 0u : end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+		__hip_atomic_store(posted + 2 * f + 1, rc | 0x100u | tag << 12, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+	}
+}
+
 template <uint32_t RING>
-__global__ void __launch_bounds__(64) k_gc_encode(const GEncArgs* __restrict__ ap)
+__global__ void __launch_bounds__(64) k_gc_encode(const GEncArgs* __restrict__ ap, uint32_t* posted, uint32_t tag)
 {
 	const GEncArgs& a = *ap;
 	const int f = blockIdx.x;
@@ -643,6 +660,7 @@ __global__ void __launch_bounds__(64) k_gc_encode(const GEncArgs* __restrict__ a
 		gst(a.res)[2 * f + 1] = rc;
 		if (a.ts) ts_put(a.ts, f, t_start);
 	}
+	post_result(posted, tag, f, rc, end);
 }
 
 
@@ -1313,7 +1331,7 @@ __global__ void __launch_bounds__(64) k_gc_decode(const GDecArgs* __restrict__ a
 // k_gc_decode write.  A stream that failed is not decoded (result word 0).
 template <bool ETAB>
 __global__ void __launch_bounds__(64) k_gc_roundtrip(const GEncArgs* __restrict__ eap, const GDecArgs* __restrict__ dap,
-                                                    uint32_t* posted)
+                                                    uint32_t* posted, uint32_t tag)
 {
 	const GEncArgs& ea = *eap;
 	const GDecArgs& da = *dap;
@@ -1323,17 +1341,13 @@ __global__ void __launch_bounds__(64) k_gc_roundtrip(const GEncArgs* __restrict_
 	load_huff();
 	uint32_t end;
 	const uint32_t rc = enc_frame<4096>(ea, f, end);
-	// the stream's stores reach memory (system scope: the host's copy engine
-	// reads it) before the words that announce it; the acquire half lets this
-	// wave's decoder read them back
-	__threadfence_system();
 	if (lane_id() == 0) {
 		gst(ea.res)[2 * f] = rc ? 0u : end;
 		gst(ea.res)[2 * f + 1] = rc;
 		if (ea.ts) ts_put(ea.ts, f, t_start);
-		__hip_atomic_store(posted + 2 * f, rc ? 0u : end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-		__hip_atomic_store(posted + 2 * f + 1, rc | 0x100u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 	}
+	post_result(posted, tag, f, rc, end);
+	// (the fence in post_result also lets this wave's decoder read the stream back)
 	__threadfence();
 	const uint64_t t_dec = __builtin_amdgcn_s_memrealtime();
 	if (da.prio == 1) set_prio<1>(1);
@@ -1359,15 +1373,15 @@ static size_t gc_dyn_lds(const void* kernel)
 	return (size_t)want > fa.sharedSizeBytes ? (size_t)want - fa.sharedSizeBytes : 0;
 }
 
-int launch_gc_encode(const GEncArgs* dev_args, int nframes, int lossless, hipStream_t st)
+int launch_gc_encode(const GEncArgs* dev_args, int nframes, int lossless, hipStream_t st, uint32_t* posted, uint32_t tag)
 {
 	if (nframes <= 0) return 0;
 	if (lossless) {
 		static const size_t dyn = gc_dyn_lds((const void*)k_gc_encode<8192>);
-		hipLaunchKernelGGL(k_gc_encode<8192>, dim3(nframes), dim3(64), dyn, st, dev_args);
+		hipLaunchKernelGGL(k_gc_encode<8192>, dim3(nframes), dim3(64), dyn, st, dev_args, posted, tag & 0xFFFFFu);
 	} else {
 		static const size_t dyn = gc_dyn_lds((const void*)k_gc_encode<4096>);
-		hipLaunchKernelGGL(k_gc_encode<4096>, dim3(nframes), dim3(64), dyn, st, dev_args);
+		hipLaunchKernelGGL(k_gc_encode<4096>, dim3(nframes), dim3(64), dyn, st, dev_args, posted, tag & 0xFFFFFu);
 	}
 	return hipGetLastError() == hipSuccess ? 0 : -1;
 }
@@ -1429,11 +1443,20 @@ int launch_gc_flag(uint32_t* flag, uint32_t v, hipStream_t st)
 	return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_gc_roundtrip(const GEncArgs* dev_eargs, const GDecArgs* dev_dargs, uint32_t* posted, int nframes, hipStream_t st)
+int launch_gc_roundtrip(const GEncArgs* dev_eargs, const GDecArgs* dev_dargs, uint32_t* posted, uint32_t tag, int nframes,
+                        hipStream_t st)
 {
 	if (nframes <= 0) return 0;
-	if (enum16_upload(st)) return -1;
-	hipLaunchKernelGGL(k_gc_roundtrip<true>, dim3(nframes), dim3(64), 0, st, dev_eargs, dev_dargs, posted);
+	// RIC_GC_ETAB=0 and RIC_GC_LDS act here as in the separate launches
+	static const bool etab = [] { const char* e = getenv("RIC_GC_ETAB"); return !e || atoi(e) != 0; }();
+	if (etab) {
+		if (enum16_upload(st)) return -1;
+		static const size_t dyn = gc_dyn_lds((const void*)k_gc_roundtrip<true>);
+		hipLaunchKernelGGL(k_gc_roundtrip<true>, dim3(nframes), dim3(64), dyn, st, dev_eargs, dev_dargs, posted, tag & 0xFFFFFu);
+	} else {
+		static const size_t dyn = gc_dyn_lds((const void*)k_gc_roundtrip<false>);
+		hipLaunchKernelGGL(k_gc_roundtrip<false>, dim3(nframes), dim3(64), dyn, st, dev_eargs, dev_dargs, posted, tag & 0xFFFFFu);
+	}
 	return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

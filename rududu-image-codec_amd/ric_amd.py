@@ -7,8 +7,9 @@ Names follow the reference: ``Wavelet2D`` ~ CWavelet2D (src/lib/wavelet2d.h),
 
 This module is plumbing for tests and the benchmark; the product is the HIP
 library.  Loading fails loudly when the library is missing -- there is no CPU
-fallback.  Device buffers are passed as raw pointers (e.g. a torch tensor's
-``data_ptr()``); host buffers as numpy arrays.
+fallback.  Device buffers are DeviceArray objects (HBM allocated by the
+library's own HIP runtime, ric_device_alloc) or raw pointers; host buffers are
+numpy arrays.
 """
 import ctypes
 import os
@@ -69,6 +70,7 @@ def lib():
         "ric_band_read": (_I, [_P, _I, _P]),
         "ric_band_write": (_I, [_P, _I, _P]),
         "ric_band_host": (_I, [_P, _I, ctypes.POINTER(_P), ctypes.POINTER(_I)]),
+        "ric_band_host_ref": (_I, [_P, _I, ctypes.POINTER(_P), ctypes.POINTER(_I)]),
         "ric_mux_create_decoder_inplace": (_I, [ctypes.POINTER(_P), _P]),
         "ric_mux_reinit_encoder": (_I, [_P, _P, _S, ctypes.c_uint16]),
         "ric_mux_reinit_decoder": (_I, [_P, _P, _S]),
@@ -115,6 +117,20 @@ def lib():
         "ric_video_decode": (_I, [_P, _P, _S, ctypes.POINTER(_I)]),
         "ric_video_output": (_I, [_P, _P, _I, _I]),
         "ric_video_motion": (_I, [_P, _P]),
+        "ric_device_alloc": (_I, [_I, _S, ctypes.POINTER(_P)]),
+        "ric_device_free": (_I, [_P]),
+        "ric_host_alloc": (_I, [_S, ctypes.POINTER(_P)]),
+        "ric_host_free": (_I, [_P]),
+        "ric_device_copy": (_I, [_I, _P, _P, _S, _I]),
+        "ric_device_memset": (_I, [_I, _P, _I, _S]),
+        "ric_device_sync": (_I, [_I]),
+        "ric_device_digests": (_I, [_I, _P, _I, _P, _P, _P]),
+        "ric_comm_unique_id": (_I, [_P, _S]),
+        "ric_comm_create": (_I, [ctypes.POINTER(_P), _P, _I, _I, _I]),
+        "ric_comm_destroy": (None, [_P]),
+        "ric_comm_allreduce_f64": (_I, [_P, _P, _I, _I]),
+        "ric_comm_sendrecv": (_I, [_P, _I, _P, _P, _P, _P]),
+        "ric_batch_set_ready": (_I, [_P, _P, ctypes.c_long]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -163,6 +179,140 @@ def synth(w, h, channels=1, frame=0):
     out = np.empty((channels, h, w), np.uint8)
     lib().ric_synth_image(w, h, channels, frame, out.ctypes.data)
     return out
+
+
+RIC_COPY_H2D, RIC_COPY_D2H, RIC_COPY_D2D = 1, 2, 3
+RIC_RED_SUM, RIC_RED_MAX, RIC_RED_MIN = 0, 1, 2
+
+
+class DeviceArray:
+    """An HBM buffer allocated by the library's own HIP runtime
+    (ric_device_alloc), with a shape and a numpy dtype.  data_ptr() is what the
+    C-ABI takes; numpy() reads it back.  The plumbing for callers with no HIP
+    runtime of their own: only the library's runtime is ever mapped."""
+
+    def __init__(self, shape, dtype=np.uint8, device=0, zero=False):
+        self.shape = tuple(int(s) for s in shape) if hasattr(shape, "__len__") else (int(shape),)
+        self.dtype = np.dtype(dtype)
+        self.device = device
+        self.nbytes = int(np.prod(self.shape, dtype=np.int64)) * self.dtype.itemsize
+        p = _P()
+        _chk(lib().ric_device_alloc(device, self.nbytes, ctypes.byref(p)), "ric_device_alloc(%d bytes)" % self.nbytes)
+        self._p = p.value
+        if zero:
+            self.zero()
+
+    @classmethod
+    def from_numpy(cls, a, device=0):
+        a = np.ascontiguousarray(a)
+        d = cls(a.shape, a.dtype, device)
+        d.copy_from(a)
+        return d
+
+    def empty_like(self):
+        return DeviceArray(self.shape, self.dtype, self.device)
+
+    def zeros_like(self):
+        return DeviceArray(self.shape, self.dtype, self.device, zero=True)
+
+    def data_ptr(self):
+        return self._p
+
+    def copy_from(self, a):
+        a = np.ascontiguousarray(a, self.dtype)
+        if a.nbytes != self.nbytes:
+            raise ValueError("size mismatch: %d vs %d bytes" % (a.nbytes, self.nbytes))
+        _chk(lib().ric_device_copy(self.device, self._p, a.ctypes.data, self.nbytes, RIC_COPY_H2D), "H2D copy")
+
+    def numpy(self):
+        out = np.empty(self.shape, self.dtype)
+        _chk(lib().ric_device_copy(self.device, out.ctypes.data, self._p, self.nbytes, RIC_COPY_D2H), "D2H copy")
+        return out
+
+    def zero(self):
+        _chk(lib().ric_device_memset(self.device, self._p, 0, self.nbytes), "memset")
+
+    def __del__(self):
+        p = getattr(self, "_p", None)
+        if p and _lib is not None:
+            _lib.ric_device_free(p)
+            self._p = None
+
+
+class _Pinned:
+    def __init__(self, n):
+        p = _P()
+        _chk(lib().ric_host_alloc(n, ctypes.byref(p)), "ric_host_alloc")
+        self.p = p.value
+
+    def __del__(self):
+        if getattr(self, "p", None) and _lib is not None:
+            _lib.ric_host_free(self.p)
+            self.p = None
+
+
+def pinned_array(n):
+    """A uint8 numpy array of n bytes in pinned host memory (ric_host_alloc),
+    freed with the array."""
+    holder = _Pinned(n)
+    buf = (ctypes.c_uint8 * n).from_address(holder.p)
+    a = np.frombuffer(buf, np.uint8)
+    a_base = a.base                    # the ctypes buffer; keep the holder alive with it
+    a_base._holder = holder
+    return a
+
+
+def device_sync(device=0):
+    _chk(lib().ric_device_sync(device), "ric_device_sync")
+
+
+def device_digests(device, base, offs, lens):
+    """ric_device_digests: the 64-bit digest (ric_batch_set_digests' formula) of
+    each device byte run base + offs[i], lens[i] bytes."""
+    n = len(offs)
+    o = np.ascontiguousarray(offs, np.uint64)
+    ln = np.ascontiguousarray(lens, np.uint64)
+    out = np.zeros(n, np.uint64)
+    if n:
+        _chk(lib().ric_device_digests(device, _ptr(base), n, o.ctypes.data, ln.ctypes.data, out.ctypes.data),
+             "ric_device_digests")
+    return out
+
+
+class Comm:
+    """ric_comm: one RCCL communicator of this process (one process per GPU)."""
+    ID_BYTES = 128
+
+    @staticmethod
+    def unique_id():
+        b = np.zeros(Comm.ID_BYTES, np.uint8)
+        _chk(lib().ric_comm_unique_id(b.ctypes.data, b.size), "ric_comm_unique_id")
+        return b.tobytes()
+
+    def __init__(self, uid, nranks, rank, device=0):
+        b = np.frombuffer(uid, np.uint8).copy()
+        h = _P()
+        _chk(lib().ric_comm_create(ctypes.byref(h), b.ctypes.data, nranks, rank, device), "ric_comm_create")
+        self.h, self.nranks, self.rank, self.device = h, nranks, rank, device
+
+    def allreduce(self, vals, op=RIC_RED_SUM):
+        v = np.ascontiguousarray(vals, np.float64).copy()
+        _chk(lib().ric_comm_allreduce_f64(self.h, v.ctypes.data, v.size, op), "ric_comm_allreduce_f64")
+        return v
+
+    def sendrecv(self, ops):
+        """ops: [(peer, is_send, device buffer or pointer, nbytes)] as one group."""
+        n = len(ops)
+        peer = (ctypes.c_int * n)(*[o[0] for o in ops])
+        snd = (ctypes.c_int * n)(*[int(bool(o[1])) for o in ops])
+        bufs = (ctypes.c_void_p * n)(*[_ptr(o[2]) for o in ops])
+        nb = (ctypes.c_size_t * n)(*[int(o[3]) for o in ops])
+        _chk(lib().ric_comm_sendrecv(self.h, n, peer, snd, bufs, nb), "ric_comm_sendrecv")
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.ric_comm_destroy(self.h)
+            self.h = None
 
 
 def _prof_enable(handle, on):
@@ -443,8 +593,19 @@ class Batch:
 
     def set_digests(self, dev_digests, n):
         """Per frame of the next calls, the 64-bit digest of its decoded pixels
-        into dev_digests[i] (a device int64 tensor / pointer; n = 0: off)."""
+        into dev_digests[i] (a device uint64 DeviceArray / pointer; n = 0: off).
+        The buffer is kept referenced here while the library holds its pointer."""
         _chk(lib().ric_batch_set_digests(self.h, _ptr(dev_digests) if n else None, n), "ric_batch_set_digests")
+        self._digests = dev_digests if n else None
+
+    def set_ready(self, words, n):
+        """ric_batch_set_ready: words (a uint32 numpy array) gets frame i's
+        .ric length as soon as its file is complete (n = 0: off); kept
+        referenced here while the library holds its pointer."""
+        if n and (not isinstance(words, np.ndarray) or words.dtype != np.uint32 or words.size < n):
+            raise ValueError("set_ready: a uint32 numpy array of at least n words")
+        _chk(lib().ric_batch_set_ready(self.h, words.ctypes.data if n else None, n), "ric_batch_set_ready")
+        self._ready = words if n else None
 
     def hybrid_config(self, pool_frames, stream_cap):
         """Pool of the GPU stream coder (ric_batch_hybrid_config)."""

@@ -1,12 +1,15 @@
 """Frame / tile sharding across GPUs and the gather of compressed .ric streams
 (SURVEY.md §8(e)).
 
-Independent frames (C5) and tiles (C4) are independent .ric streams, so ranks
-share no state while coding: frame f goes to rank f mod N, tile (tx, ty) of a
-2x2 grid to rank 2*ty + tx.  The only exchange is the final gather of the
-variable-size compressed streams to rank 0: an all_gather of the stream sizes
-(int64), then a gather of the size-padded payloads to rank 0 (RCCL over xGMI
-with the "nccl" backend on GPUs, gloo on CPU).
+Independent frames (C3, C5) and tiles (C4) are independent .ric streams, so
+ranks share no state while coding: frame f goes to rank f mod N, tile (tx, ty)
+of a 2x2 grid to rank 2*ty + tx.  The only exchange is the gather of the
+variable-size compressed streams to rank 0 (StreamGather): every stream a rank
+codes, shipped in bounded chunks while the step still runs (a stream leaves as
+soon as its .ric file is complete), so rank 0 holds at most one chunk per peer
+whatever the step's size.  Transports: RCCL over xGMI between the GPUs
+(RcclTransport: the library's own communicator, device buffers) and gloo on
+the CPU (GlooTransport: the tests and the one-GPU rehearsals).
 
 Tile container ("RTL1", our extension -- the reference has no tile syntax):
   "RTL1" | u16 W | u16 H | u8 nx | u8 ny | nx*ny u32 LE stream sizes |
@@ -69,88 +72,261 @@ def unpack_tiles(blob):
     return W, H, nx, ny, streams
 
 
-def gather_streams(local, dist, device=None, to_host=True):
-    """All ranks pass their list of byte streams; rank 0 gets every rank's
-    list (in rank order), other ranks get None.  Two collectives: sizes, then
-    the padded payloads.  to_host=False: rank 0 gets (payload tensors, size
-    tensors) per rank as they arrived on `device` (size tensor = [n, len...])."""
-    import torch
-    world = dist.get_world_size()
-    rank = dist.get_rank()
-    dev = device if device is not None else torch.device("cpu")
-    n_local = len(local)
-    counts = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
-    dist.all_gather(counts, torch.tensor([n_local], dtype=torch.int64, device=dev))
-    maxn = max(int(c[0]) for c in counts)
-    sz = torch.zeros(maxn + 1, dtype=torch.int64, device=dev)
-    sz[0] = n_local
-    if n_local:
-        sz[1:n_local + 1] = torch.tensor([len(x) for x in local], dtype=torch.int64, device=dev)
-    all_sz = [torch.zeros_like(sz) for _ in range(world)]
-    dist.all_gather(all_sz, sz)
-    total = max(int(t[1:].sum()) for t in all_sz)
-    buf = torch.zeros(max(total, 1), dtype=torch.uint8, device=dev)
-    if n_local:
-        payload = np.frombuffer(b"".join(local), np.uint8)
-        buf[:payload.size] = torch.from_numpy(payload.copy()).to(dev)
-    # payloads go to rank 0 only (a gather, not an all_gather: the other
-    # ranks never need them)
-    all_buf = [torch.zeros_like(buf) for _ in range(world)] if rank == 0 else None
-    dist.gather(buf, gather_list=all_buf, dst=0)
+MAX_PER_CHUNK = 64          # streams per chunk (the header's capacity)
+HDR_WORDS = 4 + 3 * MAX_PER_CHUNK
+_DMUL = np.uint64(0x9E3779B97F4A7C15)
+
+
+def digest_bytes(a):
+    """The 64-bit digest of ric_batch_set_digests / ric_device_digests over a
+    byte run: sum over byte k of a[k] * (k * 0x9E3779B97F4A7C15 + 1) mod 2^64."""
+    a = np.frombuffer(a, np.uint8) if not isinstance(a, np.ndarray) else a.reshape(-1)
+    if a.size == 0:
+        return np.uint64(0)
+    v = a.astype(np.uint64)
+    with np.errstate(over="ignore"):
+        s1 = np.uint64(np.sum(v, dtype=np.uint64))
+        s2 = np.uint64(np.dot(v, np.arange(a.size, dtype=np.uint64)))
+        return np.uint64(s2 * _DMUL + s1)
+
+
+class GlooTransport:
+    """The gather's CPU transport: torch.distributed (gloo) point-to-point on
+    host buffers (numpy uint8 arrays)."""
+
+    def __init__(self, dist):
+        self.dist = dist
+
+    def alloc(self, nbytes):
+        return np.zeros(max(int(nbytes), 16), np.uint8)
+
+    def put(self, buf, off, data):
+        src = np.frombuffer(data, np.uint8) if not isinstance(data, np.ndarray) else data.reshape(-1)
+        buf[off:off + src.size] = src
+
+    def get(self, buf, off, n):
+        return buf[off:off + n]
+
+    def sendrecv(self, ops):
+        import torch
+        reqs = []
+        for peer, is_send, buf, n in ops:
+            if not n:
+                continue
+            t = torch.from_numpy(buf[:n])
+            reqs.append(self.dist.isend(t, peer) if is_send else self.dist.irecv(t, peer))
+        for r in reqs:
+            r.wait()
+
+    def digests(self, buf, offs, lens):
+        return np.array([digest_bytes(buf[o:o + n]) for o, n in zip(offs, lens)], np.uint64)
+
+
+class RcclTransport:
+    """The gather's GPU transport: the library's RCCL communicator (ric_comm,
+    xGMI between the GPUs of a node) on device buffers; streams are staged
+    from their host buffers into a device chunk, digested on the device."""
+
+    def __init__(self, comm, device=0):
+        import ric_amd
+        self.R = ric_amd
+        self.comm = comm
+        self.device = device
+        self._pinned = None
+
+    def alloc(self, nbytes):
+        return self.R.DeviceArray(max(int(nbytes), 16), np.uint8, self.device)
+
+    def put(self, buf, off, data):
+        src = np.frombuffer(data, np.uint8) if not isinstance(data, np.ndarray) else data.reshape(-1)
+        if src.size:
+            self.R._chk(self.R.lib().ric_device_copy(self.device, buf.data_ptr() + off, src.ctypes.data, src.size,
+                                                     self.R.RIC_COPY_H2D), "gather H2D")
+
+    def get(self, buf, off, n):
+        # into one pinned sink buffer, reused every round (rank 0 holds no more)
+        if self._pinned is None or self._pinned.size < n:
+            self._pinned = self.R.pinned_array(max(n, 1 << 20))
+        if n:
+            self.R._chk(self.R.lib().ric_device_copy(self.device, self._pinned.ctypes.data, buf.data_ptr() + off, n,
+                                                     self.R.RIC_COPY_D2H), "gather D2H")
+        return self._pinned[:n]
+
+    def sendrecv(self, ops):
+        self.comm.sendrecv([(p, s, b, n) for p, s, b, n in ops if n])
+
+    def digests(self, buf, offs, lens):
+        return self.R.device_digests(self.device, buf.data_ptr(), list(offs), list(lens))
+
+
+class StreamGather:
+    """The gather of every rank's .ric streams to rank 0, in bounded chunks.
+
+    A round: every sender still active sends one chunk -- a header (round,
+    count, done, payload bytes, then per stream: its index, length and
+    digest) and the payload (whole streams back to back at 16-byte offsets,
+    at most `chunk_bytes`, at most MAX_PER_CHUNK streams) -- and rank 0
+    receives them all, checks each stream's digest against the sender's, and
+    hands each stream to `on_stream(rank, index, bytes)` from its sink buffer.
+    A sender takes into a chunk the streams that are ready (any order) and
+    waits only when none is; its last chunk carries `done`.  Rank 0's memory:
+    one chunk buffer per peer on the transport, whatever the number of streams.
+    """
+
+    def __init__(self, transport, rank, world, chunk_bytes=64 << 20):
+        self.t = transport
+        self.rank, self.world = rank, world
+        self.chunk = int(chunk_bytes)
+        self.hdr = [self.t.alloc(HDR_WORDS * 8) for _ in range(max(world - 1, 1))]
+        if rank == 0:
+            self.bufs = [self.t.alloc(self.chunk) for _ in range(world - 1)]
+        else:
+            self.bufs = [self.t.alloc(self.chunk)]
+        self.stats = {}
+
+    # ---- sender
+    def send(self, n, words, data, poll_s=0.0005, stop=None):
+        """Ship streams 0..n-1 of this rank.  words: a uint32 array whose
+        word i becomes stream i's length once it is ready (ric_batch_set_ready;
+        0 until then); data(i, length) -> its bytes (host).  stop(): an
+        optional check that raises when the producer failed."""
+        import time
+        pending = np.ones(n, bool)
+        left = n
+        rnd = sent = nbytes = 0
+        hdr = np.zeros(HDR_WORDS, np.int64)
+        while True:
+            take, offs, off = [], [], 0
+            while True:
+                cand = np.flatnonzero(pending & (words[:n] != 0)) if left else []
+                for i in cand[:MAX_PER_CHUNK]:
+                    ln = int(words[i])
+                    if ln > self.chunk:
+                        raise ValueError("stream %d (%d bytes) larger than the gather chunk (%d)" % (i, ln, self.chunk))
+                    o = (off + 15) & ~15
+                    if o + ln > self.chunk:
+                        break
+                    take.append((int(i), ln))
+                    offs.append(o)
+                    off = o + ln
+                if take or not left:
+                    break
+                if stop is not None:
+                    stop()
+                time.sleep(poll_s)
+            for i, _ in take:
+                pending[i] = False
+            left -= len(take)
+            for (i, ln), o in zip(take, offs):
+                self.t.put(self.bufs[0], o, data(i, ln))
+            dg = np.asarray(self.t.digests(self.bufs[0], offs, [ln for _, ln in take]), np.uint64)
+            hdr[:] = 0
+            hdr[0], hdr[1], hdr[2], hdr[3] = rnd, len(take), int(left == 0), off
+            for k, (i, ln) in enumerate(take):
+                hdr[4 + 3 * k], hdr[5 + 3 * k] = i, ln
+            hdr[6:6 + 3 * len(take):3] = dg.view(np.int64)
+            self.t.put(self.hdr[0], 0, hdr.view(np.uint8))
+            self.t.sendrecv([(0, True, self.hdr[0], HDR_WORDS * 8)])
+            self.t.sendrecv([(0, True, self.bufs[0], off)])
+            sent += len(take)
+            nbytes += off
+            rnd += 1
+            if not left:
+                break
+        self.stats = {"rounds": rnd, "streams": sent, "bytes": nbytes}
+        return self.stats
+
+    # ---- rank 0
+    def receive(self, on_stream=None, to_host=True):
+        """Receive every peer's streams; returns per-rank counts and bytes and
+        the digest mismatches.  to_host: every chunk also lands in the
+        transport's host sink (where a server would write the files out)."""
+        active = list(range(1, self.world))
+        counts = [0] * self.world
+        nbytes = [0] * self.world
+        bad = []
+        rnd = 0
+        while active:
+            self.t.sendrecv([(r, False, self.hdr[r - 1], HDR_WORDS * 8) for r in active])
+            heads = {}
+            for r in active:
+                h = np.frombuffer(bytes(self.t.get(self.hdr[r - 1], 0, HDR_WORDS * 8)), np.int64).copy()
+                if h[0] != rnd or h[1] > MAX_PER_CHUNK or h[3] > self.chunk:
+                    raise RuntimeError("gather: bad chunk header from rank %d (round %d): %s" % (r, rnd, h[:4]))
+                heads[r] = h
+            self.t.sendrecv([(r, False, self.bufs[r - 1], int(heads[r][3])) for r in active])
+            for r in active:
+                h = heads[r]
+                k = int(h[1])
+                idx = h[4:4 + 3 * k:3]
+                ln = h[5:5 + 3 * k:3]
+                want = h[6:6 + 3 * k:3].view(np.uint64)
+                offs, o = [], 0
+                for L in ln:
+                    o = (o + 15) & ~15
+                    offs.append(o)
+                    o += int(L)
+                got = self.t.digests(self.bufs[r - 1], offs, [int(L) for L in ln])
+                for j in range(k):
+                    if got[j] != want[j]:
+                        bad.append((r, int(idx[j])))
+                if k and (on_stream is not None or to_host):
+                    sink = self.t.get(self.bufs[r - 1], 0, int(h[3]))
+                    if on_stream is not None:
+                        for j in range(k):
+                            on_stream(r, int(idx[j]), sink[offs[j]:offs[j] + int(ln[j])])
+                counts[r] += k
+                nbytes[r] += int(h[3])
+            active = [r for r in active if not heads[r][2]]
+            rnd += 1
+        self.stats = {"rounds": rnd, "streams": counts, "bytes": nbytes, "digest_mismatches": bad}
+        return self.stats
+
+
+def gather_streams(local, transport, rank, world, chunk_bytes=1 << 20):
+    """One-shot gather of byte streams (e.g. C4's tiles): rank 0 gets every
+    rank's list in rank order (its own first), others None."""
+    g = StreamGather(transport, rank, world, max(chunk_bytes, max([len(s) for s in local] + [16]) + 16))
     if rank != 0:
+        g.send(len(local), np.array([len(x) for x in local], np.uint32), lambda i, n: local[i])
         return None
-    if not to_host:
-        return all_buf, all_sz
-    out = []
-    for r in range(world):
-        n = int(all_sz[r][0])
-        lens = [int(x) for x in all_sz[r][1:n + 1]]
-        data = all_buf[r].cpu().numpy().tobytes()
-        off, lst = 0, []
-        for L in lens:
-            lst.append(data[off:off + L])
-            off += L
-        out.append(lst)
-    return out
+    got = [dict() for _ in range(world)]
+    g.receive(lambda r, i, b: got[r].__setitem__(i, bytes(b)))
+    if g.stats["digest_mismatches"]:
+        raise RuntimeError("gather: digest mismatches %s" % g.stats["digest_mismatches"][:8])
+    return [list(local)] + [[got[r][i] for i in sorted(got[r])] for r in range(1, world)]
 
 
-def scatter_streams(per_rank, dist, device=None):
+def scatter_streams(per_rank, transport, rank, world):
     """The decode side of gather_streams: rank 0 holds one list of byte
     streams per rank (`per_rank`, ignored elsewhere); every rank gets its own
-    list.  A broadcast of the padded sizes, then two scatters (sizes,
-    payloads) -- RCCL over xGMI with "nccl", gloo on CPU."""
-    import torch
-    world = dist.get_world_size()
-    rank = dist.get_rank()
-    dev = device if device is not None else torch.device("cpu")
-    head = torch.zeros(2, dtype=torch.int64, device=dev)
+    list.  Per peer a header (count, lengths) then the payload, point to point."""
     if rank == 0:
-        head[0] = max(len(x) for x in per_rank)
-        head[1] = max(max(sum(len(s) for s in x) for x in per_rank), 1)
-    dist.broadcast(head, src=0)
-    maxn, maxb = int(head[0]), int(head[1])
-    sz = torch.zeros(maxn + 1, dtype=torch.int64, device=dev)
-    buf = torch.zeros(maxb, dtype=torch.uint8, device=dev)
-    sz_list = buf_list = None
-    if rank == 0:
-        sz_list, buf_list = [], []
-        for lst in per_rank:
-            t = torch.zeros(maxn + 1, dtype=torch.int64)
-            t[0] = len(lst)
-            if lst:
-                t[1:len(lst) + 1] = torch.tensor([len(x) for x in lst], dtype=torch.int64)
-            b = torch.zeros(maxb, dtype=torch.uint8)
-            if lst:
-                payload = np.frombuffer(b"".join(lst), np.uint8)
-                b[:payload.size] = torch.from_numpy(payload.copy())
-            sz_list.append(t.to(dev))
-            buf_list.append(b.to(dev))
-    dist.scatter(sz, scatter_list=sz_list, src=0)
-    dist.scatter(buf, scatter_list=buf_list, src=0)
-    n = int(sz[0])
-    data = buf.cpu().numpy().tobytes()
+        for r in range(1, world):
+            lst = per_rank[r]
+            hdr = np.zeros(HDR_WORDS, np.int64)
+            if len(lst) > MAX_PER_CHUNK:
+                raise ValueError("scatter: at most %d streams per rank" % MAX_PER_CHUNK)
+            hdr[0] = len(lst)
+            hdr[1:1 + len(lst)] = [len(x) for x in lst]
+            payload = b"".join(lst)
+            hb = transport.alloc(HDR_WORDS * 8)
+            transport.put(hb, 0, hdr.view(np.uint8))
+            pb = transport.alloc(len(payload))
+            transport.put(pb, 0, payload)
+            transport.sendrecv([(r, True, hb, HDR_WORDS * 8)])
+            transport.sendrecv([(r, True, pb, len(payload))])
+        return list(per_rank[0])
+    hb = transport.alloc(HDR_WORDS * 8)
+    transport.sendrecv([(0, False, hb, HDR_WORDS * 8)])
+    hdr = np.frombuffer(bytes(transport.get(hb, 0, HDR_WORDS * 8)), np.int64)
+    k = int(hdr[0])
+    lens = [int(x) for x in hdr[1:1 + k]]
+    pb = transport.alloc(sum(lens))
+    transport.sendrecv([(0, False, pb, sum(lens))])
+    data = bytes(transport.get(pb, 0, sum(lens)))
     out, off = [], 0
-    for L in (int(x) for x in sz[1:n + 1]):
+    for L in lens:
         out.append(data[off:off + L])
         off += L
     return out

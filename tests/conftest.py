@@ -27,14 +27,8 @@ def gpu_available():
 
 @pytest.fixture(scope="session")
 def ric():
-    # torch (plumbing for device buffers) brings its own HIP runtime: let it
-    # initialise first so both share one runtime instance in this process
-    try:
-        import torch
-        if torch.cuda.is_available():
-            torch.cuda.init()
-    except ImportError:
-        pass
+    # device buffers come from the library itself (ric_amd.DeviceArray): no
+    # other HIP runtime is loaded into the test process
     import ric_amd
     if ric_amd.lib().ric_device_count() < 1:
         pytest.fail("no HIP device visible: the gpu tests must run on an MI355X (no CPU fallback exists)")

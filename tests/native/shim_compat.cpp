@@ -12,6 +12,7 @@
 //                                                  read through (C*) pBand,
 //                                                  canonical order, int32
 //   shim_compat stats W H TRANS in.raw              Transform, then Stats()
+//   shim_compat poke W H TRANS in.raw               writes through pBand reach the device
 #include <cstdio>
 #include <cstring>
 #include <fstream>
@@ -94,12 +95,41 @@ int dec(const char* in, const char* out)
 	return 0;
 }
 
+// the caller recomputes the row stride the reference's way (CBand::Init,
+// src/lib/band.cpp:57: DimX * sizeof(C) rounded up to ALIGN = 32 bytes) and
+// walks pBand with it
+template <class C>
+unsigned int ref_stride(const CBand& b)
+{
+	return (unsigned int)(((b.DimX * sizeof(C) + 31) & ~(size_t)31) / sizeof(C));
+}
+
 template <class C>
 void dump_band(CBand& b, std::vector<int32_t>& out)
 {
+	if (b.DimXAlign != ref_stride<C>(b)) throw RicError(RIC_E_ARG, "DimXAlign is not the reference's");
 	const C* p = (C*)b.pBand;
+	const unsigned int stride = ref_stride<C>(b);
 	for (unsigned int j = 0; j < b.DimY; j++)
-		for (unsigned int i = 0; i < b.DimX; i++) out.push_back(p[j * b.DimXAlign + i]);
+		for (unsigned int i = 0; i < b.DimX; i++) out.push_back(p[j * stride + i]);
+}
+
+// writes through pBand (the reference's stride), then a device operation on
+// the band (CBand::Add(0): the write must reach the device first) and the band
+// read back through pBand: every written sample, in place
+template <class C>
+int poke_band(CBand& b)
+{
+	C* p = (C*)b.pBand;
+	const unsigned int stride = ref_stride<C>(b);
+	for (unsigned int j = 0; j < b.DimY; j++)
+		for (unsigned int i = 0; i < b.DimX; i++) p[j * stride + i] = (C)((int)i * 3 - (int)j * 5 + 7);
+	b.Add<C>(0);
+	const C* q = (C*)b.pBand;
+	for (unsigned int j = 0; j < b.DimY; j++)
+		for (unsigned int i = 0; i < b.DimX; i++)
+			if (q[j * stride + i] != (C)((int)i * 3 - (int)j * 5 + 7)) return 4;
+	return 0;
 }
 
 void dump_any(CBand& b, std::vector<int32_t>& out)
@@ -129,6 +159,18 @@ int bands(int W, int H, int Quant, trans Trans, const char* in, const char* out)
 	return 0;
 }
 
+int poke(int W, int H, trans Trans, const char* in)
+{
+	std::vector<short> img = gray_plane(slurp(in), 9);
+	CWavelet2D Wavelet(W, H, kLevels, kLevels - 4);
+	Wavelet.SetWeight(Trans);
+	Wavelet.Transform(img.data(), W, Trans);
+	CWavelet2D* c = &Wavelet;
+	while (c->pLow) c = c->pLow;
+	if (int r = poke_band<short>(Wavelet.HBand)) return r;      // finest level: short
+	return poke_band<int>(c->VBand);                             // coarsest: int (level_chg)
+}
+
 int stats(int W, int H, trans Trans, const char* in)
 {
 	std::vector<short> img = gray_plane(slurp(in), 9);
@@ -149,6 +191,7 @@ int main(int argc, char** argv)
 		if (mode == "dec" && argc == 4) return dec(argv[2], argv[3]);
 		if (mode == "bands" && argc == 8) return bands(atoi(argv[2]), atoi(argv[3]), atoi(argv[4]), (trans)atoi(argv[5]), argv[6], argv[7]);
 		if (mode == "stats" && argc == 6) return stats(atoi(argv[2]), atoi(argv[3]), (trans)atoi(argv[4]), argv[5]);
+		if (mode == "poke" && argc == 6) return poke(atoi(argv[2]), atoi(argv[3]), (trans)atoi(argv[4]), argv[5]);
 	} catch (const RicError& e) {
 		fprintf(stderr, "%s\n", e.what());
 		return 2;

@@ -140,10 +140,18 @@ def test_shim_reference_call_forms(ric, port, tmp_path, w, h, q, t):
     dec = str(tmp_path / "o.raw")
     subprocess.run([SHIM, "dec", out, dec], check=True, timeout=120)
     assert np.array_equal(np.fromfile(dec, np.uint8).reshape(1, h, w), port.decode_ric(r)[0])
+    # every band read through (C*) pBand with the stride the caller recomputes
+    # the reference's way (DimX rounded up to 32 bytes, band.cpp:57)
     bd = str(tmp_path / "b.i32")
     subprocess.run([SHIM, "bands", str(w), str(h), str(q), str(t), raw, bd], check=True, timeout=120)
     exp = np.concatenate([b.ravel() for b in port.bands(O.gray_plane(pix[0], q), 5, 1, t, 0)])
     assert np.array_equal(np.fromfile(bd, np.int32), exp)
+    ref = O.ref()
+    if ref is not None:
+        assert np.array_equal(np.fromfile(bd, np.int32),
+                              np.concatenate([b.ravel() for b in ref.bands(O.gray_plane(pix[0], q), 5, 1, t, 0)]))
+    # writes through pBand (reference stride) reach the device and read back
+    subprocess.run([SHIM, "poke", str(w), str(h), str(t), raw], check=True, timeout=120)
     # Stats(): the reference's order and arithmetic on the same bands
     st = subprocess.run([SHIM, "stats", str(w), str(h), str(t), raw], check=True, capture_output=True,
                         text=True, timeout=120).stdout.split("\n")

@@ -51,19 +51,17 @@ def test_batch_mixed_q_decode(ric, port):
 
 @pytest.mark.parametrize("slots,n", [(4, 11), (3, 3), (2, 5)])
 def test_batch_roundtrip_pipeline(ric, port, slots, n):
-    torch = pytest.importorskip("torch")
     w, h = 768, 512
     host = [ric.synth(w, h, 1, 40 + i) for i in range(n)]
-    frames = [torch.from_numpy(x).cuda() for x in host]
-    outs = [torch.empty_like(f) for f in frames]
+    frames = [ric.DeviceArray.from_numpy(x) for x in host]
+    outs = [f.empty_like() for f in frames]
     b = ric.Batch(w, h, 1, slots=slots, threads=3)
     b.prof_enable(True)
     b.roundtrip(frames, outs, q=9, trans=0)
-    torch.cuda.synchronize()
     for i in range(n):
         r = b.stream(i)
         assert r == port.encode_ric(host[i], 9, 0)
-        assert np.array_equal(outs[i].cpu().numpy(), port.decode_ric(r)[0])
+        assert np.array_equal(outs[i].numpy(), port.decode_ric(r)[0])
     prof = b.prof_read()
     assert prof["fwd_l0"][1] == n and prof["inv_l0"][1] == n and prof["host_enc"][1] == n
 
@@ -71,19 +69,17 @@ def test_batch_roundtrip_pipeline(ric, port, slots, n):
 def test_batch_full_size_golden(ric):
     """C3 (8K) and C2/C5 (4096^2) frames through the batched pipeline against
     the reference's SHA-256 (frame 0 = C3 / C2, frame 1 = C5 frame 1)."""
-    torch = pytest.importorskip("torch")
     for (W, H, names) in [(7680, 4320, {0: "C3_7680x4320_q9"}),
                           (4096, 4096, {0: "C2_4096x4096_q9", 1: "C5_frame1_4096x4096_q9"})]:
-        frames = [torch.from_numpy(ric.synth(W, H, 1, f)).cuda() for f in range(3)]
-        outs = [torch.empty_like(f) for f in frames]
+        frames = [ric.DeviceArray.from_numpy(ric.synth(W, H, 1, f)) for f in range(3)]
+        outs = [f.empty_like() for f in frames]
         b = ric.Batch(W, H, 1, slots=2, threads=3)
         b.roundtrip(frames, outs, q=9, trans=0)
-        torch.cuda.synchronize()
         for f, nm in names.items():
             e = large(nm)
             r = b.stream(f)
             assert len(r) == e["ric_bytes"] and sha(r) == e["ric_sha256"], nm
-            assert sha(outs[f].cpu().numpy().tobytes()) == e["decoded_sha256"], nm
+            assert sha(outs[f].numpy().tobytes()) == e["decoded_sha256"], nm
         del b
 
 
@@ -130,18 +126,16 @@ def test_batch_output_digests(ric, port, w, h, ch):
     """ric_batch_set_digests: every frame's digest is taken in stream order
     right after its pixels, so frames sharing one output buffer keep their own
     (the bench verifies its serving step this way)"""
-    torch = pytest.importorskip("torch")
     n = 7
     host = [ric.synth(w, h, ch, 50 + i) for i in range(n)]
-    frames = [torch.from_numpy(x).cuda() for x in host]
-    shared = [torch.empty_like(frames[0]) for _ in range(2)]
+    frames = [ric.DeviceArray.from_numpy(x) for x in host]
+    shared = [frames[0].empty_like() for _ in range(2)]
     outs = [shared[i % 2] for i in range(n)]
-    dig = torch.zeros(n, dtype=torch.int64, device="cuda")
+    dig = ric.DeviceArray(n, np.uint64, zero=True)
     b = ric.Batch(w, h, ch, slots=2, threads=2)
     b.set_digests(dig, n)
     b.roundtrip(frames, outs, q=9, trans=0)
-    torch.cuda.synchronize()
-    got = dig.cpu().numpy().view(np.uint64)
+    got = dig.numpy()
     for i in range(n):
         want = port.decode_ric(port.encode_ric(host[i], 9, 0))[0]
         assert got[i] == _digest(want), i

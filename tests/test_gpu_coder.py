@@ -19,14 +19,13 @@ def _slots(n, c):
 
 
 def _gpu_encode(ric, frames, q, t):
-    import torch
     c, h, w = frames[0].shape[-3:]
-    dev = [torch.from_numpy(np.ascontiguousarray(f)).cuda() for f in frames]
+    dev = [ric.DeviceArray.from_numpy(f) for f in frames]
     b = ric.Batch(w, h, c, slots=_slots(len(frames), c), threads=1)
     ostride = (w * h * c * 2 + 65536 + 4095) // 4096 * 4096
-    out = torch.zeros(len(frames) * ostride, dtype=torch.uint8, device="cuda")
+    out = ric.DeviceArray(len(frames) * ostride, np.uint8, zero=True)
     lens = b.compress_gpu(dev, out, ostride, q, t)
-    host = out.cpu().numpy()
+    host = out.numpy()
     return [host[i * ostride:i * ostride + n].tobytes() for i, n in enumerate(lens)]
 
 
@@ -70,10 +69,9 @@ def test_gpu_coder_large_sha(ric, name):
 def test_hybrid_roundtrip(ric, port, w, h, q, t, n, n_host, pool, slots, gpu_decode):
     """GPU-encoded and host-encoded frames in one pipelined call (several
     coder launches, both halves of the stream buffer, both slot sets)."""
-    import torch
     host = [ric.synth(w, h, 1, 80 + i) for i in range(n)]
-    frames = [torch.from_numpy(x).cuda() for x in host]
-    outs = [torch.empty_like(f) for f in frames]
+    frames = [ric.DeviceArray.from_numpy(x) for x in host]
+    outs = [f.empty_like() for f in frames]
     b = ric.Batch(w, h, 1, slots=slots, threads=3)
     b.hybrid_config(pool, (w * h * 2 + 65536 + 15) // 16 * 16)
     for rep in range(2):
@@ -82,20 +80,19 @@ def test_hybrid_roundtrip(ric, port, w, h, q, t, n, n_host, pool, slots, gpu_dec
             r = b.stream(i)
             assert len(r) == lens[i]
             assert r == port.encode_ric(host[i], q, t), (rep, i)
-            assert np.array_equal(outs[i].cpu().numpy(), port.decode_ric(r)[0]), (rep, i)
+            assert np.array_equal(outs[i].numpy(), port.decode_ric(r)[0]), (rep, i)
 
 
 def _gpu_decode(ric, rics, w, h, c=1):
-    import torch
     istride = (max(len(r) for r in rics) + 4095) // 4096 * 4096
     buf = np.zeros(len(rics) * istride, np.uint8)
     for i, r in enumerate(rics):
         buf[i * istride:i * istride + len(r)] = np.frombuffer(r, np.uint8)
-    src = torch.from_numpy(buf).cuda()
-    outs = [torch.zeros((c, h, w), dtype=torch.uint8, device="cuda") for _ in rics]
+    src = ric.DeviceArray.from_numpy(buf)
+    outs = [ric.DeviceArray((c, h, w), np.uint8, zero=True) for _ in rics]
     b = ric.Batch(w, h, c, slots=_slots(len(rics), c), threads=1)
     rc = b.decompress_gpu(src, istride, [len(r) for r in rics], outs)
-    return rc, [o.cpu().numpy() for o in outs]
+    return rc, [o.numpy() for o in outs]
 
 
 @pytest.mark.parametrize("w,h,q,t", [(1024, 768, 9, 0), (640, 480, 0, 1), (328, 200, 20, 0), (257, 129, 9, 0),
@@ -138,29 +135,27 @@ def test_gpu_decoder_golden_small(ric):
 @pytest.mark.parametrize("name", ["C3_7680x4320_q9", "C2_4096x4096_q9", "lossless53_1001x603"])
 def test_gpu_roundtrip_large_sha(ric, name):
     """Encode and decode on the GPU: the reference's SHA-256 of both."""
-    import torch
     e = [x for x in G["large"] if x["name"] == name][0]
     w, h = e["w"], e["h"]
-    frame = torch.from_numpy(ric.synth(w, h, 1, e["frame"])).cuda()
+    frame = ric.DeviceArray.from_numpy(ric.synth(w, h, 1, e["frame"]))
     b = ric.Batch(w, h, 1, slots=1, threads=1)
     ostride = (w * h * 2 + 65536 + 4095) // 4096 * 4096
-    out = torch.zeros(ostride, dtype=torch.uint8, device="cuda")
+    out = ric.DeviceArray(ostride, np.uint8, zero=True)
     lens = b.compress_gpu([frame], out, ostride, e["q"], e["trans"])
-    assert hashlib.sha256(out[:lens[0]].cpu().numpy().tobytes()).hexdigest() == e["ric_sha256"]
-    pix = torch.zeros((1, h, w), dtype=torch.uint8, device="cuda")
+    assert hashlib.sha256(out.numpy()[:lens[0]].tobytes()).hexdigest() == e["ric_sha256"]
+    pix = ric.DeviceArray((1, h, w), np.uint8, zero=True)
     b.decompress_gpu(out, ostride, lens, [pix])
-    assert hashlib.sha256(pix.cpu().numpy().tobytes()).hexdigest() == e["decoded_sha256"]
+    assert hashlib.sha256(pix.numpy().tobytes()).hexdigest() == e["decoded_sha256"]
 
 
 def test_gpu_encoder_rejects_unaligned_capacity(ric):
     """The stream coder stores 16-byte chunks: a capacity or stride that is not
     a multiple of 16 would drop a stream's tail unflagged, so it is refused."""
     import ctypes
-    import torch
     w, h = 64, 48
-    frame = torch.from_numpy(ric.synth(w, h, 1, 1)).cuda()
+    frame = ric.DeviceArray.from_numpy(ric.synth(w, h, 1, 1))
     b = ric.Batch(w, h, 1, slots=1, threads=1)
-    out = torch.zeros(65536, dtype=torch.uint8, device="cuda")
+    out = ric.DeviceArray(65536, np.uint8, zero=True)
     lens = (ctypes.c_size_t * 1)()
     for ostride, cap in ((8192, 8190), (8200, 8192), (8192, 8192)):
         rc = ric.lib().ric_batch_encode_gpu(b.h, ric._ptrs([frame]), 1, 9, 0, out.data_ptr(), ostride, cap, lens)
@@ -202,3 +197,55 @@ def test_gpu_coder_colour_large_sha(ric):
     assert hashlib.sha256(got).hexdigest() == e["ric_sha256"]
     rc, dec = _gpu_decode(ric, [got], w, h, 3)
     assert hashlib.sha256(dec[0].tobytes()).hexdigest() == e["decoded_sha256"]
+
+
+def test_hybrid_tagged_results_across_launch_forms(ric, port):
+    """Repeated calls on one batch alternate the merged k_gc_roundtrip launch
+    over both pool halves, per-half k_gc_encode launches (a call with one
+    coder batch, a call's third batch, lossless streams), odd pool and slot
+    geometries, and new frames every call: each stream copier must take only
+    its own launch's posted results (tagged per launch), never a word an
+    earlier launch left over the same frames.  The stream-ready words
+    (ric_batch_set_ready) carry every frame's length."""
+    w, h = 200, 136
+    b = ric.Batch(w, h, 1, slots=3, threads=2)
+    b.hybrid_config(5, (w * h * 2 + 65536 + 15) // 16 * 16)
+    plan = [(13, 2, 9, 0), (4, 0, 9, 0), (13, 1, 20, 0), (11, 0, 0, 1), (9, 3, 9, 0), (3, 3, 9, 0), (12, 1, 5, 0),
+            (12, 1, 5, 0)]
+    for call, (n, n_host, q, t) in enumerate(plan):
+        host = [ric.synth(w, h, 1, 300 + 17 * call + i) for i in range(n)]
+        frames = [ric.DeviceArray.from_numpy(x) for x in host]
+        outs = [f.empty_like() for f in frames]
+        words = np.zeros(n, np.uint32)
+        b.set_ready(words, n)
+        lens = b.roundtrip_hybrid(frames, outs, n_host, q, t, gpu_decode=1)
+        b.set_ready(None, 0)
+        assert list(words) == lens, call
+        for i in range(n):
+            r = b.stream(i)
+            assert r == port.encode_ric(host[i], q, t), (call, i)
+            assert np.array_equal(outs[i].numpy(), port.decode_ric(r)[0]), (call, i)
+
+
+def test_device_digests_and_comm_self(ric):
+    """The gather's device primitives: ric_device_digests = shard.digest_bytes
+    (the host formula); a one-rank RCCL communicator sending to itself; the
+    all-reduce; a StreamGather-style chunk through RcclTransport."""
+    import shard
+    rng = np.random.default_rng(5)
+    data = rng.integers(0, 256, 1 << 20, dtype=np.uint8)
+    d = ric.DeviceArray.from_numpy(data)
+    offs, lens = [0, 16, 1000, 4099, 65536], [1, 999, 3000, 70000, 900000]
+    got = ric.device_digests(0, d, offs, lens)
+    for o, n, g in zip(offs, lens, got):
+        assert g == shard.digest_bytes(data[o:o + n]), (o, n)
+    comm = ric.Comm(ric.Comm.unique_id(), 1, 0, 0)
+    assert comm.allreduce([3.0, -1.5], ric.RIC_RED_SUM).tolist() == [3.0, -1.5]
+    back = ric.DeviceArray(data.size, np.uint8, zero=True)
+    comm.sendrecv([(0, True, d, data.size), (0, False, back, data.size)])
+    assert np.array_equal(back.numpy(), data)
+    t = shard.RcclTransport(comm, 0)
+    buf = t.alloc(1 << 16)
+    t.put(buf, 32, data[:5000])
+    assert bytes(t.get(buf, 32, 5000)) == data[:5000].tobytes()
+    assert t.digests(buf, [32], [5000])[0] == shard.digest_bytes(data[:5000])

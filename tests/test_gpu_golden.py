@@ -232,17 +232,16 @@ def test_concurrent_codecs(ric, port):
 
 
 def test_device_resident_buffers(ric, port):
-    torch = pytest.importorskip("torch")
     w, h = 1024, 768
     pix = ric.synth(w, h, 1, 3)
-    d = torch.from_numpy(pix).cuda()
-    out = torch.empty_like(d)
+    d = ric.DeviceArray.from_numpy(pix)
+    out = d.empty_like()
     c = ric.Codec(w, h, 1)
     r = c.compress(d, 9, 0, on_device=True)
     assert r == port.encode_ric(pix, 9, 0)
     c.decompress(r, pix_out=out)
-    torch.cuda.synchronize()
-    assert np.array_equal(out.cpu().numpy(), port.decode_ric(r)[0])
+    ric.device_sync()
+    assert np.array_equal(out.numpy(), port.decode_ric(r)[0])
 
 
 @pytest.mark.parametrize("kind", ["uniform", "alt", "ramp"])

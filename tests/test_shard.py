@@ -1,6 +1,6 @@
 """Frame/tile sharding and the stream gather (rududu-image-codec_amd/shard.py):
-host logic plus a world_size-2 gloo run (the GPU runs use the same code with
-the nccl=RCCL backend)."""
+host logic plus multi-process gloo runs of the gather protocol (the GPU runs
+use the same StreamGather over the library's RCCL communicator)."""
 import os
 import socket
 
@@ -76,61 +76,96 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _init(rank, world, port):
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                     "rududu-image-codec_amd"))
     import torch.distributed as dist
-    import shard as S
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    frames = S.frames_of_rank(7, world, rank)
-    local = [(b"frame%d:" % f) * (f + 1) for f in frames]
-    res = S.gather_streams(local, dist)
-    dev = S.gather_streams(local, dist, to_host=False)   # bench.py's form
-    if dev is not None:
-        bufs, szs = dev
-        dev = [[bytes(b[int(s[1:1 + i].sum()):int(s[1:2 + i].sum())].numpy()) for i in range(int(s[0]))]
-               for b, s in zip(bufs, szs)]
-    q.put((rank, (res, dev)))
+    return dist
+
+
+def _stream(rank, i):
+    rng = np.random.default_rng(1000 * rank + i)
+    return rng.integers(0, 256, int(rng.integers(1, 9000)), dtype=np.uint8).tobytes()
+
+
+def _worker_gather(rank, world, port, nper, q):
+    """Every rank codes nper[rank] streams that become ready in a random
+    order over time (a producer thread sets their ready words, as
+    ric_batch_set_ready does); they are shipped in 16 KiB chunks."""
+    import threading
+    import time
+    dist = _init(rank, world, port)
+    import shard as S
+    t = S.GlooTransport(dist)
+    g = S.StreamGather(t, rank, world, chunk_bytes=16 << 10)
+    n = nper[rank]
+    streams = [_stream(rank, i) for i in range(n)]
+    if rank == 0:
+        got = {}
+        g.receive(lambda r, i, b: got.__setitem__((r, i), bytes(b)))
+        held = sum(b.size for b in g.bufs) + sum(h.size for h in g.hdr)
+        q.put((rank, (got, g.stats, held)))
+    else:
+        words = np.zeros(n, np.uint32)
+        order = np.random.default_rng(rank).permutation(n)
+
+        def produce():
+            for k, i in enumerate(order):
+                words[i] = len(streams[i])
+                if k % 7 == 0:
+                    time.sleep(0.002)
+        th = threading.Thread(target=produce)
+        th.start()
+        st = g.send(n, words, lambda i, ln: streams[i])
+        th.join()
+        q.put((rank, st))
     dist.destroy_process_group()
 
 
-def test_gather_streams_gloo_world2():
+def _spawn(target, world, *args):
     import multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=target, args=(r, world, port) + args + (q,)) for r in range(world)]
     for p in ps:
         p.start()
-    out = dict(q.get(timeout=120) for _ in range(2))
+    out = dict(q.get(timeout=180) for _ in range(world))
     for p in ps:
         p.join(timeout=60)
-    assert out[1] == (None, None)
-    got, got_dev = out[0]
-    assert got_dev == got
-    assert [len(x) for x in got] == [4, 3]
-    flat = {}
-    for r, lst in enumerate(got):
-        for f, s in zip(shard.frames_of_rank(7, 2, r), lst):
-            flat[f] = s
-    assert all(flat[f] == (b"frame%d:" % f) * (f + 1) for f in range(7))
+    return out
+
+
+@pytest.mark.parametrize("world,nper", [(2, [0, 150]), (3, [5, 97, 0])])
+def test_stream_gather_gloo(world, nper):
+    """Every stream of every rank arrives at rank 0 byte-exact (digests
+    checked on arrival), in bounded chunks: rank 0 holds one 16 KiB chunk per
+    peer however many streams there are."""
+    out = _spawn(_worker_gather, world, nper)
+    got, stats, held = out[0]
+    assert stats["digest_mismatches"] == []
+    for r in range(1, world):
+        assert stats["streams"][r] == nper[r] == out[r]["streams"]
+        for i in range(nper[r]):
+            assert got[(r, i)] == _stream(r, i), (r, i)
+    assert len(got) == sum(nper[1:])
+    assert held <= (world - 1) * ((16 << 10) + 8 * 196 + 64)
+    if nper[1] > 64:
+        assert stats["rounds"] > 2             # many streams: several chunks
 
 
 def _worker_tiles(rank, world, port, q):
     """C4's exchange: each rank's tile streams to rank 0 (gather), the RTL1
     container there, and the decode side: unpack + scatter back."""
-    import sys
-    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
-                                    "rududu-image-codec_amd"))
-    import torch.distributed as dist
+    dist = _init(rank, world, port)
     import shard as S
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    t = S.GlooTransport(dist)
     mine = S.tiles_of_rank(world, rank)
     local = [(b"tile%d|" % i) * (50 + 7 * i) for i in mine]
-    got = S.gather_streams(local, dist)
+    got = S.gather_streams(local, t, rank, world)
     blob = None
     per_rank = None
     if rank == 0:
@@ -141,25 +176,26 @@ def _worker_tiles(rank, world, port, q):
         blob = S.pack_tiles(7680, 4320, 2, 2, streams)
         _, _, _, _, back = S.unpack_tiles(blob)
         per_rank = [[back[i] for i in S.tiles_of_rank(world, r)] for r in range(world)]
-    mine_back = S.scatter_streams(per_rank, dist)
+    mine_back = S.scatter_streams(per_rank, t, rank, world)
     q.put((rank, (local, mine_back, blob)))
     dist.destroy_process_group()
 
 
 def test_tiles_gather_container_scatter_gloo_world2():
-    import multiprocessing as mp
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    ps = [ctx.Process(target=_worker_tiles, args=(r, 2, port, q)) for r in range(2)]
-    for p in ps:
-        p.start()
-    out = dict(q.get(timeout=120) for _ in range(2))
-    for p in ps:
-        p.join(timeout=60)
+    out = _spawn(_worker_tiles, 2)
     for r in range(2):
         local, back, _ = out[r]
         assert back == local and len(local) == 2
     W, H, nx, ny, streams = shard.unpack_tiles(out[0][2])
     assert (W, H, nx, ny) == (7680, 4320, 2, 2)
     assert streams == [(b"tile%d|" % i) * (50 + 7 * i) for i in range(4)]
+
+
+def test_digest_matches_device_formula():
+    """shard.digest_bytes is ric_batch_set_digests' formula (bench.py
+    pixel_digest), which the device digest kernel implements"""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    a = np.random.default_rng(3).integers(0, 256, 100003, dtype=np.uint8)
+    assert shard.digest_bytes(a) == bench.pixel_digest(a)
