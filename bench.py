@@ -383,7 +383,7 @@ def main():
         if b is not None:
             b.set_ready(ready, nfr)
 
-    hybrid = a.coder in ("hybrid", "gpu", "mix") and CH == 1 and b is not None
+    hybrid = a.coder in ("hybrid", "gpu", "mix") and b is not None
     gpu_dec = {"hybrid": 0, "gpu": 1, "mix": 2}.get(a.coder, 0)
     n_host = 0
     nstep = nfr                                # frames coded per step
@@ -394,7 +394,7 @@ def main():
         nstep = n_host + n_gpu
         # stream capacity: 3 bits per pixel (a q9 C3 stream is 1.7), 16-byte multiple
         pool = min(a.pool, max(n_gpu, 1))
-        scap = (W * H * 3 // 8 + 65536) // 16 * 16
+        scap = (W * H * CH * 3 // 8 + 65536) // 16 * 16
         # the pool holds bands + records + a stream per frame in flight (C3:
         # ~110 MB): if it does not fit this GPU's memory, shrink it
         while True:

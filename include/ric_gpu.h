@@ -245,10 +245,13 @@ int ric_batch_decode_gpu(ric_batch* b, const uint8_t* in, size_t istride, const 
  * Size dev_buf for n*2048 words plus the pyramid's sample count.  NULL: off.
  * One caller at a time (the pointer is a process global). */
 int ric_diag_gdec_dbg(void* dev_buf);
-/* Hybrid round trip (gray): the serial encoder runs on the GPU (one wave per
+/* Hybrid round trip: the serial encoder runs on the GPU (one wave per
  * stream, launches of `pool_frames` frames, each stream up to stream_cap
  * bytes: a multiple of 16; a longer stream fails the call with
- * RIC_E_CAPACITY), the serial decoder on the host pool.  Configure once.
+ * RIC_E_CAPACITY), the serial decoder on the GPU or the host pool.  Gray or
+ * colour (a colour frame's Y, Co, Cg plane pyramids sit side by side in the
+ * pool and one wave codes them into the frame's one stream, ric.cpp:157-176).
+ * Configure once.
  * A pool that does not fit in device memory returns RIC_E_CAPACITY with
  * nothing allocated (the batch stays usable: retry with fewer frames). */
 int ric_batch_hybrid_config(ric_batch* b, int pool_frames, size_t stream_cap);
@@ -274,7 +277,10 @@ int ric_batch_set_ready(ric_batch* b, uint32_t* host_words, long n);
  * [n_host, n) encoded by the GPU stream coder and decoded by the GPU stream
  * decoder (gpu_decode 1), on the host pool (0), or per coder launch by
  * whichever is free (2: the host pool while its backlog is shorter than a
- * launch, the GPU for the rest).  Byte-identical streams either way. */
+ * launch, the GPU for the rest).  Byte-identical streams either way.  Colour
+ * frames coded or decoded on the host take three slots each (one per plane),
+ * so their groups are slots / 3 frames: with host frames or gpu_decode != 1
+ * a colour batch needs slots >= 3 (else RIC_E_ARG). */
 int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, int n_host, int gpu_decode, int q,
                                int trans, uint8_t* const* out, const size_t* cap, size_t* len, uint8_t* const* pix_out);
 /* When each side of the last ric_batch_roundtrip_hybrid finished, in ms from

@@ -214,7 +214,8 @@ struct ric_batch {
 	// hybrid round trip: the pool of frames the GPU stream coder works on
 	struct CoderPool {
 		int n = 0;                                 // frames per coder launch
-		size_t abstride = 0, ocap = 0;             // A+B bytes per frame, stream bytes per frame
+		size_t abstride = 0, ocap = 0;             // A+B bytes per plane pyramid, stream bytes per frame
+		size_t fstride = 0;                        // bytes per frame: channels * abstride
 		char* d_ab = nullptr;                      // 2 halves of n frames' bands + records
 		uint8_t* d_out = nullptr;                  // 2 halves of n streams
 		GEncArgs* d_args = nullptr;                // argument blocks, one per half
@@ -297,6 +298,8 @@ int lambda_of(int q, int p) { return q ? quants(q + 13 + (p ? 8 : 0)) : 0; }
 // frames keeps a frame's three plane pyramids side by side (amul 3).
 // yflag: the GPU stream coder's yield flag (coder_yield, gcoder.hip), raised
 // around the level kernels only (not the copies), or null
+int d2h_slots(ric_batch* b, int set, int n);
+
 int gpu_encode_plane(ric_batch* b, int set, int n, int p, const uint8_t* const* pix, int q, int trans, bool d2h = true,
                      int abase = -1, int amul = 1, uint32_t* yflag = nullptr)
 {
@@ -365,6 +368,17 @@ int gpu_encode_plane(ric_batch* b, int set, int n, int p, const uint8_t* const* 
 	if (yf.lower()) return RIC_E_HIP;
 	if (!d2h) return RIC_OK;
 	if (abase != s0 || amul != 1) return RIC_E_ARG;      // the host mirrors follow the slots
+	return d2h_slots(b, set, n);
+}
+
+// The bands + records of slots set * slots .. + n - 1 (after their forward
+// levels) to the host mirrors: the compacted 16-bit values and the dense rest
+// (or the dense arenas).  Colour frames of a hybrid host group take C slots
+// each (plane p of frame i in slot C i + p), so n counts slots, not frames.
+int d2h_slots(ric_batch* b, int set, int n)
+{
+	Pyramid& P = b->P;
+	const int s0 = set * b->slots;
 	if (b->compact) {
 		// the 16-bit bands' values in walk order (compact.hip), written by a
 		// kernel into the head of each frame's host mirror (only the values,
@@ -393,18 +407,15 @@ int gpu_encode_plane(ric_batch* b, int set, int n, int p, const uint8_t* const* 
 	return RIC_OK;
 }
 
-// The GPU half of DecompressImage for plane p of n frames of set `set`: the
-// host-decoded bands to the device (one strided copy), then every inverse
-// level with the fused TSUQi factors of each frame, as one launch per level.
-int gpu_decode_plane(ric_batch* b, int set, int n, int p, const int* qs, int trans, bool h2d = true, int abase = -1,
-                     int amul = 1, uint32_t* yflag = nullptr)
+// The host-decoded bands of slots set * slots .. + n - 1 to the device: one
+// strided copy (levels 1.. dense and each slot's compacted finest level,
+// scattered by k_dcmp_expand; or the dense arenas).  n counts slots (colour
+// frames of a hybrid host group take C slots each).
+int h2d_slots(ric_batch* b, int set, int n)
 {
 	Pyramid& P = b->P;
 	const int s0 = set * b->slots;
-	if (abase < 0) abase = s0;
-	if (h2d && (abase != s0 || amul != 1)) return RIC_E_ARG;
-	const size_t ast = (size_t)amul * b->astride;
-	if (h2d) {
+	{
 		bool cmp = b->dcompact;
 		for (int i = 0; i < n && cmp; i++) cmp = b->dcmp_ok[s0 + i] != 0;
 		auto sp = b->prof.begin(B_H2D, n, b->st);
@@ -440,6 +451,24 @@ int gpu_decode_plane(ric_batch* b, int set, int n, int p, const int* qs, int tra
 			BCHK(hipMemcpy2DAsync(b->arena(s0), b->astride, b->harena(s0), b->hstride, P.a_end, n, hipMemcpyHostToDevice, b->st));
 		}
 		b->prof.end(sp);
+	}
+	return RIC_OK;
+}
+
+// The GPU half of DecompressImage for plane p of n frames of set `set`: the
+// host-decoded bands to the device (one strided copy), then every inverse
+// level with the fused TSUQi factors of each frame, as one launch per level.
+int gpu_decode_plane(ric_batch* b, int set, int n, int p, const int* qs, int trans, bool h2d = true, int abase = -1,
+                     int amul = 1, uint32_t* yflag = nullptr)
+{
+	Pyramid& P = b->P;
+	const int s0 = set * b->slots;
+	if (abase < 0) abase = s0;
+	if (h2d && (abase != s0 || amul != 1)) return RIC_E_ARG;
+	const size_t ast = (size_t)amul * b->astride;
+	if (h2d) {
+		const int r = h2d_slots(b, set, n);
+		if (r) return r;
 	}
 	P.set_weight(trans);
 	YieldFlag yf(yflag, b->st);
@@ -482,7 +511,6 @@ int gpu_pix_out(ric_batch* b, int set, int n, const int* qs, uint8_t* const* pix
 {
 	const int s0 = set * b->slots;
 	auto sp = b->prof.begin(B_PIXOUT, n, b->st);
-	const size_t npix = (size_t)b->w * b->h * b->channels;
 	// every frame of the group below ndigest gets its digest (a group may
 	// straddle the limit)
 	const long ndig = b->digest && idx0 >= 0 ? std::max(0L, std::min((long)n, b->ndigest - idx0)) : 0;
@@ -490,8 +518,8 @@ int gpu_pix_out(ric_batch* b, int set, int n, const int* qs, uint8_t* const* pix
 	for (int i = 0; i < n; i++) {
 		if (!pix_out[i]) continue;
 		uint8_t* dst = on_device ? pix_out[i] : b->stage(s0 + i);
-		launch_pix_out(b->plane(s0 + i, 0), b->pitch, b->w, b->h, b->channels, qs[i], dst, nullptr, b->st);
-		if (i < ndig) launch_digest(dst, npix, b->digest + idx0 + i, b->st);
+		launch_pix_out(b->plane(s0 + i, 0), b->pitch, b->w, b->h, b->channels, qs[i], dst, nullptr, b->st,
+		               i < ndig ? b->digest + idx0 + i : nullptr);
 	}
 	b->prof.end(sp);
 	BCHK(hipGetLastError());
@@ -505,11 +533,13 @@ int gpu_pix_out(ric_batch* b, int set, int n, const int* qs, uint8_t* const* pix
 // Host coder of plane p of the frame in slot s.  Encode: the .ric file is
 // written in place into out (the coder buffer starts at out + 7, so the
 // payload lands at out + 9 and the two dropped leading coder bytes are
-// overwritten by the header at the end).
-int host_encode_plane(ric_batch* b, int s, int p, int q, int trans, uint8_t* out, size_t cap, size_t* len)
+// overwritten by the header at the end).  ms: the slot whose coder carries
+// the frame's stream across its planes (default s; a hybrid colour frame keeps
+// each plane in a slot of its own, the stream in its first).
+int host_encode_plane(ric_batch* b, int s, int p, int q, int trans, uint8_t* out, size_t cap, size_t* len, int ms = -1)
 {
 	Pyramid& P = b->P;
-	Mux& m = b->enc[s];
+	Mux& m = b->enc[ms < 0 ? s : ms];
 	if (p == 0) {
 		if (cap < 16) return RIC_E_CAPACITY;
 		m.init_encoder(out + 7, cap - 7, 0);
@@ -554,10 +584,10 @@ int host_encode_plane(ric_batch* b, int s, int p, int q, int trans, uint8_t* out
 
 // Host decoder of plane p of one .ric file into the host mirror of slot s
 // (CWavelet2D::DecodeBand, src/lib/wavelet2d.cpp:179-222).
-int host_decode_plane(ric_batch* b, int s, int p, const uint8_t* ric, size_t len)
+int host_decode_plane(ric_batch* b, int s, int p, const uint8_t* ric, size_t len, int ms = -1)
 {
 	Pyramid& P = b->P;
-	Mux& m = b->dec[s];
+	Mux& m = b->dec[ms < 0 ? s : ms];
 	if (p == 0) {
 		// the reference reads W*H*C payload bytes (ric.cpp:203-205)
 		const size_t pay = std::min(len - 9, (size_t)b->w * b->h * b->channels);
@@ -1119,7 +1149,6 @@ int ric_batch_hybrid_config(ric_batch* b, int pool_frames, size_t stream_cap)
 {
 	if (!b || pool_frames < 1 || pool_frames > 65536 || stream_cap < 64 || (stream_cap & 15) || stream_cap > 0xFFFFFFF0u)
 		return RIC_E_ARG;
-	if (b->channels != 1) return RIC_E_ARG;
 	if (set_dev(b->device)) return RIC_E_HIP;
 	auto& c = b->cp;
 	for (int h = 0; h < 2; h++)
@@ -1134,11 +1163,14 @@ int ric_batch_hybrid_config(ric_batch* b, int pool_frames, size_t stream_cap)
 		BCHK(hipMemset(c.d_yield, 0, 256));
 	}
 	c.n = pool_frames;
+	// colour: a frame's Y, Co, Cg plane pyramids side by side (the coder codes
+	// them into one stream on one wave, ric.cpp:157-176)
 	c.abstride = (b->P.b_end + 65535) / 65536 * 65536;
+	c.fstride = (size_t)b->channels * c.abstride;
 	c.ocap = stream_cap;
 	// out of memory: nothing stays allocated and the error is not left
 	// pending (a caller may retry with a smaller pool)
-	if (hipMalloc(&c.d_ab, 2 * c.abstride * c.n) != hipSuccess || hipMalloc(&c.d_out, 2 * c.ocap * c.n) != hipSuccess) {
+	if (hipMalloc(&c.d_ab, 2 * c.fstride * c.n) != hipSuccess || hipMalloc(&c.d_out, 2 * c.ocap * c.n) != hipSuccess) {
 		const hipError_t e = hipGetLastError();
 		if (c.d_ab) (void)hipFree(c.d_ab);
 		c.d_ab = nullptr;
@@ -1201,8 +1233,11 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 	if (!b || !pix || !out || !cap || !len || !pix_out || n < 0 || n_host < 0 || n_host > n || q < 0 || q > 31 ||
 	    trans < 0 || trans > 2)
 		return RIC_E_ARG;
-	if (b->channels != 1) return RIC_E_ARG;
 	if (n_host < n && (!b->cp.d_ab || !b->cp.h_res || !b->cp.d_post)) return RIC_E_ARG;    // ric_batch_hybrid_config first
+	// colour frames round-tripped or decoded on the host keep each plane's
+	// bands in a slot of its own: a host group is slots / 3 frames
+	const int C = b->channels;
+	if (C == 3 && b->slots < 3 && (n_host > 0 || gpu_decode != 1)) return RIC_E_ARG;
 	if (n == 0) return RIC_OK;
 	if (!outputs_distinct(out, n))
 		return set_last_error("ric_batch_roundtrip_hybrid: out[] buffers must be distinct"), RIC_E_ARG;
@@ -1216,6 +1251,7 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 	auto& c = b->cp;
 	Pyramid& P = b->P;
 	const int S = b->slots;
+	const int SG = S / C;                                  // frames per host group (slots per frame: C)
 	// word offsets into d_res / h_res: the encoder's 2 words per frame of both
 	// halves, then the decoder's word per frame of both (so the two halves can
 	// also run as one launch over 2 n frames)
@@ -1236,8 +1272,8 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 			a.ts = tstamp ? c.d_ts + (size_t)h * 4 * c.n : nullptr;
 			a.prio = gc_prio();
 			a.yield = yield_on ? c.d_yield : nullptr;
-			a.arena = c.d_ab + (size_t)h * c.n * c.abstride; a.astride = c.abstride;
-			a.pstride = c.abstride; a.nplanes = 1;                        // gray (checked above)
+			a.arena = c.d_ab + (size_t)h * c.n * c.fstride; a.astride = c.fstride;
+			a.pstride = c.abstride; a.nplanes = C;
 			a.out = c.d_out + (size_t)h * c.n * c.ocap; a.ostride = c.ocap; a.cap = c.ocap;
 			a.res = c.d_res + res_enc(h);
 			a.status_off = (uint32_t)P.status_off;
@@ -1245,7 +1281,7 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 			gc_bands(P, a.ll, a.b, a.nb);
 			GDecArgs& d = c.dargs[h];
 			d.arena = (char*)a.arena; d.astride = a.astride;
-			d.pstride = a.pstride; d.nplanes = 1;
+			d.pstride = a.pstride; d.nplanes = C;
 			d.in = a.out; d.istride = c.ocap;
 			d.lens = a.res; d.lens_stride = 2;
 			d.res = c.d_res + res_dec(h);
@@ -1275,7 +1311,7 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 	int host_groups_done = 0;
 	b->hyb_host_ms = b->hyb_gpu_ms = 0;
 	std::deque<HGroup> ready_host, ready_dec;
-	for (int f0 = 0; f0 < n_host; f0 += S) ready_host.push_back({f0, std::min(S, n_host - f0), false, 0, 0});
+	for (int f0 = 0; f0 < n_host; f0 += SG) ready_host.push_back({f0, std::min(SG, n_host - f0), false, 0, 0});
 	const int ng = n - n_host;
 	const int nbatch = ng > 0 ? (ng + c.n - 1) / c.n : 0;
 	int kicked = 0, finished = 0;
@@ -1294,7 +1330,7 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 	std::vector<int> qs(S, q);
 	auto batch_f0 = [&](int j) { return n_host + j * c.n; };
 	auto batch_m = [&](int j) { return std::min(c.n, n - batch_f0(j)); };
-	auto abslot = [&](int h, int k) { return c.d_ab + ((size_t)h * c.n + k) * c.abstride; };
+	auto abslot = [&](int h, int k) { return c.d_ab + ((size_t)h * c.n + k) * c.fstride; };   // frame k of half h, plane 0
 	// RIC_FWD_AHEAD=0: each batch's coder launch starts after its own forward
 	// levels (the second batch's then run beside the first batch's coder waves)
 	static const bool fwd_ahead = [] { const char* e = getenv("RIC_FWD_AHEAD"); return !e || atoi(e) != 0; }();
@@ -1359,10 +1395,12 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 		const int f0 = batch_f0(j), m = batch_m(j), h = j & 1;
 		for (int g0 = 0; g0 < m; g0 += S) {
 			const int gm = std::min(S, m - g0);
-			int r = gpu_encode_plane(b, 0, gm, 0, pix + f0 + g0, q, trans, false);
-			if (r) return r;
-			BCHK(hipMemcpy2DAsync(abslot(h, g0), c.abstride, b->arena(0), b->astride, P.b_end, gm, hipMemcpyDeviceToDevice,
-			                      b->st));
+			for (int p = 0; p < C; p++) {                   // (p 0 converts every plane's pixels)
+				int r = gpu_encode_plane(b, 0, gm, p, pix + f0 + g0, q, trans, false);
+				if (r) return r;
+				BCHK(hipMemcpy2DAsync(abslot(h, g0) + (size_t)p * c.abstride, c.fstride, b->arena(0), b->astride, P.b_end, gm,
+				                      hipMemcpyDeviceToDevice, b->st));
+			}
 		}
 		BCHK(hipEventRecord(c.ev_fwd[h], b->st));
 		return RIC_OK;
@@ -1547,15 +1585,18 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 		}
 		if (!bgpu[j]) {
 			enc_ms_est = 0.5 * enc_ms_est + 0.5 * (now_ms() - t_kick[j]);
-			for (int g0 = 0; g0 < m; g0 += S) ready_dec.push_back({f0 + g0, std::min(S, m - g0), true, h, g0});
+			for (int g0 = 0; g0 < m; g0 += SG) ready_dec.push_back({f0 + g0, std::min(SG, m - g0), true, h, g0});
 			return RIC_OK;
 		}
 		for (int g0 = 0; g0 < m; g0 += S) {
 			const int gm = std::min(S, m - g0);
-			BCHK(hipMemcpy2DAsync(b->arena(0), b->astride, abslot(h, g0), c.abstride, P.a_end, gm, hipMemcpyDeviceToDevice,
-			                      b->st));
-			int r = gpu_decode_plane(b, 0, gm, 0, qs.data(), trans, false);
-			if (!r) r = gpu_pix_out(b, 0, gm, qs.data(), pix_out + f0 + g0, 1, f0 + g0);
+			for (int p = 0; p < C; p++) {
+				BCHK(hipMemcpy2DAsync(b->arena(0), b->astride, abslot(h, g0) + (size_t)p * c.abstride, c.fstride, P.a_end, gm,
+				                      hipMemcpyDeviceToDevice, b->st));
+				int r = gpu_decode_plane(b, 0, gm, p, qs.data(), trans, false);
+				if (r) return r;
+			}
+			int r = gpu_pix_out(b, 0, gm, qs.data(), pix_out + f0 + g0, 1, f0 + g0);
 			if (r) return r;
 		}
 		return RIC_OK;
@@ -1578,23 +1619,38 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 		Flight& F = fl.back();
 		F.g = g; F.set = set; F.ev = evs[set];
 		if (!g.gpu) {
-			int r = gpu_encode_plane(b, set, g.m, 0, pix + g.f0, q, trans, true, -1, 1, yflag);
-			if (r) return r;
+			if (C == 1) {
+				int r = gpu_encode_plane(b, set, g.m, 0, pix + g.f0, q, trans, true, -1, 1, yflag);
+				if (r) return r;
+			} else {
+				// plane p of frame i in slot C i + p, then every slot's bands to the host
+				const int s0 = set * S;
+				for (int p = 0; p < C; p++) {
+					int r = gpu_encode_plane(b, set, g.m, p, pix + g.f0, q, trans, false, s0 + p, C, yflag);
+					if (r) return r;
+				}
+				int r = d2h_slots(b, set, C * g.m);
+				if (r) return r;
+			}
 			BCHK(hipEventRecord(F.ev, b->st));
 			if (trace > 2) tr("  forward issued", g.f0);
 		}
 		F.done.reset(g.m);
 		if (trace > 1) tr(g.gpu ? "decode group launched" : "host group launched", g.f0);
 		for (int i = 0; i < g.m; i++) {
-			const int slot = set * S + i, f = g.f0 + i;
+			const int slot = set * S + C * i, f = g.f0 + i;    // colour: the frame's planes in slots slot .. slot + 2
 			Flight* pf = &F;
 			if (!g.gpu) {
 				b->pool->submit([=] {
 					int r1 = bfail(hipEventSynchronize(pf->ev), "hipEventSynchronize") ? RIC_E_HIP : RIC_OK;
 					if (trace > 2 && i == 0) tr("  task: forward passed", f);
-					if (!r1) r1 = host_encode_plane(b, slot, 0, q, trans, out[f], cap[f], &len[f]);
+					for (int p = 0; p < C && !r1; p++) r1 = host_encode_plane(b, slot + p, p, q, trans, out[f], cap[f], &len[f], slot);
 					if (!r1) mark_ready(b, f, len[f]);
-					if (!r1) r1 = host_decode_plane(b, slot, 0, out[f], len[f]);
+					for (int p = 0; p < C && !r1; p++) {
+						const int rp = host_decode_plane(b, slot + p, p, out[f], len[f], slot);
+						if (rp == RIC_E_STREAM && p + 1 < C) continue;     // (the last plane reports the overrun)
+						r1 = rp;
+					}
 					pf->err.put(r1);
 					pf->done.done();
 				});
@@ -1612,7 +1668,11 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 					// the set's mirrors: the previous group's H2D from them has passed
 					if (!r1) r1 = bfail(hipEventSynchronize(pf->ev), "hipEventSynchronize") ? RIC_E_HIP : RIC_OK;
 					const double t0 = now_ms();
-					if (!r1) r1 = host_decode_plane(b, slot, 0, out[f], len[f]);
+					for (int p = 0; p < C && !r1; p++) {
+						const int rp = host_decode_plane(b, slot + p, p, out[f], len[f], slot);
+						if (rp == RIC_E_STREAM && p + 1 < C) continue;     // (the last plane reports the overrun)
+						r1 = rp;
+					}
 					pdec_us->fetch_add((long)((now_ms() - t0) * 1e3));
 					pdec_n->fetch_add(1);
 					pf->err.put(r1);
@@ -1634,7 +1694,12 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 		} else if (trace > 1) {
 			tr("decode group done", F.g.f0);
 		}
-		if (!r2) r2 = gpu_decode_plane(b, F.set, F.g.m, 0, qs.data(), trans, true, -1, 1, yflag);
+		if (!r2 && C == 1) r2 = gpu_decode_plane(b, F.set, F.g.m, 0, qs.data(), trans, true, -1, 1, yflag);
+		if (!r2 && C > 1) {
+			r2 = h2d_slots(b, F.set, C * F.g.m);
+			for (int p = 0; p < C && !r2; p++)
+				r2 = gpu_decode_plane(b, F.set, F.g.m, p, qs.data(), trans, false, F.set * S + p, C, yflag);
+		}
 		if (trace > 2) tr("  inverse issued", F.g.f0);
 		if (!r2) r2 = gpu_pix_out(b, F.set, F.g.m, qs.data(), pix_out + F.g.f0, 1, F.g.f0);
 		if (trace > 2) tr("  pix out issued", F.g.f0);

@@ -142,21 +142,44 @@ __global__ void k_rgb_in8(const uint8_t* __restrict__ pix, int16_t* __restrict__
 	*reinterpret_cast<uint4*>(out + 2 * ps + o) = pack8s(Co);
 }
 
-__global__ void k_gray_out8(const int16_t* __restrict__ in, long pi, int w, int q, uint8_t* __restrict__ pix,
-                            int16_t* __restrict__ planes)
+constexpr unsigned long long kDigestMul = 0x9E3779B97F4A7C15ull;
+
+// DIG: `rows` rows per workgroup and the frame's output digest (the formula of
+// k_digest below, ric_batch_set_digests) taken from the bytes as they are
+// written -- no second pass over the frame; one atomic per workgroup
+template <bool DIG>
+__global__ void k_gray_out8(const int16_t* __restrict__ in, long pi, int w, int h, int q, uint8_t* __restrict__ pix,
+                            int16_t* __restrict__ planes, int rows, unsigned long long* dig)
 {
-	const int x = (blockIdx.x * blockDim.x + threadIdx.x) * 8, y = blockIdx.y;
-	if (x >= w) return;
-	int16_t v[8];
-	unpack8s(*reinterpret_cast<const uint4*>(in + (long)y * pi + x), v);
+	const int x = (blockIdx.x * blockDim.x + threadIdx.x) * 8, y0 = blockIdx.y * rows;
+	unsigned long long s = 0;
+	if (x < w) {
+		for (int y = y0; y < y0 + rows && y < h; y++) {
+			int16_t v[8];
+			unpack8s(*reinterpret_cast<const uint4*>(in + (long)y * pi + x), v);
 #pragma unroll
-	for (int i = 0; i < 8; i++) {
-		if (q == 0) v[i] = (int16_t)(v[i] + 128);
-		else v[i] = clip255((int16_t)(128 + ((v[i] + (1 << (kShift - 1))) >> kShift)));
+			for (int i = 0; i < 8; i++) {
+				if (q == 0) v[i] = (int16_t)(v[i] + 128);
+				else v[i] = clip255((int16_t)(128 + ((v[i] + (1 << (kShift - 1))) >> kShift)));
+			}
+			const long i0 = (long)y * w + x;
+			if (planes) *reinterpret_cast<uint4*>(planes + i0) = pack8s(v);
+			if (pix) *reinterpret_cast<uint2*>(pix + i0) = pack8b(v);
+			if (DIG) {
+#pragma unroll
+				for (int i = 0; i < 8; i++)
+					s += (unsigned long long)(uint8_t)clip255(v[i]) * ((unsigned long long)(i0 + i) * kDigestMul + 1);
+			}
+		}
 	}
-	const long i0 = (long)y * w + x;
-	if (planes) *reinterpret_cast<uint4*>(planes + i0) = pack8s(v);
-	if (pix) *reinterpret_cast<uint2*>(pix + i0) = pack8b(v);
+	if (DIG) {
+#pragma unroll
+		for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+		__shared__ unsigned long long part[4];
+		if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+		__syncthreads();
+		if (threadIdx.x == 0) atomicAdd(dig, part[0] + part[1] + part[2] + part[3]);
+	}
 }
 
 __global__ void k_rgb_out8(const int16_t* __restrict__ in, long pi, int w, int h, int q, uint8_t* __restrict__ pix,
@@ -219,7 +242,6 @@ void launch_pix_in(const uint8_t* pix, int16_t* planes, int w, int h, long po, i
 }
 
 namespace {
-constexpr unsigned long long kDigestMul = 0x9E3779B97F4A7C15ull;
 // 16 bytes per thread (a 16-byte load where the run is aligned and whole),
 // a block sum, one 64-bit atomic add per block
 __global__ __launch_bounds__(256) void k_digest(const uint8_t* __restrict__ p, size_t n, unsigned long long* out)
@@ -251,17 +273,28 @@ void launch_digest(const uint8_t* p, size_t n, unsigned long long* out, hipStrea
 }
 
 void launch_pix_out(const int16_t* planes_in, long pi, int w, int h, int channels, int q,
-                    uint8_t* pix, int16_t* planes_out, hipStream_t st)
+                    uint8_t* pix, int16_t* planes_out, hipStream_t st, unsigned long long* dig)
 {
 	if (vec8_ok(pix, planes_in, planes_out, w, pi)) {
 		dim3 grid8((w / 8 + 255) / 256, h);
-		if (channels == 3) hipLaunchKernelGGL(k_rgb_out8, grid8, dim3(256), 0, st, planes_in, pi, w, h, q, pix, planes_out);
-		else hipLaunchKernelGGL(k_gray_out8, grid8, dim3(256), 0, st, planes_in, pi, w, q, pix, planes_out);
+		if (channels == 3) {
+			hipLaunchKernelGGL(k_rgb_out8, grid8, dim3(256), 0, st, planes_in, pi, w, h, q, pix, planes_out);
+		} else if (dig && pix) {
+			constexpr int kRows = 16;
+			hipLaunchKernelGGL(k_gray_out8<true>, dim3(grid8.x, (h + kRows - 1) / kRows), dim3(256), 0, st, planes_in, pi, w, h,
+			                   q, pix, planes_out, kRows, dig);
+			return;
+		} else {
+			hipLaunchKernelGGL(k_gray_out8<false>, grid8, dim3(256), 0, st, planes_in, pi, w, h, q, pix, planes_out, 1,
+			                   (unsigned long long*)nullptr);
+		}
+		if (dig && pix) launch_digest(pix, (size_t)w * h * channels, dig, st);
 		return;
 	}
 	dim3 grid((w + 255) / 256, h);
 	if (channels == 3) hipLaunchKernelGGL(k_rgb_out, grid, dim3(256), 0, st, planes_in, pi, w, h, q, pix, planes_out);
 	else hipLaunchKernelGGL(k_gray_out, grid, dim3(256), 0, st, planes_in, pi, w, h, q, pix, planes_out);
+	if (dig && pix) launch_digest(pix, (size_t)w * h * channels, dig, st);
 }
 
 }  // namespace ric

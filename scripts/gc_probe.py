@@ -27,15 +27,14 @@ def main():
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--check", type=int, default=4, help="frames compared with the host coder")
     a = ap.parse_args()
-    import torch
     import ric_amd
-    frames = [torch.from_numpy(ric_amd.synth(a.w, a.h, 1, f)).cuda() for f in range(a.n)]
+    frames = [ric_amd.DeviceArray.from_numpy(ric_amd.synth(a.w, a.h, 1, f)) for f in range(a.n)]
     b = ric_amd.Batch(a.w, a.h, 1, slots=a.n, threads=min(16, a.n))
     ostride = (a.w * a.h * 2 + 65536 + 4095) // 4096 * 4096
-    out = torch.zeros(a.n * ostride, dtype=torch.uint8, device="cuda")
+    out = ric_amd.DeviceArray(a.n * ostride, np.uint8, zero=True)
     t0 = time.time()
     lens = b.compress_gpu(frames, out, ostride, a.q, 0)
-    torch.cuda.synchronize()
+    ric_amd.device_sync()
     first = time.time() - t0
     best = 1e9
     for _ in range(a.reps):
@@ -46,17 +45,17 @@ def main():
     b.compress_gpu(frames, out, ostride, a.q, 0)
     p = b.prof_read()
     # the GPU stream decoder on the streams just written
-    pix = [torch.zeros((1, a.h, a.w), dtype=torch.uint8, device="cuda") for _ in range(a.n)]
+    pix = [ric_amd.DeviceArray((1, a.h, a.w), np.uint8, zero=True) for _ in range(a.n)]
     b.decompress_gpu(out, ostride, lens, pix)
-    torch.cuda.synchronize()
+    ric_amd.device_sync()
     t0 = time.time()
     b.decompress_gpu(out, ostride, lens, pix)
-    torch.cuda.synchronize()
+    ric_amd.device_sync()
     dec_s = time.time() - t0
     b.prof_enable(True)
     b.decompress_gpu(out, ostride, lens, pix)
     pd = b.prof_read()
-    host = out.cpu().numpy()
+    host = out.numpy()
     nc = min(a.check, a.n)
     ref = b.compress([frames[i] for i in range(nc)], a.q, 0, on_device=True)
     ok = []
@@ -71,7 +70,7 @@ def main():
     dok = []
     for i in range(nc):
         want = b.decompress([ref[i]])[0]
-        dok.append(bool(np.array_equal(pix[i].cpu().numpy().reshape(want.shape), want)))
+        dok.append(bool(np.array_equal(pix[i].numpy().reshape(want.shape), want)))
     t0 = time.time()
     nh = min(a.n, 16)                     # host coder reference timing on one group
     b.compress([frames[i] for i in range(nh)], a.q, 0, on_device=True)

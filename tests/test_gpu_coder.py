@@ -249,3 +249,23 @@ def test_device_digests_and_comm_self(ric):
     t.put(buf, 32, data[:5000])
     assert bytes(t.get(buf, 32, 5000)) == data[:5000].tobytes()
     assert t.digests(buf, [32], [5000])[0] == shard.digest_bytes(data[:5000])
+
+
+@pytest.mark.parametrize("gpu_decode", [1, 0, 2])
+@pytest.mark.parametrize("w,h,q,t,n,n_host,pool,slots", [(256, 192, 9, 0, 8, 2, 3, 6), (129, 77, 5, 0, 7, 1, 2, 4),
+                                                         (160, 96, 0, 1, 5, 2, 2, 3)])
+def test_hybrid_roundtrip_colour(ric, port, w, h, q, t, n, n_host, pool, slots, gpu_decode):
+    """RGB frames through the serving step: the GPU stream coder codes each
+    frame's Y, Co, Cg pyramids into one stream on one wave (ric.cpp:157-176);
+    host round trips beside it keep each plane in a slot of its own."""
+    host = [ric.synth(w, h, 3, 120 + i) for i in range(n)]
+    frames = [ric.DeviceArray.from_numpy(x) for x in host]
+    outs = [f.empty_like() for f in frames]
+    b = ric.Batch(w, h, 3, slots=slots, threads=3)
+    b.hybrid_config(pool, (w * h * 3 * 2 + 65536 + 15) // 16 * 16)
+    for rep in range(2):
+        b.roundtrip_hybrid(frames, outs, n_host, q, t, gpu_decode=gpu_decode)
+        for i in range(n):
+            r = b.stream(i)
+            assert r == port.encode_ric(host[i], q, t), (rep, i)
+            assert np.array_equal(outs[i].numpy(), port.decode_ric(r)[0].reshape(3, h, w)), (rep, i)
