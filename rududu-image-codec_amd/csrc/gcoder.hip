@@ -301,9 +301,17 @@ struct GBit {
 // The idx-dependent parameters (k, shift, the shift's thresholds) are read
 // from the lane tables when the context is loaded and again only when idx
 // moves, not per coded value.
+// The idx-dependent values the per-value step uses are kept ready-made: the
+// adaptation shift 3 + s, the low threshold t0 and the span t1 - t0 of the
+// re-index test, so that test costs one subtract, mask and compare per value.
 struct GGeoCtx {
-	uint32_t freq, idx, k, s, thr;
-	GC_DI void params(const GTabs& T) { const uint32_t ks = lget(T.geo_ks, idx); k = ks & 0xFFu; s = ks >> 8; thr = lget(T.geo_thr, s); }
+	uint32_t freq, idx, k, s3, t0, span;
+	GC_DI void params(const GTabs& T)
+	{
+		const uint32_t ks = lget(T.geo_ks, idx), s = ks >> 8;
+		const uint32_t thr = lget(T.geo_thr, s);
+		k = ks & 0xFFu; s3 = s + 3; t0 = thr & 0xFFFFu; span = (thr >> 16) - t0;
+	}
 	GC_DI void load(uint32_t arr, uint32_t c, const GTabs& T) { const uint32_t v = lget(arr, c); freq = v & 0xFFFFu; idx = v >> 16; params(T); }
 	GC_DI uint32_t packed() const { return freq | idx << 16; }
 	// magnitude - 1 (unary + k raw bits) then, if SIGNED, one raw sign bit:
@@ -313,20 +321,20 @@ struct GGeoCtx {
 	{
 		const uint32_t f = freq;
 		uint32_t fr = freq;
-		uint32_t run = sym >> k;
-		if (__builtin_expect(run > (1u << 20), 0)) { run = 0; e.ovf |= 4; }   // not a coefficient of this path
+		const uint32_t run = sym >> k;
 		if (__builtin_expect(run != 0, 0)) {             // most runs are empty: fall through
-			for (uint32_t l = run; l > 0; l--) {
-				e.bin(f, 1);
-				fr -= fr >> (3 + s);
-			}
+			if (__builtin_expect(run > (1u << 20), 0)) e.ovf |= 4;   // not a coefficient of this path
+			else
+				for (uint32_t l = run; l > 0; l--) {
+					e.bin(f, 1);
+					fr -= fr >> s3;
+				}
 		}
 		e.bin(f, 0);
 		if (SIGNED) e.bits(((sym & ((1u << k) - 1)) << 1) | sign, k + 1);
 		else if (k > 0) e.bits(sym & ((1u << k) - 1), k);
-		fr = (fr + ((4096u - fr) >> (3 + s))) & 0xFFFFu;
-		const uint32_t t0 = thr & 0xFFFFu, t1 = thr >> 16;
-		if (__builtin_expect(((fr - t0) & 0xFFFFu) > t1 - t0, 0)) {
+		fr = (fr + ((4096u - fr) >> s3)) & 0xFFFFu;
+		if (__builtin_expect(((fr - t0) & 0xFFFFu) > span, 0)) {
 			if (fr < t0) { if (idx < 24) idx++; }
 			else if (idx > 0) idx--;
 			if (idx >= 9) fr = 2048;
@@ -921,7 +929,11 @@ struct GDec {
 		uint32_t c = enum_code(cnk, kk, 16);
 		if (c >= lim) c = 0;                                 // the host reads code 0 past C(16, k) (corrupt streams)
 		const uint32_t i = off + c;
-		const uint32_t m = (etab[i >> 1] >> ((i & 1) * 16)) & 0xFFFFu;
+		// a global-address-space load made wave-uniform: a load through a generic
+		// (flat) pointer counts as divergent to the compiler, and a divergent
+		// pattern would turn the whole decoder (every value the coefficient loop
+		// touches) into per-lane VGPR code with exec-mask branches
+		const uint32_t m = (__builtin_amdgcn_readfirstlane(*gld(etab + (i >> 1))) >> ((i & 1) * 16)) & 0xFFFFu;
 		return comp ? ~m & 0xFFFFu : m;
 	}
 	GC_DI uint32_t max_dec(uint32_t max)                 // maxDecode, muxcodec.cpp:526-534
@@ -986,8 +998,13 @@ struct GBitD {                                          // CBitCodec::decode, bi
 };
 
 struct GGeoD {                                          // one CGeomCodec context in scalars (as GGeoCtx)
-	uint32_t freq, idx, k, s, thr;
-	GC_DI void params(const GTabs& T) { const uint32_t ks = lget(T.geo_ks, idx); k = ks & 0xFFu; s = ks >> 8; thr = lget(T.geo_thr, s); }
+	uint32_t freq, idx, k, s3, t0, span;
+	GC_DI void params(const GTabs& T)
+	{
+		const uint32_t ks = lget(T.geo_ks, idx), s = ks >> 8;
+		const uint32_t thr = lget(T.geo_thr, s);
+		k = ks & 0xFFu; s3 = s + 3; t0 = thr & 0xFFFFu; span = (thr >> 16) - t0;
+	}
 	GC_DI void load(uint32_t arr, uint32_t c, const GTabs& T) { const uint32_t v = lget(arr, c); freq = v & 0xFFFFu; idx = v >> 16; params(T); }
 	GC_DI uint32_t packed() const { return freq | idx << 16; }
 	// SIGNED: magnitude - 1 then the raw sign (decoder.cpp GeoReg::decode_signed);
@@ -999,7 +1016,7 @@ struct GGeoD {                                          // one CGeomCodec contex
 		uint32_t fr = freq, l = 0;
 		if (__builtin_expect(d.bit(f), 0)) {             // most runs are empty: fall through
 			do {
-				fr -= fr >> (3 + s);
+				fr -= fr >> s3;
 				if (++l > lmax) break;
 				d.ensure();
 			} while (d.bit(f));
@@ -1013,9 +1030,8 @@ struct GGeoD {                                          // one CGeomCodec contex
 			if (k > 0) l = (l << k) | d.bits(k);
 			out = (int)l;
 		}
-		fr = (fr + ((4096u - fr) >> (3 + s))) & 0xFFFFu;
-		const uint32_t t0 = thr & 0xFFFFu, t1 = thr >> 16;
-		if (__builtin_expect(((fr - t0) & 0xFFFFu) > t1 - t0, 0)) {
+		fr = (fr + ((4096u - fr) >> s3)) & 0xFFFFu;
+		if (__builtin_expect(((fr - t0) & 0xFFFFu) > span, 0)) {
 			if (fr < t0) { if (idx < 24) idx++; }
 			else if (idx > 0) idx--;
 			if (idx >= 9) fr = 2048;

@@ -17,7 +17,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "librududu_amd.so")
+# RIC_AMD_LIB: another build of the library (A/B runs of a variant in one box call)
+LIB_PATH = os.environ.get("RIC_AMD_LIB") or os.path.join(HERE, "librududu_amd.so")
 
 RIC_OK, RIC_E_ARG, RIC_E_HIP, RIC_E_CAPACITY, RIC_E_FORMAT, RIC_E_STREAM = 0, -1, -2, -3, -4, -5
 CDF97, CDF53, HAAR = 0, 1, 2
