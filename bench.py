@@ -634,15 +634,22 @@ def main():
     # to code one whole stream, with every stream of the launch in flight)
     coder = None
     if hybrid:
-        coder = {"streams_per_launch": b.cp_pool, "frames_host_round_trip": n_host,
-                 # rocprofv3 --pmc SQ_INSTS_SALU / GRBM_GUI_ACTIVE over scripts/gc_probe.py (not measurable
-                 # inside this process): SALU instructions per CU per cycle at 1920 1080p streams in flight
-                 "salu_frac": {"encode": 0.489, "decode": 0.488, "decode_first_launch": 0.649,
-                               "issue_frac_all_types": {"encode": 0.564, "decode": 0.586},
-                               "source": "profiles/r03_stream_coder_salu.json",
-                               "note": "k_gc_encode / k_gc_decode over 1920 1080p streams in two side-by-side "
-                                       "launches (scripts/gc_probe.py), before the merged launch, the priority "
-                                       "schedule and the enumDecode table fix"}}
+        coder = {"streams_per_launch": b.cp_pool, "frames_host_round_trip": n_host}
+        # the coder's issue counters (SQ_INSTS_SALU / VALU, SQ_WAIT_ANY, ... per stream)
+        # cannot be read inside this process: rocprofv3 --pmc over one serving step
+        # of this path at C3 (scripts/gpu_sq.sh), committed under profiles/
+        sqf = os.path.join(REPO, "profiles", "r04_stream_coder_sq.json")
+        if os.path.exists(sqf) and a.workload == "C3":
+            try:
+                sq = json.load(open(sqf))
+                run = sq["runs"]["r4g_v2"]
+                coder["issue"] = {k: run[k] for k in ("kernel_s", "SQ_INSTS_SALU", "SQ_INSTS_VALU", "salu_share",
+                                                       "instr_per_simd_per_4_cycles", "salu_per_cu_cycle", "wait_frac")
+                                  if k in run}
+                coder["issue"]["source"] = "profiles/r04_stream_coder_sq.json runs.r4g_v2 (per stream, %d streams in " \
+                                           "one k_gc_roundtrip launch)" % sq["streams"]
+            except (OSError, ValueError, KeyError):
+                pass
         if balance:
             coder["balance"] = balance
         for k, name in (("gpu_enc", "encode"), ("gpu_dec", "decode"), ("gpu_rt", "encode_then_decode")):

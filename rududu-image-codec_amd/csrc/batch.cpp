@@ -300,8 +300,12 @@ int lambda_of(int q, int p) { return q ? quants(q + 13 + (p ? 8 : 0)) : 0; }
 // around the level kernels only (not the copies), or null
 int d2h_slots(ric_batch* b, int set, int n);
 
+// pool (the GPU stream coder's pool, pstr bytes per frame): regions A and B
+// of frame i go to pool + i * pstr instead of its arena -- written there by
+// the level kernels directly when every level is a fused one (region C, the
+// scratch, stays in the arena), else copied there after the levels.
 int gpu_encode_plane(ric_batch* b, int set, int n, int p, const uint8_t* const* pix, int q, int trans, bool d2h = true,
-                     int abase = -1, int amul = 1, uint32_t* yflag = nullptr)
+                     int abase = -1, int amul = 1, uint32_t* yflag = nullptr, char* pool = nullptr, size_t pstr = 0)
 {
 	YieldFlag yf(yflag, b->st);
 	if (yf.raise()) return RIC_E_HIP;
@@ -309,6 +313,18 @@ int gpu_encode_plane(ric_batch* b, int set, int n, int p, const uint8_t* const* 
 	const int s0 = set * b->slots;
 	if (abase < 0) abase = s0;
 	const size_t ast = (size_t)amul * b->astride;
+	bool direct = pool != nullptr;
+	if (pool) {
+		// direct writes need every level fused, the coarsest with the LL TSUQ
+		P.set_weight(trans);
+		const int lambda = lambda_of(q, p);
+		int qin = quant_of(q, p);
+		for (int l = 0; l < P.nlev && direct; l++) {
+			const int mode = fwdq_mode(P.L[l], trans, level_qp(P, l, qin, lambda), 1);
+			direct = mode != FQ_NONE && (l + 1 < P.nlev || mode == FQ_GENERIC);
+		}
+		if (direct) BCHK(hipMemset2DAsync(pool + P.status_off, pstr, 0, sizeof(int32_t), n, b->st));
+	}
 	if (p == 0) {
 		auto sp = b->prof.begin(B_PIXIN, n, b->st);
 		for (int i = 0; i < n; i++) launch_pix_in(pix[i], b->plane(s0 + i, 0), b->w, b->h, b->pitch, b->channels, q, b->st);
@@ -323,6 +339,10 @@ int gpu_encode_plane(ric_batch* b, int set, int n, int p, const uint8_t* const* 
 		ZFrames fr;
 		fr.arena = b->arena(abase); fr.astride = ast; fr.nz = n;
 		fr.ring = b->fq_ring;
+		if (direct) {
+			fr.arena = pool; fr.astride = pstr;
+			fr.scratch = b->arena(abase); fr.scstride = ast; fr.split = P.b_end;
+		}
 		if (l == 0) {
 			fr.src = b->plane(s0, p); fr.sstride = b->pstride; fr.sp = b->pitch;
 		} else {
@@ -366,7 +386,9 @@ int gpu_encode_plane(ric_batch* b, int set, int n, int p, const uint8_t* const* 
 	}
 	BCHK(hipGetLastError());
 	if (yf.lower()) return RIC_E_HIP;
-	if (!d2h) return RIC_OK;
+	if (pool && !direct)
+		BCHK(hipMemcpy2DAsync(pool, pstr, b->arena(abase), ast, P.b_end, n, hipMemcpyDeviceToDevice, b->st));
+	if (!d2h || pool) return RIC_OK;
 	if (abase != s0 || amul != 1) return RIC_E_ARG;      // the host mirrors follow the slots
 	return d2h_slots(b, set, n);
 }
@@ -458,13 +480,16 @@ int h2d_slots(ric_batch* b, int set, int n)
 // The GPU half of DecompressImage for plane p of n frames of set `set`: the
 // host-decoded bands to the device (one strided copy), then every inverse
 // level with the fused TSUQi factors of each frame, as one launch per level.
+// pool (as gpu_encode_plane): the decoded bands of frame i are read from
+// pool + i * pstr (region A) while the inverse's intermediate LL planes
+// (region C) stay in the frame's arena -- no copy of the bands.
 int gpu_decode_plane(ric_batch* b, int set, int n, int p, const int* qs, int trans, bool h2d = true, int abase = -1,
-                     int amul = 1, uint32_t* yflag = nullptr)
+                     int amul = 1, uint32_t* yflag = nullptr, char* pool = nullptr, size_t pstr = 0)
 {
 	Pyramid& P = b->P;
 	const int s0 = set * b->slots;
 	if (abase < 0) abase = s0;
-	if (h2d && (abase != s0 || amul != 1)) return RIC_E_ARG;
+	if (h2d && (abase != s0 || amul != 1 || pool)) return RIC_E_ARG;
 	const size_t ast = (size_t)amul * b->astride;
 	if (h2d) {
 		const int r = h2d_slots(b, set, n);
@@ -478,6 +503,10 @@ int gpu_decode_plane(ric_batch* b, int set, int n, int p, const int* qs, int tra
 		const Level& L = P.L[l];
 		ZFrames fr;
 		fr.arena = b->arena(abase); fr.astride = ast; fr.nz = n;
+		if (pool) {
+			fr.arena = pool; fr.astride = pstr;
+			fr.scratch = b->arena(abase); fr.scstride = ast; fr.split = P.b_end;
+		}
 		int out_int;
 		if (l == 0) {
 			fr.out = b->plane(s0, p); fr.ostride = b->pstride; fr.po = b->pitch; out_int = 0;
@@ -1396,10 +1425,10 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 		for (int g0 = 0; g0 < m; g0 += S) {
 			const int gm = std::min(S, m - g0);
 			for (int p = 0; p < C; p++) {                   // (p 0 converts every plane's pixels)
-				int r = gpu_encode_plane(b, 0, gm, p, pix + f0 + g0, q, trans, false);
+				// the bands + records straight into the pool (the arenas keep the scratch)
+				int r = gpu_encode_plane(b, 0, gm, p, pix + f0 + g0, q, trans, false, -1, 1, nullptr,
+				                         abslot(h, g0) + (size_t)p * c.abstride, c.fstride);
 				if (r) return r;
-				BCHK(hipMemcpy2DAsync(abslot(h, g0) + (size_t)p * c.abstride, c.fstride, b->arena(0), b->astride, P.b_end, gm,
-				                      hipMemcpyDeviceToDevice, b->st));
 			}
 		}
 		BCHK(hipEventRecord(c.ev_fwd[h], b->st));
@@ -1591,9 +1620,9 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 		for (int g0 = 0; g0 < m; g0 += S) {
 			const int gm = std::min(S, m - g0);
 			for (int p = 0; p < C; p++) {
-				BCHK(hipMemcpy2DAsync(b->arena(0), b->astride, abslot(h, g0) + (size_t)p * c.abstride, c.fstride, P.a_end, gm,
-				                      hipMemcpyDeviceToDevice, b->st));
-				int r = gpu_decode_plane(b, 0, gm, p, qs.data(), trans, false);
+				// the inverse reads the decoded bands in the pool
+				int r = gpu_decode_plane(b, 0, gm, p, qs.data(), trans, false, -1, 1, nullptr,
+				                         abslot(h, g0) + (size_t)p * c.abstride, c.fstride);
 				if (r) return r;
 			}
 			int r = gpu_pix_out(b, 0, gm, qs.data(), pix_out + f0 + g0, 1, f0 + g0);

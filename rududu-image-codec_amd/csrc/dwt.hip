@@ -2459,7 +2459,8 @@ void fwd_launch(const Level& L, const void* src, long sp, char* arena, int vec, 
 }
 
 template <typename TB, typename TO>
-InvArgs<TB, TB, TO> inv_args(const Level& L, const Band& lls, char* arena, void* out, long po, const int* q, int S)
+InvArgs<TB, TB, TO> inv_args(const Level& L, const Band& lls, char* arena, void* out, long po, const int* q, int S,
+                             char* scratch = nullptr, size_t split = 0)
 {
 	InvArgs<TB, TB, TO> a;
 	memset(&a, 0, sizeof a);
@@ -2467,7 +2468,8 @@ InvArgs<TB, TB, TO> inv_args(const Level& L, const Band& lls, char* arena, void*
 	a.ovec = (po % 4 == 0) && ((uintptr_t)out % 16 == 0);
 	a.nofast = dbg_nofast();
 	for (int b = 0; b < 3; b++) { a.d[b] = (const TB*)(arena + L.b[b].off); a.p[b] = L.b[b].pitch; }
-	a.ll = (const TB*)(arena + lls.off); a.pl = lls.pitch;
+	// split arenas (ZFrames): the LL input from scratch when it lies in region C
+	a.ll = (const TB*)((scratch && lls.off >= split ? scratch : arena) + lls.off); a.pl = lls.pitch;
 	a.out = (TO*)out; a.po = po;
 	a.W = L.w; a.H = L.h;
 	a.nseg = (L.h + S - 1) / S;
@@ -2549,10 +2551,12 @@ int fwdq_mode(const Level& L, int trans, const QuantParams& qp, int vec16)
 namespace {
 // The arguments of a fused level launch over one frame's arena.  gen: the
 // generic kernel (k_fwdq_gen), else the packed ring forms.
+// scratch (split arenas, ZFrames): offsets from P.b_end on (region C) there
 FqArgs fq_args(const Pyramid& P, int l, const void* src, long sp, int vec8, int vec16, const QuantParams& qp,
-               char* arena, bool gen)
+               char* arena, bool gen, char* scratch = nullptr)
 {
 	const Level& L = P.L[l];
+	auto at = [&](size_t off) { return (scratch && off >= P.b_end ? scratch : arena) + off; };
 	FqArgs a;
 	memset(&a, 0, sizeof a);   // (padding too: batched launches compare argument images)
 	a.wgt = nullptr;
@@ -2564,16 +2568,16 @@ FqArgs fq_args(const Pyramid& P, int l, const void* src, long sp, int vec8, int 
 	} else {
 		a.vec16 = vec16; a.nofast = dbg_nofast(); a.pk = 1;
 	}
-	for (int b = 0; b < 4; b++) { a.d[b] = (int16_t*)(arena + L.b[b].off); a.p[b] = L.b[b].pitch; }
+	for (int b = 0; b < 4; b++) { a.d[b] = (int16_t*)at(L.b[b].off); a.p[b] = L.b[b].pitch; }
 	for (int b = 0; b < 3; b++) {
 		const Band& B = L.b[b];
 		a.dx[b] = B.dx; a.dy[b] = B.dy; a.bw[b] = B.bw(); a.bh[b] = B.bh();
-		a.rd[b] = (uint32_t*)(arena + B.rd_off);
-		a.rec[b] = (uint64_t*)(arena + P.rec_off[l][b]);
+		a.rd[b] = (uint32_t*)at(B.rd_off);
+		a.rec[b] = (uint64_t*)at(P.rec_off[l][b]);
 		if (l > 0) {
 			const Band& C = P.L[l - 1].b[b];
-			a.crd[b] = (const uint32_t*)(arena + C.rd_off); a.cbw[b] = C.bw();
-			a.cpin[b] = (uint8_t*)(arena + P.pin_off[l - 1][b]); a.cpw[b] = C.bw(); a.cph[b] = C.bh();
+			a.crd[b] = (const uint32_t*)at(C.rd_off); a.cbw[b] = C.bw();
+			a.cpin[b] = (uint8_t*)at(P.pin_off[l - 1][b]); a.cpw[b] = C.bw(); a.cph[b] = C.bh();
 		} else {
 			a.crd[b] = nullptr; a.cbw[b] = 0;
 			a.cpin[b] = nullptr; a.cpw[b] = 0; a.cph[b] = 0;
@@ -2581,7 +2585,7 @@ FqArgs fq_args(const Pyramid& P, int l, const void* src, long sp, int vec8, int 
 		a.Q[b] = qp.Q[b]; a.iQ[b] = qp.iQ[b];
 		for (int i = 0; i < 16; i++) a.thres[b][i] = qp.thres[b][i];
 	}
-	a.err = (int*)(arena + P.status_off);
+	a.err = (int*)at(P.status_off);
 	a.fault = gen ? 0 : g_ring_fault.load(std::memory_order_relaxed);
 	return a;
 }
@@ -2680,7 +2684,8 @@ int launch_fwdq_level_z(const Pyramid& P, int l, const ZFrames& fr, int vec8, in
 	const int S = pc_seg_rows_z(L.w, L.h, fr.nz, l);
 	std::vector<FqArgs> v(fr.nz);
 	for (int f = 0; f < fr.nz; f++) {
-		v[f] = fq_args(P, l, (const char*)fr.src + f * fr.sstride, fr.sp, vec8, vec16, qp, fr.arena + f * fr.astride, false);
+		v[f] = fq_args(P, l, (const char*)fr.src + f * fr.sstride, fr.sp, vec8, vec16, qp, fr.arena + f * fr.astride, false,
+		               fr.scratch ? fr.c_base(f) : nullptr);
 		v[f].nseg = (L.h + S - 1) / S;
 	}
 	if (zargs_put(z, v.data(), v.size() * sizeof(FqArgs), st)) return -1;
@@ -2712,7 +2717,8 @@ int launch_fwdq_gen_level_z(const Pyramid& P, int l, const ZFrames& fr, int vec8
 	const int nseg = (L.h + GR - 1) / GR;
 	std::vector<FqArgs> v(fr.nz);
 	for (int f = 0; f < fr.nz; f++) {
-		v[f] = fq_args(P, l, (const char*)fr.src + f * fr.sstride, fr.sp, vec8, 0, qp, fr.arena + f * fr.astride, true);
+		v[f] = fq_args(P, l, (const char*)fr.src + f * fr.sstride, fr.sp, vec8, 0, qp, fr.arena + f * fr.astride, true,
+		               fr.scratch ? fr.c_base(f) : nullptr);
 		v[f].nseg = nseg;
 	}
 	if (zargs_put(z, v.data(), v.size() * sizeof(FqArgs), st)) return -1;
@@ -2752,7 +2758,7 @@ int inv_launch_z(const Level& L, const Band& lls, const ZFrames& fr, int nz, con
 	std::vector<InvArgs<TB, TB, TO>> v(nz);
 	for (int f = 0; f < nz; f++)
 		v[f] = inv_args<TB, TO>(L, lls, fr.arena + f * fr.astride, (char*)fr.out + f * fr.ostride, fr.po,
-		                        q ? q + 4 * f : nullptr, S);
+		                        q ? q + 4 * f : nullptr, S, fr.scratch ? fr.c_base(f) : nullptr, fr.split);
 	if (zargs_put(z, v.data(), v.size() * sizeof(v[0]), st)) return -1;
 	const dim3 grid((L.w + kStripValid - 1) / kStripValid, (v[0].nseg + kWavesPerBlock - 1) / kWavesPerBlock, nz);
 	hipLaunchKernelGGL((k_inv_z<TRANS, TB, TB, TO, S>), grid, dim3(256), 0, st, (const InvArgs<TB, TB, TO>*)z.dev);

@@ -29,6 +29,13 @@
 #include "coder_tables.h"
 #include "gcoder.h"
 
+#ifndef RIC_GC_UNIFORM
+#define RIC_GC_UNIFORM 0
+#endif
+#ifndef RIC_GC_ELOW_V
+#define RIC_GC_ELOW_V 0
+#endif
+
 namespace ric {
 
 #include "huff_tables.inc"
@@ -220,7 +227,11 @@ struct GEnc {
 		uint32_t it = 0;
 		do {
 			put(q0, low >> 24);
+#if RIC_GC_ELOW_V
+			range = __builtin_amdgcn_readfirstlane(((low + range - 1) ^ low) >= 0x01000000u ? (0u - low) & 4095u : range);
+#else
 			if (((low + range - 1) ^ low) >= 0x01000000u) range = (0u - low) & 4095u;
+#endif
 			q0 = q1; q1 = q2; q2 = q3; q3 = p++;
 			range <<= 8;
 			low <<= 8;
@@ -245,7 +256,12 @@ struct GEnc {
 	GC_DI void init(uint8_t* o, uint32_t c, uint32_t base)   // init_encoder at out + base
 	{
 		out = o; cap = c;
-		low = 0; range = 1u << 16;
+#if RIC_GC_ELOW_V
+		low = to_vgpr(0u);                               // (experiment: the coder's low on the VALU)
+#else
+		low = 0;
+#endif
+		range = 1u << 16;
 		ebits = 0; ebuf = 0;
 		reserved = 0;
 		q0 = base; q1 = base + 1; q2 = base + 2; q3 = base + 3;
@@ -929,11 +945,20 @@ struct GDec {
 		uint32_t c = enum_code(cnk, kk, 16);
 		if (c >= lim) c = 0;                                 // the host reads code 0 past C(16, k) (corrupt streams)
 		const uint32_t i = off + c;
-		// a global-address-space load made wave-uniform: a load through a generic
-		// (flat) pointer counts as divergent to the compiler, and a divergent
-		// pattern would turn the whole decoder (every value the coefficient loop
-		// touches) into per-lane VGPR code with exec-mask branches
+		// RIC_GC_UNIFORM: the pattern made wave-uniform (a global-address-space
+		// load + readfirstlane).  Read through the generic pointer (the default)
+		// the compiler counts it as divergent, and the decoder state the
+		// coefficient loop touches lives in VGPRs with exec-mask branches: about
+		// half the decoder's instructions go to the VALU instead of the scalar
+		// unit.  Measured (C3 serving step, 2816 streams, k_gc_roundtrip per
+		// stream): divergent 1313 M SALU + 1323 M VALU, 11.94 s per launch;
+		// uniform 2229 M SALU + 366 M VALU, 13.02 s.  With ~3 coder waves per
+		// SIMD the scalar unit is the shared port: the balanced mix issues more.
+#if RIC_GC_UNIFORM
 		const uint32_t m = (__builtin_amdgcn_readfirstlane(*gld(etab + (i >> 1))) >> ((i & 1) * 16)) & 0xFFFFu;
+#else
+		const uint32_t m = (etab[i >> 1] >> ((i & 1) * 16)) & 0xFFFFu;
+#endif
 		return comp ? ~m & 0xFFFFu : m;
 	}
 	GC_DI uint32_t max_dec(uint32_t max)                 // maxDecode, muxcodec.cpp:526-534

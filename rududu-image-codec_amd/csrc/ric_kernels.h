@@ -77,6 +77,12 @@ struct ZFrames {
 	// workgroup) or the double buffer (0, 20 KiB: more workgroups fit beside
 	// the stream coder's waves)
 	int ring = 1;
+	// Split arenas (the GPU stream coder's pool): regions A and B (bands,
+	// status word, records, parent info: offsets below `split` = Pyramid::b_end)
+	// of frame f at arena + f * astride, region C (intermediate LL planes, pRD)
+	// at scratch + f * scstride.  scratch null: one arena per frame.
+	char* scratch = nullptr; size_t scstride = 0; size_t split = 0;
+	char* c_base(int f) const { return scratch ? scratch + (size_t)f * scstride : arena + (size_t)f * astride; }
 };
 // Per-frame argument array of one batched launch, on the device; re-uploaded
 // (after a stream sync) only when it changes.
