@@ -1217,9 +1217,11 @@ int ric_batch_hybrid_config(ric_batch* b, int pool_frames, size_t stream_cap)
 		// stream's own copies until the kernel ended (seconds)
 		BCHK(hipHostMalloc(&c.h_res, sizeof(uint32_t) * 6 * c.n, hipHostMallocMapped | hipHostMallocCoherent));
 		BCHK(hipHostGetDevicePointer((void**)&c.d_res, c.h_res, 0));
-		BCHK(hipHostMalloc(&c.h_post, sizeof(uint32_t) * 4 * c.n, hipHostMallocCoherent | hipHostMallocMapped));
+		// posted words: the encoder's two per frame of both halves, then the
+		// round trip's decode word per frame of both
+		BCHK(hipHostMalloc(&c.h_post, sizeof(uint32_t) * 6 * c.n, hipHostMallocCoherent | hipHostMallocMapped));
 		BCHK(hipHostGetDevicePointer((void**)&c.d_post, c.h_post, 0));
-		memset(c.h_post, 0, sizeof(uint32_t) * 4 * c.n);
+		memset(c.h_post, 0, sizeof(uint32_t) * 6 * c.n);
 		if (!c.d_args) BCHK(hipMalloc(&c.d_args, 3 * sizeof(GEncArgs)));   // the halves, then both as one launch
 		if (!c.d_dargs) BCHK(hipMalloc(&c.d_dargs, 3 * sizeof(GDecArgs)));
 		for (int h = 0; h < 2; h++) {
@@ -1371,6 +1373,7 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 	static const bool fuse = [] { const char* e = getenv("RIC_GC_FUSE"); return !e || atoi(e) != 0; }();
 	// each coder launch's tag (launch_gc_encode): its posted result words carry it
 	std::vector<uint32_t> tagj(nbatch > 0 ? nbatch : 1, 0);
+	bool fused = false;                                    // batches 0 and 1 run as one k_gc_roundtrip
 	auto next_tag = [&]() {
 		c.epoch = (c.epoch + 1) & 0xFFFFFu;
 		if (!c.epoch) c.epoch = 1;
@@ -1484,8 +1487,9 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 		if (fuse && q != 0) {
 			// one kernel: each wave encodes its frame, posts the stream (the
 			// copiers take it from there at once) and decodes it
+			fused = true;
 			auto sp = b->prof.begin(B_GRT, m, c.st[0]);
-			if (launch_gc_roundtrip(c.d_args + 2, c.d_dargs + 2, c.d_post, tagj[0], m, c.st[0]))
+			if (launch_gc_roundtrip(c.d_args + 2, c.d_dargs + 2, c.d_post, c.d_post + 4 * (size_t)c.n, tagj[0], m, c.st[0]))
 				return bfail(hipGetLastError(), "k_gc_roundtrip") ? RIC_E_HIP : RIC_E_HIP;
 			b->prof.end(sp);
 			for (int j = 0; j < 2; j++) {
@@ -1522,6 +1526,50 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 	auto kick = [&](int j) -> int {
 		const int r = kick_fwd(j);
 		return r ? r : kick_coder(j, false);
+	};
+	// The inverse levels + pixel output of frames g0 .. g0 + S - 1 of GPU-decoded
+	// batch j (the inverse reads the decoded bands in the pool)
+	std::vector<std::vector<char>> hv_done(nbatch > 0 ? nbatch : 1);
+	for (int j = 0; j < nbatch; j++) hv_done[j].assign((batch_m(j) + S - 1) / S, 0);
+	int hv_early = 0;
+	auto harvest_group = [&](int j, int g0) -> int {
+		const int f0 = batch_f0(j), m = batch_m(j), h = j & 1;
+		const int gm = std::min(S, m - g0);
+		for (int p = 0; p < C; p++) {
+			int r = gpu_decode_plane(b, 0, gm, p, qs.data(), trans, false, -1, 1, nullptr,
+			                         abslot(h, g0) + (size_t)p * c.abstride, c.fstride);
+			if (r) return r;
+		}
+		const int r = gpu_pix_out(b, 0, gm, qs.data(), pix_out + f0 + g0, 1, f0 + g0);
+		hv_done[j][g0 / S] = 1;
+		return r;
+	};
+	// While the fused launch runs: a group whose frames have all posted their
+	// decode (k_gc_roundtrip's posted_dec words, this launch's tag, no failure)
+	// is harvested at once, beside the waves still decoding, instead of after
+	// the launch (RIC_EARLY_HARVEST=0: after the launch only)
+	static const bool early_on = [] { const char* e = getenv("RIC_EARLY_HARVEST"); return !e || atoi(e) != 0; }();
+	auto early_harvest = [&]() -> int {
+		if (!fused || !early_on) return RIC_OK;
+		const uint32_t want = 0x100u | tagj[0] << 12;
+		const uint32_t* pd = c.h_post + 4 * (size_t)c.n;       // frames of both halves, in pool order
+		for (int j = finished; j < 2 && j < nbatch; j++) {
+			const int m = batch_m(j);
+			for (int g0 = 0; g0 < m; g0 += S) {
+				if (hv_done[j][g0 / S]) continue;
+				const int gm = std::min(S, m - g0);
+				bool ok = true;
+				for (int k = 0; k < gm && ok; k++) {
+					const uint32_t w = __atomic_load_n(pd + (size_t)j * c.n + g0 + k, __ATOMIC_ACQUIRE);
+					ok = (w & ~0xFFu) == want && !(w & 0x80u) && (w & 15u) != 3u;
+				}
+				if (!ok) continue;
+				const int r = harvest_group(j, g0);
+				if (r) return r;
+				hv_early++;
+			}
+		}
+		return RIC_OK;
 	};
 	auto harvest = [&](int j) -> int {
 		const int f0 = batch_f0(j), m = batch_m(j), h = j & 1;
@@ -1618,14 +1666,8 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 			return RIC_OK;
 		}
 		for (int g0 = 0; g0 < m; g0 += S) {
-			const int gm = std::min(S, m - g0);
-			for (int p = 0; p < C; p++) {
-				// the inverse reads the decoded bands in the pool
-				int r = gpu_decode_plane(b, 0, gm, p, qs.data(), trans, false, -1, 1, nullptr,
-				                         abslot(h, g0) + (size_t)p * c.abstride, c.fstride);
-				if (r) return r;
-			}
-			int r = gpu_pix_out(b, 0, gm, qs.data(), pix_out + f0 + g0, 1, f0 + g0);
+			if (hv_done[j][g0 / S]) continue;                  // harvested while the launch ran
+			const int r = harvest_group(j, g0);
 			if (r) return r;
 		}
 		return RIC_OK;
@@ -1808,6 +1850,10 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 			if (rc) break;
 		}
 		if (rc) break;
+		if (finished < kicked) {
+			rc = early_harvest();
+			if (rc) break;
+		}
 		if (!fl.empty()) {
 			if (fl.front().done.wait_for_ms(finished < kicked ? 2 : 20)) {
 				rc = finish_group();
@@ -1824,6 +1870,7 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 	for (int h = 0; h < 2; h++)
 		if (c.st[h]) (void)hipStreamSynchronize(c.st[h]);
 	const bool ok = !bfail(hipStreamSynchronize(b->st), "hipStreamSynchronize");
+	if (trace) fprintf(stderr, "[hybrid] %d coder-frame groups harvested while the launch ran\n", hv_early);
 	tr("end", rc);
 	for (auto& e : evs) (void)hipEventDestroy(e);
 	if (rc == RIC_E_HIP) clear_status(b);

@@ -84,9 +84,11 @@ int launch_gc_encode(const GEncArgs* dev_args, int nframes, int lossless, hipStr
 
 // k_gc_roundtrip over n lossy frames: each wave encodes its frame (as
 // k_gc_encode), posts its result tagged as launch_gc_encode does, then decodes
-// the stream (as k_gc_decode, lens from the encoder).
-int launch_gc_roundtrip(const GEncArgs* dev_eargs, const GDecArgs* dev_dargs, uint32_t* posted, uint32_t tag, int nframes,
-                        hipStream_t st);
+// the stream (as k_gc_decode, lens from the encoder) and, with posted_dec,
+// posts that its bands are in memory: posted_dec[f] = the decoder's result
+// word (0x80 if the encode failed) | 0x100 | (tag & 0xFFFFF) << 12.
+int launch_gc_roundtrip(const GEncArgs* dev_eargs, const GDecArgs* dev_dargs, uint32_t* posted, uint32_t* posted_dec,
+                        uint32_t tag, int nframes, hipStream_t st);
 
 // Fill the band descriptors (coding order) of a pyramid.
 inline void gc_bands(const Pyramid& P, GBandDesc& ll, GBandDesc* b, int& nb)

@@ -1372,7 +1372,7 @@ __global__ void __launch_bounds__(64) k_gc_decode(const GDecArgs* __restrict__ a
 // k_gc_decode write.  A stream that failed is not decoded (result word 0).
 template <bool ETAB>
 __global__ void __launch_bounds__(64) k_gc_roundtrip(const GEncArgs* __restrict__ eap, const GDecArgs* __restrict__ dap,
-                                                    uint32_t* posted, uint32_t tag)
+                                                    uint32_t* posted, uint32_t* posted_dec, uint32_t tag)
 {
 	const GEncArgs& ea = *eap;
 	const GDecArgs& da = *dap;
@@ -1396,6 +1396,15 @@ __global__ void __launch_bounds__(64) k_gc_roundtrip(const GEncArgs* __restrict_
 	if (lane_id() == 0) {
 		gst(da.res)[f] = r;
 		if (da.ts) ts_put(da.ts, f, t_dec);
+	}
+	// the decoded bands are the harvest's input, read by kernels the host
+	// launches while this one still runs (on any XCD): written back (agent-scope
+	// release) before the word that announces them.  posted_dec[f] = the decoder's
+	// result (0x80: the encode failed) | 0x100 | tag << 12
+	if (posted_dec) {
+		__threadfence();
+		if (lane_id() == 0)
+			__hip_atomic_store(posted_dec + f, (rc ? 0x80u : r) | 0x100u | tag << 12, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 	}
 }
 }  // namespace
@@ -1484,8 +1493,8 @@ int launch_gc_flag(uint32_t* flag, uint32_t v, hipStream_t st)
 	return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_gc_roundtrip(const GEncArgs* dev_eargs, const GDecArgs* dev_dargs, uint32_t* posted, uint32_t tag, int nframes,
-                        hipStream_t st)
+int launch_gc_roundtrip(const GEncArgs* dev_eargs, const GDecArgs* dev_dargs, uint32_t* posted, uint32_t* posted_dec,
+                        uint32_t tag, int nframes, hipStream_t st)
 {
 	if (nframes <= 0) return 0;
 	// RIC_GC_ETAB=0 and RIC_GC_LDS act here as in the separate launches
@@ -1493,10 +1502,12 @@ int launch_gc_roundtrip(const GEncArgs* dev_eargs, const GDecArgs* dev_dargs, ui
 	if (etab) {
 		if (enum16_upload(st)) return -1;
 		static const size_t dyn = gc_dyn_lds((const void*)k_gc_roundtrip<true>);
-		hipLaunchKernelGGL(k_gc_roundtrip<true>, dim3(nframes), dim3(64), dyn, st, dev_eargs, dev_dargs, posted, tag & 0xFFFFFu);
+		hipLaunchKernelGGL(k_gc_roundtrip<true>, dim3(nframes), dim3(64), dyn, st, dev_eargs, dev_dargs, posted, posted_dec,
+		                   tag & 0xFFFFFu);
 	} else {
 		static const size_t dyn = gc_dyn_lds((const void*)k_gc_roundtrip<false>);
-		hipLaunchKernelGGL(k_gc_roundtrip<false>, dim3(nframes), dim3(64), dyn, st, dev_eargs, dev_dargs, posted, tag & 0xFFFFFu);
+		hipLaunchKernelGGL(k_gc_roundtrip<false>, dim3(nframes), dim3(64), dyn, st, dev_eargs, dev_dargs, posted, posted_dec,
+		                   tag & 0xFFFFFu);
 	}
 	return hipGetLastError() == hipSuccess ? 0 : -1;
 }
