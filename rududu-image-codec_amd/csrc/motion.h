@@ -64,7 +64,10 @@ int launch_vid_extend(const VidGeom& g, const VidSubs& s, int n, hipStream_t st)
 int launch_vid_epzs(const VidGeom& g, const int16_t* cur, const VidSubs& ref, uint32_t* mv, uint16_t* dist,
                     uint64_t* gran, uint32_t epoch, uint32_t* status, hipStream_t st);
 // COBMC::apply_mv (obmc.cpp:278-332) into pred, reference frame `ref`
-int launch_vid_obmc(const VidGeom& g, const uint32_t* mv, const VidSubs& ref, int16_t* pred, hipStream_t st);
+// residual != nullptr (the encoder): also residual = residual - prediction over
+// the whole w x h plane, in the same pass (CImage::operator-=, k_vid_addsub's -1)
+int launch_vid_obmc(const VidGeom& g, const uint32_t* mv, const VidSubs& ref, int16_t* pred, int16_t* residual,
+                    hipStream_t st);
 // the samples CWavelet2D::TransformI (given the plane's end pointer) leaves
 // outside the plane: its level-1 output, dx1 x dy1 at (row h - dy1, column
 // dimXAlign - dx1) of the plane, wrapping into the next row's left border

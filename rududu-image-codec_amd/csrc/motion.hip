@@ -250,62 +250,27 @@ __global__ __launch_bounds__(64) void k_vid_epzs_full(EpzsArgs a)
 			for (int k = 1; k < n; k++)                     // sets B and C (:151-161)
 				if (cand[k] != kVidIntra && bd > sd[k]) { best = cand[k]; bd = sd[k]; }
 			// DiamondSearch (obme.cpp:79-108): the four neighbours of the
-			// centre, never straight back along the last two moves.  The
-			// SADs come two steps at a time: one round of loads covers the
-			// 12 positions within two unit moves of the centre (lane k of
-			// vsd: ring 1 in the step order up, down, left, right, then
-			// (0,-2) (0,2) (-2,0) (2,0) (-1,-1) (1,-1) (-1,1) (1,1); lane 12,
-			// the centre, is never taken: going back is excluded), and the
-			// second step reads its four candidates there (kStep2) instead
-			// of waiting on another round of loads.
-			constexpr int kOx[12] = {0, 0, -1, 1, 0, 0, -2, 2, -1, 1, -1, 1};
-			constexpr int kOy[12] = {-1, 1, 0, 0, -2, 2, 0, 0, -1, -1, 1, 1};
-			// step-2 candidates (up, down, left, right) after step-1 move m,
-			// 4 bits each, up in the high nibble of m's 16 bits
-			constexpr uint64_t kStep2 = 0x4C89ull | 0xC5ABull << 16 | 0x8A6Cull << 32 | 0x9BC7ull << 48;
+			// centre, never straight back along the last two moves; one step
+			// per round of 4 loads.  (Loading the 12 positions within two
+			// moves to take two steps per round halves the rounds but was
+			// slower: 2.58 against 1.97 ms per 1080p frame)
 			const int dx[4] = {0, 0, -1, 1}, dy[4] = {-1, 1, 0, 0};
 			const int tst[4] = {kDown, kUp, kRight, kLeft}, stp[4] = {kUp, kDown, kLeft, kRight};
 			int last = 0, last2 = 0;
-			for (int it = 0; it < 65536; it += 2) {
+			for (int it = 0; it < 65536; it++) {
 				const int bxv = mvx(best), byv = mvy(best);
-				int q[12];
+				int d4[4];
 #pragma unroll
-				for (int k = 0; k < 12; k++)
-					q[k] = ref_px(ref, a, cx + (int16_t)(bxv + kOx[k]), cy + (int16_t)(byv + kOy[k]), lane);
-				int vsd = 0x7FFFFFFF;
+				for (int k = 0; k < 4; k++)
+					d4[k] = sad_of(abs(cur - ref_px(ref, a, cx + (int16_t)(bxv + dx[k]), cy + (int16_t)(byv + dy[k]), lane)));
+				int move = 0;
 #pragma unroll
-				for (int k = 0; k < 12; k++) {
-					const int d = sad_of(abs(cur - q[k]));
-					vsd = lane == k ? d : vsd;
-				}
-				// step 1: ring 1, lanes 0..3
-				int move = 0, mk = 0;
-#pragma unroll
-				for (int k = 0; k < 4; k++) {
-					const int d = __builtin_amdgcn_readlane(vsd, k);
-					if (!(last2 & tst[k]) && bd > d) {
+				for (int k = 0; k < 4; k++)
+					if (!(last2 & tst[k]) && bd > d4[k]) {
 						best = mvmake(bxv + dx[k], byv + dy[k]);
-						bd = d;
-						move = stp[k];
-						mk = k;
-					}
-				}
-				last2 = move | last;
-				last = move;
-				if (!last) break;
-				// step 2 from the new centre, candidates from the same round
-				const int b2x = mvx(best), b2y = mvy(best);
-				move = 0;
-#pragma unroll
-				for (int k = 0; k < 4; k++) {
-					const int idx = (int)((kStep2 >> (16 * mk + 4 * (3 - k))) & 15u);
-					const int d = __builtin_amdgcn_readlane(vsd, idx);
-					if (!(last2 & tst[k]) && bd > d) {
-						best = mvmake(b2x + dx[k], b2y + dy[k]);
-						bd = d;
+						bd = d4[k];
 						move = stp[k];
 					}
-				}
 				last2 = move | last;
 				last = move;
 				if (!last) break;
@@ -370,10 +335,6 @@ __global__ __launch_bounds__(64) void k_vid_epzs_sub(EpzsArgs a)
 }
 
 // ----------------------------------------------------------------- OBMC
-__constant__ int16_t kWin[8][8] = {                      // COBMC::window, obmc.cpp:56-66
-	{0, 0, 0, 0, 1, 1, 1, 1},   {0, 0, 1, 1, 1, 2, 2, 2},   {0, 1, 1, 2, 2, 3, 4, 4},    {0, 1, 2, 3, 4, 5, 6, 6},
-	{1, 1, 2, 4, 5, 7, 8, 9},   {1, 2, 3, 5, 7, 9, 9, 11}, {1, 2, 4, 6, 8, 9, 12, 13}, {1, 2, 4, 6, 9, 11, 13, 14}};
-
 // COBMC::apply_mv (obmc.cpp:278-332) gathered per output sample.  Block
 // (bi, bj) writes a 16x16 window at (8 bi - 4, 8 bj - 4) in raster order, so a
 // sample receives, in order, the bottom-right quadrant of block (a-1, b-1),
@@ -385,77 +346,148 @@ __constant__ int16_t kWin[8][8] = {                      // COBMC::window, obmc.
 // first statement is the previous prediction (the LEFT column's first
 // statement accumulates onto it: obmc.cpp:158).  Intra blocks contribute 0
 // (obmc_block_intra, :179-250).
-// One workgroup per 64-column x 16-row tile (a lane per column, four rows at
-// a time): the rows of a tile re-read the same source windows (a block's
-// window spans 16 rows), so they share the CU's L1 and the XCD's L2 instead
-// of being fetched once per row by workgroups spread over the XCDs.
-constexpr int kObmcRows = 16;
-__device__ __forceinline__ void obmc_sample(const VidSubs& ref, const uint32_t* __restrict__ mv, int16_t* __restrict__ pred,
-                                            int w, int h, int S, long pc, int bx, int by, int x, int y);
-__global__ __launch_bounds__(256) void k_vid_obmc(VidSubs ref, const uint32_t* __restrict__ mv, int16_t* __restrict__ pred,
-                                                  int w, int h, int S, long P, int bx, int by)
+// One workgroup per 64-column x 4 RW-row tile, a lane per column, wave w
+// owning tile rows w RW .. w RW + RW - 1.  Every (block, window sample) pair
+// feeds exactly one output sample, so the 12 B per sample are already the
+// minimum.  The tile's blocks (10 columns x (RW/2 + 2) rows around it) are
+// resolved once into a window-origin address in LDS (motion vector ->
+// quarter-pel plane, get_pos clamping; 1 = intra, 0 = outside the frame); a
+// lane then issues its RW prediction loads and all 4 RW window gathers before
+// the first statement, so a tile costs two dependent memory trips (vectors,
+// then samples) rather than two per quadrant.  The quadrant of each of the
+// four contributions is static (k = 0..3: bottom-right, bottom-left,
+// top-right, top-left), the window row is wave-uniform and the column is the
+// lane's (x + 4) mod 8, so the weights are nibbles of two packed window rows.
+// What bounds it: the windows' 32-byte rows sit in lines of
+// their own when neighbouring blocks' vectors differ, so the L2 fetches whole
+// lines for a quarter of their bytes; staging the window rows in LDS with
+// aligned 16-byte loads (a quarter of the load instructions) and a persistent
+// one-wave-per-strip form that prefetches the next strip's vectors were both
+// slower (52.9 and 42.5 us against 40.7 at 1080p).
+__constant__ uint32_t kWinRow[8] = {   // COBMC::window (obmc.cpp:56-66): window[j][i] at bits 4 i of word j
+	0x11110000u, 0x22211100u, 0x44322110u, 0x66543210u, 0x98754211u, 0xB9975321u, 0xDC986421u, 0xEDB96421u};
+
+// one statement of obmc_block<flags> (obmc.cpp:80-177) for the quadrant (top, left) of a block with
+// edge flags T, Bo, L, R at window row jj / column cu, stored to short as the reference stores it
+__device__ __forceinline__ int obmc_statement(int dd, int sv, bool top, bool left, bool T, bool Bo, bool L, bool R, int jj,
+                                             int cu)
 {
-	const int x = blockIdx.x * 64 + threadIdx.x;
-	if (x >= 8 * bx) return;
-	const long pc = blockIdx.z * P;
-	const int y1 = min((int)(blockIdx.y + 1) * kObmcRows, 8 * by);
-	for (int y = blockIdx.y * kObmcRows + threadIdx.y; y < y1; y += 4) obmc_sample(ref, mv, pred, w, h, S, pc, bx, by, x, y);
+	const uint32_t rj = kWinRow[jj], rm = kWinRow[7 - jj];
+	const int wl = (rj >> (4 * cu)) & 15, wr = (rj >> (28 - 4 * cu)) & 15;
+	const int wlm = (rm >> (4 * cu)) & 15, wrm = (rm >> (28 - 4 * cu)) & 15;
+	int q;
+	if (top && left) {                             // top-left: the block's own quadrant
+		if (T && L) q = sv;
+		else if (T) q = (dd + sv * (wl + wlm) + 8) >> 4;
+		else if (L) q = (dd + sv * (wl + wr) + 8) >> 4;
+		else q = (dd + sv * wl + 8) >> 4;
+	} else if (top) {                              // top-right
+		if (T && R) q = sv;
+		else if (T) q = sv * (wr + wrm);
+		else if (R) q = (dd + sv * (wr + wl) + 8) >> 4;
+		else q = dd + sv * wr;
+	} else if (left) {                             // bottom-left
+		if (Bo && L) q = sv;
+		else if (Bo) q = (dd + sv * (wl + wlm) + 8) >> 4;
+		else if (L) q = dd + sv * (wl + wr);
+		else q = dd + sv * wl;
+	} else {                                       // bottom-right
+		if (Bo && R) q = sv;
+		else if (Bo) q = sv * (wr + wrm);
+		else if (R) q = sv * (wr + wl);
+		else q = sv * wr;
+	}
+	return (int16_t)q;
 }
 
-__device__ __forceinline__ void obmc_sample(const VidSubs& ref, const uint32_t* __restrict__ mv, int16_t* __restrict__ pred,
-                                            int w, int h, int S, long pc, int bx, int by, int x, int y)
+typedef const __attribute__((address_space(1))) int16_t* gsamples;
+
+template <int RW>
+__global__ __launch_bounds__(256) void k_vid_obmc(VidSubs ref, const uint32_t* __restrict__ mv, int16_t* __restrict__ pred,
+                                                  int16_t* __restrict__ img, int w, int h, int S, long P, int bx, int by,
+                                                  int ntx, int nty)
 {
-	const long o = pc + (long)y * S + x;
-	int d = pred[o];
-	const int a0 = (x + 4) >> 3, b0 = (y + 4) >> 3, cu = x + 4 - 8 * a0, cv = y + 4 - 8 * b0;
-#pragma unroll
-	for (int k = 0; k < 4; k++) {
-		const int bi = a0 - ((k & 1) ? 0 : 1), bj = b0 - ((k & 2) ? 0 : 1);
-		const int u = cu + ((k & 1) ? 0 : 8), v = cv + ((k & 2) ? 0 : 8);
-		if (bi < 0 || bi >= bx || bj < 0 || bj >= by) continue;
-		const bool T = bj == 0, Bo = bj == by - 1, L = bi == 0, R = bi == bx - 1;
-		const bool top = v < 8, left = u < 8;
-		const int jj = top ? v : 15 - v;                  // the window row (second loop counts down)
-		const int ii = left ? u : u - 8;
-		if (top ? jj < (T ? 4 : 0) : jj < (Bo ? 4 : 0)) continue;
-		if (left ? ii < (L ? 4 : 0) : ii >= (R ? 4 : 8)) continue;
-		const uint32_t m = mv[(long)bj * bx + bi];
-		int s = 0;
-		if (m != kVidIntra) {
-			const int mx = mvx(m), my = mvy(m);
-			int px = 8 * bi + (mx >> 2) - 4, py = 8 * bj + (my >> 2) - 4;   // get_pos, obmc.cpp:252-263
-			if (px < -15) px = -15;
-			if (px >= w) px = w - 1;
-			if (py < -15) py = -15;
-			if (py >= h) py = h - 1;
-			s = ref.p[((mx & 3) << 2) | (my & 3)][pc + (long)(py + v) * S + px + u];
+	constexpr int TR = 4 * RW, NJ = TR / 8 + 2, NI = 10;
+	__shared__ unsigned long long blk[NJ * NI];
+	// XCD-aware tile order (as k_vid_epzs_sub): workgroup g takes tile
+	// (g % 8) C + g / 8, so each XCD sweeps one band of tile rows and the
+	// windows a tile shares with the one above it are still in its L2
+	const int nt = ntx * nty * 3, C = (nt + 7) >> 3;
+	const int tile = (int)(blockIdx.x & 7) * C + (int)(blockIdx.x >> 3);
+	if (tile >= nt) return;
+	const int X0 = tile % ntx * 64, Y0 = tile / ntx % nty * TR, J0 = Y0 / 8 - 1;
+	const long pc = tile / (ntx * nty) * P;
+	const int t = threadIdx.x;
+	if (t < NJ * NI) {
+		const int bi = X0 / 8 - 1 + t % NI, bj = J0 + t / NI;
+		unsigned long long e = 0;
+		if (bi >= 0 && bi < bx && bj >= 0 && bj < by) {
+			const uint32_t m = mv[(long)bj * bx + bi];
+			e = 1;
+			if (m != kVidIntra) {
+				const int mx = mvx(m), my = mvy(m);
+				int px = 8 * bi + (mx >> 2) - 4, py = 8 * bj + (my >> 2) - 4;   // get_pos, obmc.cpp:252-263
+				px = px < -15 ? -15 : px >= w ? w - 1 : px;
+				py = py < -15 ? -15 : py >= h ? h - 1 : py;
+				e = (unsigned long long)(ref.p[((mx & 3) << 2) | (my & 3)] + pc + (long)py * S + px);
+			}
 		}
-		const int wl = kWin[jj][ii], wr = kWin[jj][7 - ii], wlm = kWin[7 - jj][ii], wrm = kWin[7 - jj][7 - ii];
-		int r;
-		if (top && left) {                                 // top-left: the block's own quadrant
-			if (T && L) r = s;
-			else if (T) r = (d + s * (wl + wlm) + 8) >> 4;
-			else if (L) r = (d + s * (wl + wr) + 8) >> 4;
-			else r = (d + s * wl + 8) >> 4;
-		} else if (top) {                                  // top-right
-			if (T && R) r = s;
-			else if (T) r = s * (wr + wrm);
-			else if (R) r = (d + s * (wr + wl) + 8) >> 4;
-			else r = d + s * wr;
-		} else if (left) {                                 // bottom-left
-			if (Bo && L) r = s;
-			else if (Bo) r = (d + s * (wl + wlm) + 8) >> 4;
-			else if (L) r = d + s * (wl + wr);
-			else r = d + s * wl;
-		} else {                                           // bottom-right
-			if (Bo && R) r = s;
-			else if (Bo) r = s * (wr + wrm);
-			else if (R) r = s * (wr + wl);
-			else r = s * wr;
-		}
-		d = (int16_t)r;
+		blk[t] = e;
 	}
-	pred[o] = (int16_t)d;
+	const int lane = t & 63, wv = __builtin_amdgcn_readfirstlane(t >> 6);
+	// with img (the encoder) the tiles cover the whole w x h plane: the
+	// residual img - prediction is taken here (CImage::operator-=), also on
+	// the columns / rows past the last whole block that OBMC leaves alone
+	const int x = X0 + lane, xe = img ? w : 8 * bx, ye = img ? h : 8 * by;
+	const bool xin = x < 8 * bx;
+	int d[RW], c[RW];
+#pragma unroll
+	for (int r = 0; r < RW; r++) {
+		const int y = Y0 + wv * RW + r;
+		const bool ok = x < xe && y < ye;
+		d[r] = ok ? pred[pc + (long)y * S + x] : 0;
+		c[r] = ok && img ? img[pc + (long)y * S + x] : 0;
+	}
+	__syncthreads();
+	if (x >= xe) return;
+	const int a0 = (x + 4) >> 3, cu = x + 4 - 8 * a0, ia = a0 - (X0 / 8 - 1);
+	const bool Lm = a0 - 1 == 0, Rm = a0 - 1 == bx - 1, La = a0 == 0, Ra = a0 == bx - 1;
+	int s[RW][4];
+#pragma unroll
+	for (int r = 0; r < RW; r++) {
+		const int y = Y0 + wv * RW + r;
+		const int b0 = (y + 4) >> 3, cv = y + 4 - 8 * b0;
+#pragma unroll
+		for (int k = 0; k < 4; k++) {
+			const int sel = (k & 2) ? 1 : 0, bq = ia - ((k & 1) ? 0 : 1);
+			const unsigned long long e = blk[(b0 - 1 + sel - J0) * NI + bq];
+			const int u = cu + ((k & 1) ? 0 : 8), v = cv + (sel ? 0 : 8);
+			s[r][k] = 0;
+			if (xin && y < 8 * by && e > 1) s[r][k] = ((gsamples)e)[(long)v * S + u];
+		}
+	}
+#pragma unroll
+	for (int r = 0; r < RW; r++) {
+		const int y = Y0 + wv * RW + r;
+		if (y >= ye) continue;
+		const long o = pc + (long)y * S + x;
+		const int b0 = (y + 4) >> 3, cv = y + 4 - 8 * b0;
+		const bool inb = xin && y < 8 * by;
+		int dd = d[r];
+#pragma unroll
+		for (int k = 0; k < 4 && inb; k++) {
+			const bool top = k & 2, left = k & 1;
+			const int bj = b0 - (top ? 0 : 1);
+			if (blk[(bj - J0) * NI + ia - (left ? 0 : 1)] == 0) continue;   // outside the frame
+			const bool T = bj == 0, Bo = bj == by - 1, L = left ? La : Lm, R = left ? Ra : Rm;
+			const int jj = top ? cv : 7 - cv;             // the window row (the bottom half counts down)
+			if (top ? (T && jj < 4) : (Bo && jj < 4)) continue;
+			if (left ? (L && cu < 4) : (R && cu >= 4)) continue;
+			dd = obmc_statement(dd, s[r][k], top, left, T, Bo, L, R, jj, cu);
+		}
+		if (inb) pred[o] = (int16_t)dd;
+		if (img) img[o] = (int16_t)(c[r] - dd);
+	}
 }
 
 // ------------------------------------------- TransformI's side effect
@@ -514,10 +546,15 @@ int launch_vid_epzs(const VidGeom& g, const int16_t* cur, const VidSubs& ref, ui
 	return launched();
 }
 
-int launch_vid_obmc(const VidGeom& g, const uint32_t* mv, const VidSubs& ref, int16_t* pred, hipStream_t st)
+int launch_vid_obmc(const VidGeom& g, const uint32_t* mv, const VidSubs& ref, int16_t* pred, int16_t* residual,
+                    hipStream_t st)
 {
-	hipLaunchKernelGGL(k_vid_obmc, dim3((8 * g.bx + 63) / 64, (8 * g.by + kObmcRows - 1) / kObmcRows, 3), dim3(64, 4), 0, st,
-	                   ref, mv, pred, g.w, g.h, g.S, g.P, g.bx, g.by);
+	static const int rw = [] { const char* e = getenv("RIC_OBMC_RW"); return e && atoi(e) == 8 ? 8 : 4; }();   // A/B knob
+	const int xe = residual ? g.w : 8 * g.bx, ye = residual ? g.h : 8 * g.by;
+	const int ntx = (xe + 63) / 64, nty = (ye + 4 * rw - 1) / (4 * rw), C = (ntx * nty * 3 + 7) / 8;
+	if (ntx < 1 || nty < 1) return 0;
+	hipLaunchKernelGGL(rw == 8 ? k_vid_obmc<8> : k_vid_obmc<4>, dim3(8 * C), dim3(256), 0, st, ref, mv, pred, residual, g.w,
+	                   g.h, g.S, g.P, g.bx, g.by, ntx, nty);
 	return launched();
 }
 

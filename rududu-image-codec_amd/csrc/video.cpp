@@ -93,13 +93,20 @@ struct ric_video {
 	int16_t* img(int id) const { return bufs[id] + g.origin(); }
 	int16_t* pred_img() const { return pred + g.origin(); }
 
+	// kImgSlack samples of allocated slack before and after every image: the
+	// OBMC kernel stages window rows with aligned 16-byte loads that reach up
+	// to 16 bytes past a row clamped to the image's first or last sample
+	static constexpr size_t kImgSlack = 128;
 	int alloc_image(int16_t** out)
 	{
-		const size_t bytes = g.image_samples() * sizeof(int16_t);
-		VCHK(hipMalloc(out, bytes));
-		VCHK(hipMemsetAsync(*out, 0, bytes, st));      // a fresh CImage reads as zeros (see oracle/ref_video.cpp)
+		const size_t bytes = (g.image_samples() + 2 * kImgSlack) * sizeof(int16_t);
+		int16_t* raw = nullptr;
+		VCHK(hipMalloc(&raw, bytes));
+		*out = raw + kImgSlack;
+		VCHK(hipMemsetAsync(raw, 0, bytes, st));      // a fresh CImage reads as zeros (see oracle/ref_video.cpp)
 		return RIC_OK;
 	}
+	static void free_image(int16_t* p) { if (p) (void)hipFree(p - kImgSlack); }
 	// CImageBuffer::getFree (imagebuffer.cpp:44-61)
 	int get_free(int* id)
 	{
@@ -256,8 +263,8 @@ void ric_video_destroy(ric_video* v)
 	if (!v) return;
 	(void)hipSetDevice(v->device);
 	if (v->st) (void)hipStreamSynchronize(v->st);
-	for (int16_t* p : v->bufs) (void)hipFree(p);
-	if (v->pred) (void)hipFree(v->pred);
+	for (int16_t* p : v->bufs) ric_video::free_image(p);
+	ric_video::free_image(v->pred);
 	if (v->d_mv) (void)hipFree(v->d_mv);
 	if (v->d_dist) (void)hipFree(v->d_dist);
 	if (v->d_gran) (void)hipFree(v->d_gran);
@@ -314,8 +321,7 @@ int ric_video_encode(ric_video* v, const uint8_t* pix, int stride, int pix_on_de
 		rc = v->sync_status();
 		if (rc) return rc;
 		mv_encode(v->mux, v->mv.data(), g.bx, g.by);       // obme->encode(&codec)
-		if (launch_vid_obmc(g, v->d_mv, ref, v->pred_img(), v->st) ||
-		    launch_vid_addsub(g, v->img(cur), v->pred_img(), -1, v->st))
+		if (launch_vid_obmc(g, v->d_mv, ref, v->pred_img(), v->img(cur), v->st))   // apply_mv, then *im -= *pred
 			return vfail(hipGetLastError(), "k_vid_obmc"), RIC_E_HIP;
 		rc = v->encode_image(cur);
 		if (rc) return rc;
@@ -354,7 +360,7 @@ int ric_video_decode(ric_video* v, const uint8_t* buf, size_t len, int* size)
 		if (rc) return rc;
 		mv_decode(v->mux, v->mv.data(), g.bx, g.by);       // obmc->decode(&codec)
 		VCHK(hipMemcpyAsync(v->d_mv, v->mv.data(), sizeof(uint32_t) * v->mv.size(), hipMemcpyHostToDevice, v->st));
-		if (launch_vid_obmc(g, v->d_mv, v->subs(1), v->pred_img(), v->st)) return vfail(hipGetLastError(), "k_vid_obmc"), RIC_E_HIP;
+		if (launch_vid_obmc(g, v->d_mv, v->subs(1), v->pred_img(), nullptr, v->st)) return vfail(hipGetLastError(), "k_vid_obmc"), RIC_E_HIP;
 		result = v->decode_image(cur);
 		if (result && result != RIC_E_STREAM) return result;
 		if (launch_vid_addsub(g, v->img(cur), v->pred_img(), +1, v->st)) return vfail(hipGetLastError(), "k_vid_addsub"), RIC_E_HIP;

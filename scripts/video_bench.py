@@ -13,8 +13,12 @@ Algorithmic bytes per frame (int16 samples, 3 planes of w x h, P = 3 w h):
   k_vid_extend     16 images x 3 planes x the border ring (15 samples deep):
                    read + write 2 B each
   k_vid_obmc       per predicted sample: the old prediction read + written and
-                   the 4 overlapping blocks' source samples: 12 B x 3 x 8bx x 8by
-  k_vid_addsub     read two images, write one: 6 B x P (twice per encoded inter frame)
+                   the 4 overlapping blocks' source samples: 12 B x 3 x 8bx x 8by;
+                   the encoder's launches also take the residual (image read +
+                   written, 4 B x P), the decoder's do not: the average over
+                   the equal numbers of both is 12 B x 3 x 64 bx by + 2 B x P
+  k_vid_addsub     read two images, write one: 6 B x P (once per encoded and
+                   once per decoded inter frame: the reconstruction)
   k_vid_input      3 B in, 6 B out per pixel
   k_vid_epzs_sub   per block: the current block + 16 candidate blocks, 128 B each
   k_vid_epzs_full  latency-bound wavefront (one wave per block row; a block
@@ -39,7 +43,7 @@ def model(w, h):
     P = 3 * w * h
     bx, by = w >> 3, h >> 3
     ring = 2 * 15 * (w + 30) + 30 * h
-    return {"k_vid_interp": 32 * P, "k_vid_extend": 16 * 3 * ring * 4, "k_vid_obmc": 12 * 3 * 64 * bx * by,
+    return {"k_vid_interp": 32 * P, "k_vid_extend": 16 * 3 * ring * 4, "k_vid_obmc": 12 * 3 * 64 * bx * by + 2 * P,
             "k_vid_addsub": 6 * P, "k_vid_input": 9 * w * h, "k_vid_epzs_sub": 17 * 128 * bx * by}
 
 
@@ -130,13 +134,10 @@ def main():
                     ks[k].update(t)
         print(json.dumps({"w": a.w, "h": a.h, "frames": a.frames, "kernels": ks}))
         return
-    import torch
     import ric_amd
     import video_seq
-    torch.cuda.init()
     seq = video_seq.sequence(a.w, a.h, a.frames, 1)
-    dev = [torch.from_numpy(np.ascontiguousarray(f)).cuda() for f in seq]
-    torch.cuda.synchronize()
+    dev = [ric_amd.DeviceArray.from_numpy(np.ascontiguousarray(f)) for f in seq]
     enc = ric_amd.VideoCodec(True, a.w, a.h)
     dec = ric_amd.VideoCodec(False, a.w, a.h)
     enc.quant = dec.quant = a.q
