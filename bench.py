@@ -110,8 +110,12 @@ def parse():
                          "encoder and decoder (one wave per stream), host threads doing whole round trips beside it; "
                          "mix = GPU stream encoder, each launch decoded by the host threads or the GPU stream decoder "
                          "(whichever has room)")
-    ap.add_argument("--pool", type=int, default=1408,
-                    help="hybrid / gpu: frames per GPU stream-coder launch (two in flight; shrunk to fit memory)")
+    ap.add_argument("--pool", type=int, default=1536,
+                    help="hybrid / gpu: frames per GPU stream-coder launch (two in flight: 3072 = three coder waves "
+                         "on every SIMD; shrunk to fit memory)")
+    ap.add_argument("--value-cap", type=int, default=-1,
+                    help="hybrid / gpu: the pool's compacted level-0 value capacity per frame plane "
+                         "(ric_batch_hybrid_config_ex: -1 the default 9/16 of the coefficients, 0 dense bands)")
     ap.add_argument("--launches", type=int, default=2, help="hybrid / gpu: stream-coder launches per step")
     ap.add_argument("--distinct", type=int, default=128,
                     help="distinct frames resident in HBM (inputs, outputs) and host stream buffers; a longer step cycles them")
@@ -395,11 +399,12 @@ def main():
         # stream capacity: 3 bits per pixel (a q9 C3 stream is 1.7), 16-byte multiple
         pool = min(a.pool, max(n_gpu, 1))
         scap = (W * H * CH * 3 // 8 + 65536) // 16 * 16
-        # the pool holds bands + records + a stream per frame in flight (C3:
-        # ~110 MB): if it does not fit this GPU's memory, shrink it
+        # the pool holds bands (the finest level compacted) + records + a
+        # stream per frame in flight (C3: ~79 MB; 98 MB with dense bands): if
+        # it does not fit this GPU's memory, shrink it
         while True:
             try:
-                b.hybrid_config(pool, scap)
+                b.hybrid_config(pool, scap, a.value_cap)
                 break
             except ric_amd.RicError as e:
                 if e.rc != ric_amd.RIC_E_CAPACITY or pool <= 64:

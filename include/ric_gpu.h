@@ -255,6 +255,15 @@ int ric_diag_gdec_dbg(void* dev_buf);
  * A pool that does not fit in device memory returns RIC_E_CAPACITY with
  * nothing allocated (the batch stays usable: retry with fewer frames). */
 int ric_batch_hybrid_config(ric_batch* b, int pool_frames, size_t stream_cap);
+/* The same, with the pool's level-0 value capacity.  value_cap > 0: the pool
+ * holds each frame's (each colour plane's) three finest bands compacted --
+ * only their non-zero values, at most value_cap of them, and a mask per 4x4
+ * block -- instead of dense (at C3 about 25 MB instead of 50 MB per frame, so
+ * more frames fit); a frame with more non-zero values than that is coded on
+ * the host instead (same bytes, slower), never an error.  value_cap < 0: the
+ * default, 9 / 16 of the finest bands' coefficients
+ * (ric_batch_hybrid_config); 0: dense bands (no compaction). */
+int ric_batch_hybrid_config_ex(ric_batch* b, int pool_frames, size_t stream_cap, long value_cap);
 /* Output digests (no reference counterpart; for verifying a serving step
  * whose output buffers are reused): while set, the decode / round-trip calls
  * write, for frame i of the call (i < n), the 64-bit digest of its decoded

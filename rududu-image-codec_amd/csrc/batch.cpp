@@ -234,6 +234,21 @@ struct ric_batch {
 		uint32_t* d_post = nullptr;
 		uint32_t* d_yield = nullptr;               // raised while the batch stream runs host frames' level kernels
 		uint32_t epoch = 0;                        // the last coder launch's tag (posted words, k_gc_*)
+		// Compacted pool (ric_batch_hybrid_config_ex): level 0's three bands of a
+		// plane are held as a compact block (compact.h DcmpLayout: cmp_cap bytes,
+		// at most vcap values) in front of the rest of its pyramid [lo, b_end);
+		// the kernels' arena base of a plane is its region + ashift (= cmp_cap -
+		// lo), so the pyramid offsets >= lo land after the block, and level 0
+		// passes through the scratch arenas (ZFrames::lo).  vcap 0: dense pool.
+		uint32_t vcap = 0;
+		size_t lo = 0, cmp_cap = 0;
+		long long ashift = 0;
+		DcmpLayout dl;
+		CmpArgs* d_pcmp = nullptr;                 // the forward compaction's arguments: [half][group][plane]
+		int pcmp_groups = 0;
+		uint32_t* d_pcnt = nullptr;                // its chunk counts / offsets (slots frames) and totals
+		size_t pcnt_stride = 0;
+		uint32_t* d_ptotal = nullptr;
 	} cp;
 
 	int nslot() const { return 2 * slots; }
@@ -304,8 +319,11 @@ int d2h_slots(ric_batch* b, int set, int n);
 // of frame i go to pool + i * pstr instead of its arena -- written there by
 // the level kernels directly when every level is a fused one (region C, the
 // scratch, stays in the arena), else copied there after the levels.
+// lo (a compacted pool, CoderPool): pool is the frames' kernel base and the
+// offsets below lo (level 0's bands) stay in the arenas, for the compaction
 int gpu_encode_plane(ric_batch* b, int set, int n, int p, const uint8_t* const* pix, int q, int trans, bool d2h = true,
-                     int abase = -1, int amul = 1, uint32_t* yflag = nullptr, char* pool = nullptr, size_t pstr = 0)
+                     int abase = -1, int amul = 1, uint32_t* yflag = nullptr, char* pool = nullptr, size_t pstr = 0,
+                     size_t lo = 0)
 {
 	YieldFlag yf(yflag, b->st);
 	if (yf.raise()) return RIC_E_HIP;
@@ -341,7 +359,7 @@ int gpu_encode_plane(ric_batch* b, int set, int n, int p, const uint8_t* const* 
 		fr.ring = b->fq_ring;
 		if (direct) {
 			fr.arena = pool; fr.astride = pstr;
-			fr.scratch = b->arena(abase); fr.scstride = ast; fr.split = P.b_end;
+			fr.scratch = b->arena(abase); fr.scstride = ast; fr.split = P.b_end; fr.lo = lo;
 		}
 		if (l == 0) {
 			fr.src = b->plane(s0, p); fr.sstride = b->pstride; fr.sp = b->pitch;
@@ -387,7 +405,7 @@ int gpu_encode_plane(ric_batch* b, int set, int n, int p, const uint8_t* const* 
 	BCHK(hipGetLastError());
 	if (yf.lower()) return RIC_E_HIP;
 	if (pool && !direct)
-		BCHK(hipMemcpy2DAsync(pool, pstr, b->arena(abase), ast, P.b_end, n, hipMemcpyDeviceToDevice, b->st));
+		BCHK(hipMemcpy2DAsync(pool + lo, pstr, b->arena(abase) + lo, ast, P.b_end - lo, n, hipMemcpyDeviceToDevice, b->st));
 	if (!d2h || pool) return RIC_OK;
 	if (abase != s0 || amul != 1) return RIC_E_ARG;      // the host mirrors follow the slots
 	return d2h_slots(b, set, n);
@@ -483,8 +501,10 @@ int h2d_slots(ric_batch* b, int set, int n)
 // pool (as gpu_encode_plane): the decoded bands of frame i are read from
 // pool + i * pstr (region A) while the inverse's intermediate LL planes
 // (region C) stay in the frame's arena -- no copy of the bands.
+// lo (a compacted pool): level 0's bands are read from the arenas (expanded
+// there from the pool's compact blocks)
 int gpu_decode_plane(ric_batch* b, int set, int n, int p, const int* qs, int trans, bool h2d = true, int abase = -1,
-                     int amul = 1, uint32_t* yflag = nullptr, char* pool = nullptr, size_t pstr = 0)
+                     int amul = 1, uint32_t* yflag = nullptr, char* pool = nullptr, size_t pstr = 0, size_t lo = 0)
 {
 	Pyramid& P = b->P;
 	const int s0 = set * b->slots;
@@ -505,7 +525,7 @@ int gpu_decode_plane(ric_batch* b, int set, int n, int p, const int* qs, int tra
 		fr.arena = b->arena(abase); fr.astride = ast; fr.nz = n;
 		if (pool) {
 			fr.arena = pool; fr.astride = pstr;
-			fr.scratch = b->arena(abase); fr.scstride = ast; fr.split = P.b_end;
+			fr.scratch = b->arena(abase); fr.scstride = ast; fr.split = P.b_end; fr.lo = lo;
 		}
 		int out_int;
 		if (l == 0) {
@@ -833,6 +853,9 @@ void ric_batch_destroy(ric_batch* b)
 		if (c.d_ts) (void)hipFree(c.d_ts);
 		if (c.h_post) (void)hipHostFree(c.h_post);
 		if (c.d_yield) (void)hipFree(c.d_yield);
+		if (c.d_pcmp) (void)hipFree(c.d_pcmp);
+		if (c.d_pcnt) (void)hipFree(c.d_pcnt);
+		if (c.d_ptotal) (void)hipFree(c.d_ptotal);
 		for (int h = 0; h < 2; h++) {
 			if (c.ev_fwd[h]) (void)hipEventDestroy(c.ev_fwd[h]);
 			if (c.ev_done[h]) (void)hipEventDestroy(c.ev_done[h]);
@@ -1176,6 +1199,11 @@ int ric_batch_set_ready(ric_batch* b, uint32_t* host_words, long n)
 
 int ric_batch_hybrid_config(ric_batch* b, int pool_frames, size_t stream_cap)
 {
+	return ric_batch_hybrid_config_ex(b, pool_frames, stream_cap, -1);
+}
+
+int ric_batch_hybrid_config_ex(ric_batch* b, int pool_frames, size_t stream_cap, long value_cap)
+{
 	if (!b || pool_frames < 1 || pool_frames > 65536 || stream_cap < 64 || (stream_cap & 15) || stream_cap > 0xFFFFFFF0u)
 		return RIC_E_ARG;
 	if (set_dev(b->device)) return RIC_E_HIP;
@@ -1187,14 +1215,33 @@ int ric_batch_hybrid_config(ric_batch* b, int pool_frames, size_t stream_cap)
 	if (c.h_res) { BCHK(hipHostFree(c.h_res)); c.h_res = c.d_res = nullptr; }
 	if (c.d_ts) { BCHK(hipFree(c.d_ts)); c.d_ts = nullptr; }
 	if (c.h_post) { BCHK(hipHostFree(c.h_post)); c.h_post = c.d_post = nullptr; }
+	if (c.d_pcmp) { BCHK(hipFree(c.d_pcmp)); c.d_pcmp = nullptr; }
+	if (c.d_pcnt) { BCHK(hipFree(c.d_pcnt)); c.d_pcnt = nullptr; }
+	if (c.d_ptotal) { BCHK(hipFree(c.d_ptotal)); c.d_ptotal = nullptr; }
 	if (!c.d_yield) {
 		BCHK(hipMalloc(&c.d_yield, 256));
 		BCHK(hipMemset(c.d_yield, 0, 256));
 	}
 	c.n = pool_frames;
+	const Pyramid& P = b->P;
+	// the compacted pool: level 0 16-bit (the 9/7 ric path), a value capacity
+	// per plane (default 9 of a block's 16 coefficients) below the dense bands
+	c.dl = dcmp_layout(P);
+	size_t l0 = 0;
+	for (int k = 0; k < 3; k++) l0 += (size_t)P.L[0].b[k].dx * P.L[0].b[k].dy;
+	const long vdef = (long)(l0 * 9 / 16);
+	const long vc = value_cap < 0 ? vdef : std::min(value_cap, (long)l0);
+	c.vcap = 0; c.lo = 0; c.cmp_cap = 0; c.ashift = 0;
+	if (vc > 0 && c.dl.ok && P.nlev >= 2) {
+		c.vcap = (uint32_t)vc;
+		c.lo = P.L[1].b[BD].off;                           // level 0's bands: [0, lo)
+		c.cmp_cap = (c.dl.vals_off + 2 * (size_t)c.vcap + 255) / 256 * 256;
+		if (c.cmp_cap == c.lo) c.cmp_cap += 256;           // (GEncArgs::cmp_rel 0 means dense)
+		c.ashift = (long long)c.cmp_cap - (long long)c.lo;
+	}
 	// colour: a frame's Y, Co, Cg plane pyramids side by side (the coder codes
 	// them into one stream on one wave, ric.cpp:157-176)
-	c.abstride = (b->P.b_end + 65535) / 65536 * 65536;
+	c.abstride = ((c.vcap ? c.cmp_cap + (P.b_end - c.lo) : P.b_end) + 65535) / 65536 * 65536;
 	c.fstride = (size_t)b->channels * c.abstride;
 	c.ocap = stream_cap;
 	// out of memory: nothing stays allocated and the error is not left
@@ -1224,6 +1271,43 @@ int ric_batch_hybrid_config(ric_batch* b, int pool_frames, size_t stream_cap)
 		memset(c.h_post, 0, sizeof(uint32_t) * 6 * c.n);
 		if (!c.d_args) BCHK(hipMalloc(&c.d_args, 3 * sizeof(GEncArgs)));   // the halves, then both as one launch
 		if (!c.d_dargs) BCHK(hipMalloc(&c.d_dargs, 3 * sizeof(GDecArgs)));
+		if (c.vcap) {
+			// the forward compaction's argument blocks, one per (half, group, plane)
+			c.pcmp_groups = (c.n + b->slots - 1) / b->slots;
+			BCHK(hipMalloc(&c.d_pcmp, sizeof(CmpArgs) * 2 * (size_t)c.pcmp_groups * b->channels));
+			int nch = 0;
+			for (int k = 0; k < 3; k++) nch += c.dl.nch[k];
+			c.pcnt_stride = (size_t)(nch + 63) / 64 * 64;
+			BCHK(hipMalloc(&c.d_pcnt, sizeof(uint32_t) * c.pcnt_stride * b->slots));
+			BCHK(hipMalloc(&c.d_ptotal, sizeof(uint32_t) * b->slots));
+			std::vector<CmpArgs> ca(2 * (size_t)c.pcmp_groups * b->channels);
+			for (int h = 0; h < 2; h++)
+				for (int g = 0; g < c.pcmp_groups; g++)
+					for (int p = 0; p < b->channels; p++) {
+						CmpArgs& a = ca[((size_t)h * c.pcmp_groups + g) * b->channels + p];
+						memset(&a, 0, sizeof a);
+						char* region = c.d_ab + ((size_t)h * c.n + (size_t)g * b->slots) * c.fstride + (size_t)p * c.abstride;
+						a.arena = region + c.ashift; a.astride = c.fstride;      // the records (pool region B)
+						a.bsrc = b->arena(0); a.bstride = b->astride;             // level 0's dense bands (scratch)
+						a.out = region + c.dl.vals_off; a.ostride = c.fstride;
+						a.cnt = c.d_pcnt; a.cstride = c.pcnt_stride;
+						a.total = c.d_ptotal;
+						a.vcap = c.vcap;
+						a.status = region + c.ashift + P.status_off; a.sstride = c.fstride;
+						int ch = 0;
+						for (int k = 0; k < 3; k++) {                             // level 0, coding order V, H, D
+							const Band& B = P.L[0].b[c.dl.band[k]];
+							CmpBand& d = a.band[k];
+							d.off = (uint32_t)B.off; d.rec_off = (uint32_t)P.rec_off[0][c.dl.band[k]];
+							d.dx = B.dx; d.dy = B.dy; d.pitch = B.pitch;
+							d.nblk = B.bw() * B.bh();
+							d.chunk0 = ch;
+							ch += (d.nblk + 63) / 64;
+						}
+						a.nb = 3; a.nchunk = ch;
+					}
+			BCHK(hipMemcpy(c.d_pcmp, ca.data(), sizeof(CmpArgs) * ca.size(), hipMemcpyHostToDevice));
+		}
 		for (int h = 0; h < 2; h++) {
 			if (!c.st[h]) BCHK(hipStreamCreateWithFlags(&c.st[h], hipStreamNonBlocking));
 			if (!c.ev_fwd[h]) BCHK(hipEventCreateWithFlags(&c.ev_fwd[h], hipEventDisableTiming));
@@ -1240,7 +1324,11 @@ int ric_batch_hybrid_config(ric_batch* b, int pool_frames, size_t stream_cap)
 		c.d_out = nullptr;
 		if (c.h_res) (void)hipHostFree(c.h_res);
 		if (c.h_post) (void)hipHostFree(c.h_post);
+		if (c.d_pcmp) (void)hipFree(c.d_pcmp);
+		if (c.d_pcnt) (void)hipFree(c.d_pcnt);
+		if (c.d_ptotal) (void)hipFree(c.d_ptotal);
 		c.h_res = c.d_res = c.h_post = c.d_post = nullptr;
+		c.d_pcmp = nullptr; c.d_pcnt = c.d_ptotal = nullptr;
 		c.n = 0;
 	}
 	return rc;
@@ -1303,13 +1391,16 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 			a.ts = tstamp ? c.d_ts + (size_t)h * 4 * c.n : nullptr;
 			a.prio = gc_prio();
 			a.yield = yield_on ? c.d_yield : nullptr;
-			a.arena = c.d_ab + (size_t)h * c.n * c.fstride; a.astride = c.fstride;
+			a.arena = c.d_ab + (size_t)h * c.n * c.fstride + c.ashift; a.astride = c.fstride;
 			a.pstride = c.abstride; a.nplanes = C;
 			a.out = c.d_out + (size_t)h * c.n * c.ocap; a.ostride = c.ocap; a.cap = c.ocap;
 			a.res = c.d_res + res_enc(h);
 			a.status_off = (uint32_t)P.status_off;
 			a.w = b->w; a.h = b->h; a.q = q; a.trans = trans;
 			gc_bands(P, a.ll, a.b, a.nb);
+			a.cmp_rel = c.vcap ? -c.ashift : 0;
+			a.cvals_off = (uint32_t)c.dl.vals_off; a.cvcap = c.vcap;
+			if (c.vcap) gc_bands_compact(a.b, a.nb, c.dl.mask_off, c.dl.coff_off);
 			GDecArgs& d = c.dargs[h];
 			d.arena = (char*)a.arena; d.astride = a.astride;
 			d.pstride = a.pstride; d.nplanes = C;
@@ -1324,6 +1415,8 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 			d.ts = tstamp ? c.d_ts + (size_t)8 * c.n + (size_t)h * 4 * c.n : nullptr;
 			d.w = b->w; d.h = b->h;
 			gc_bands(P, d.ll, d.b, d.nb);
+			d.cmp_rel = a.cmp_rel; d.cvals_off = a.cvals_off; d.cvcap = a.cvcap;
+			if (c.vcap) gc_bands_compact(d.b, d.nb, c.dl.mask_off, c.dl.coff_off);
 		}
 		// entry 2: both halves as one launch (frames 0 .. 2 n - 1 of the pool;
 		// the arenas, streams and result words of the halves are contiguous)
@@ -1362,6 +1455,11 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 	auto batch_f0 = [&](int j) { return n_host + j * c.n; };
 	auto batch_m = [&](int j) { return std::min(c.n, n - batch_f0(j)); };
 	auto abslot = [&](int h, int k) { return c.d_ab + ((size_t)h * c.n + k) * c.fstride; };   // frame k of half h, plane 0
+	// its kernels' arena base (a compacted pool: the offsets >= lo after the compact block)
+	auto kbase = [&](int h, int k) { return abslot(h, k) + c.ashift; };
+	int pcmp_nch = 0;
+	for (int k = 0; k < 3; k++) pcmp_nch += c.dl.nch[k];
+	int n_fallback = 0;                                    // frames over the compacted pool's capacity: coded on the host
 	// RIC_FWD_AHEAD=0: each batch's coder launch starts after its own forward
 	// levels (the second batch's then run beside the first batch's coder waves)
 	static const bool fwd_ahead = [] { const char* e = getenv("RIC_FWD_AHEAD"); return !e || atoi(e) != 0; }();
@@ -1409,6 +1507,7 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 					std::this_thread::sleep_for(std::chrono::microseconds(500));
 				}
 				if ((st_k & ~0xFFu) != want) break;                  // harvest reports it
+				if ((st_k & 0xFFu) == 4) continue;                    // left to the host (harvest)
 				const uint32_t len_k = __atomic_load_n(po + 2 * k, __ATOMIC_RELAXED);
 				if ((st_k & 0xFFu) || len_k > cap[f0 + k]) break;   // harvest reports it
 				if (bfail(hipMemcpy(out[f0 + k], c.d_out + ((size_t)h * c.n + k) * c.ocap, len_k, hipMemcpyDeviceToHost),
@@ -1430,8 +1529,11 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 			for (int p = 0; p < C; p++) {                   // (p 0 converts every plane's pixels)
 				// the bands + records straight into the pool (the arenas keep the scratch)
 				int r = gpu_encode_plane(b, 0, gm, p, pix + f0 + g0, q, trans, false, -1, 1, nullptr,
-				                         abslot(h, g0) + (size_t)p * c.abstride, c.fstride);
+				                         kbase(h, g0) + (size_t)p * c.abstride, c.fstride, c.lo);
 				if (r) return r;
+				// a compacted pool: level 0's values (from the arenas) into each frame's compact block
+				if (c.vcap && launch_compact(c.d_pcmp + ((size_t)h * c.pcmp_groups + g0 / S) * C + p, pcmp_nch, gm, b->st))
+					return bfail(hipGetLastError(), "pool compaction") ? RIC_E_HIP : RIC_E_HIP;
 			}
 		}
 		BCHK(hipEventRecord(c.ev_fwd[h], b->st));
@@ -1536,8 +1638,27 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 		const int f0 = batch_f0(j), m = batch_m(j), h = j & 1;
 		const int gm = std::min(S, m - g0);
 		for (int p = 0; p < C; p++) {
+			if (c.vcap) {
+				// level 0 from the compact blocks into the arenas' dense bands
+				DcmpArgs x;
+				x.arena = b->arena(0); x.astride = b->astride;
+				x.in = abslot(h, g0) + (size_t)p * c.abstride; x.istride = c.fstride;
+				int ch = 0;
+				for (int k = 0; k < 3; k++) {
+					const Band& B = P.L[0].b[c.dl.band[k]];
+					x.off[k] = (uint32_t)B.off; x.dx[k] = B.dx; x.dy[k] = B.dy; x.pitch[k] = B.pitch;
+					x.mask_off[k] = (uint32_t)c.dl.mask_off[k]; x.coff_off[k] = (uint32_t)c.dl.coff_off[k];
+					x.nblk[k] = c.dl.nblk[k];
+					x.chunk0[k] = ch;
+					ch += c.dl.nch[k];
+				}
+				x.chunk0[3] = ch;
+				x.vals_off = (uint32_t)c.dl.vals_off;
+				x.vcap = c.vcap;
+				if (launch_dcmp_expand(x, gm, b->st)) return bfail(hipGetLastError(), "k_dcmp_expand") ? RIC_E_HIP : RIC_E_HIP;
+			}
 			int r = gpu_decode_plane(b, 0, gm, p, qs.data(), trans, false, -1, 1, nullptr,
-			                         abslot(h, g0) + (size_t)p * c.abstride, c.fstride);
+			                         kbase(h, g0) + (size_t)p * c.abstride, c.fstride, c.lo);
 			if (r) return r;
 		}
 		const int r = gpu_pix_out(b, 0, gm, qs.data(), pix_out + f0 + g0, 1, f0 + g0);
@@ -1639,11 +1760,22 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 				fprintf(stderr, "\n");
 			}
 		}
+		std::vector<char> left(m, 0);                      // frames over the compacted pool's capacity
 		for (int k = 0; k < m; k++) {
 			if (re[2 * k + 1] == 2) {
 				clear_status(b);
 				set_last_error("fused level kernel: LDS ring hand-off timed out (device status word set; output discarded)");
 				return RIC_E_HIP;
+			}
+			if (re[2 * k + 1] == 4 && c.vcap) {
+				// more level-0 values than the pool holds: the frame goes round
+				// trip on the host (its GPU harvest output is overwritten then)
+				left[k] = 1;
+				n_fallback++;
+				tr("left to the host (over the pool's value capacity)", f0 + k);
+				ready_host.push_back({f0 + k, 1, false, 0, 0});
+				if (!bgpu[j]) copied[j].done();                    // (no host decode task copies its stream)
+				continue;
 			}
 			if (re[2 * k + 1]) {
 				set_last_error("GPU stream coder: a stream larger than the pool's stream capacity");
@@ -1662,7 +1794,14 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 		}
 		if (!bgpu[j]) {
 			enc_ms_est = 0.5 * enc_ms_est + 0.5 * (now_ms() - t_kick[j]);
-			for (int g0 = 0; g0 < m; g0 += SG) ready_dec.push_back({f0 + g0, std::min(SG, m - g0), true, h, g0});
+			// runs of up to SG coded frames (the ones left to the host excluded)
+			for (int g0 = 0; g0 < m;) {
+				if (left[g0]) { g0++; continue; }
+				int e = g0;
+				while (e < m && e - g0 < SG && !left[e]) e++;
+				ready_dec.push_back({f0 + g0, e - g0, true, h, g0});
+				g0 = e;
+			}
 			return RIC_OK;
 		}
 		for (int g0 = 0; g0 < m; g0 += S) {

@@ -29,7 +29,19 @@ struct CmpArgs {
 	uint32_t* total;
 	int nb, nchunk;
 	CmpBand band[3 * kMaxLevels];
+	// the GPU stream coder's compacted pool (batch.cpp): the bands come from
+	// bsrc + f * bstride (the scratch arenas) while the records are the pool's
+	// (arena); at most vcap values are written, and a frame with more sets 4 in
+	// its status word (status + f * sstride) -- the coder then leaves it to the
+	// host.  bsrc null: the bands are in arena; vcap 0: no limit.
+	const char* bsrc;
+	size_t bstride;
+	uint32_t vcap;
+	char* status;
+	size_t sstride;
 };
+// a compacted pool frame over its capacity (the status word's bit)
+constexpr int32_t kCmpOverCap = 4;
 
 // the band table of a pyramid (nb, nchunk, band[]); the pointers are the caller's
 void cmp_args(const Pyramid& P, CmpArgs& a);
@@ -68,6 +80,9 @@ struct DcmpArgs {
 	int dx[3], dy[3], pitch[3];
 	uint32_t mask_off[3], coff_off[3], vals_off;
 	int nblk[3], chunk0[4];           // chunk0[3] = total chunks
+	// values readable per block (the compacted pool's capacity: a frame the
+	// coder left to the host holds no valid offsets), 0: no limit
+	uint32_t vcap = 0;
 };
 int launch_dcmp_expand(const DcmpArgs& a, int nframes, hipStream_t st);
 

@@ -109,7 +109,10 @@ __global__ __launch_bounds__(1024) void k_cmp_scan(const CmpArgs* __restrict__ a
 		}
 		__syncthreads();
 	}
-	if (threadIdx.x == 0) a.total[f] = carry;
+	if (threadIdx.x == 0) {
+		a.total[f] = carry;
+		if (a.vcap && carry > a.vcap && a.status) atomicOr((int32_t*)(a.status + (size_t)f * a.sstride), kCmpOverCap);
+	}
 }
 
 __global__ __launch_bounds__(64 * kCmpWaves) void k_cmp_write(const CmpArgs* __restrict__ ap)
@@ -127,10 +130,12 @@ __global__ __launch_bounds__(64 * kCmpWaves) void k_cmp_write(const CmpArgs* __r
 		const int ex = wave_excl(__popc(m), tot);
 		uint32_t o = a.cnt[(size_t)f * a.cstride + c] + (uint32_t)ex;
 		if (!m) continue;
+		if (a.vcap && o + (uint32_t)__popc(m) > a.vcap) continue;   // over the pool's capacity: flagged by k_cmp_scan
 		int bx, by;
 		scan_block(s, B.dx, B.dy, bx, by);
 		const int w = B.dx - bx * 4 < 4 ? B.dx - bx * 4 : 4;
-		const int16_t* band = (const int16_t*)(arena + B.off) + (long)by * 4 * B.pitch + bx * 4;
+		const char* bsrc = a.bsrc ? a.bsrc + (size_t)f * a.bstride : arena;
+		const int16_t* band = (const int16_t*)(bsrc + B.off) + (long)by * 4 * B.pitch + bx * 4;
 		while (m) {                                  // the walk's order: ctz, raster over the w-wide block
 			const int i = __builtin_ctz(m);
 			m &= m - 1;
@@ -165,7 +170,12 @@ __global__ __launch_bounds__(64 * kCmpWaves) void k_dcmp_expand(DcmpArgs a)
 		for (int r = 0; r < h; r++)
 			for (int q = 0; q < w; q++) {
 				const int i = r * w + q;
-				band[(long)r * a.pitch[b] + q] = (m >> i) & 1 ? vals[o++] : (int16_t)0;
+				int16_t v = 0;
+				if ((m >> i) & 1) {
+					if (!a.vcap || o < a.vcap) v = vals[o];
+					o++;
+				}
+				band[(long)r * a.pitch[b] + q] = v;
 			}
 	}
 }

@@ -2460,14 +2460,18 @@ void fwd_launch(const Level& L, const void* src, long sp, char* arena, int vec, 
 
 template <typename TB, typename TO>
 InvArgs<TB, TB, TO> inv_args(const Level& L, const Band& lls, char* arena, void* out, long po, const int* q, int S,
-                             char* scratch = nullptr, size_t split = 0)
+                             char* scratch = nullptr, size_t split = 0, size_t lo = 0)
 {
 	InvArgs<TB, TB, TO> a;
 	memset(&a, 0, sizeof a);
 	for (int b = 0; b < 4; b++) a.q[b] = q ? q[b] : 1;
 	a.ovec = (po % 4 == 0) && ((uintptr_t)out % 16 == 0);
 	a.nofast = dbg_nofast();
-	for (int b = 0; b < 3; b++) { a.d[b] = (const TB*)(arena + L.b[b].off); a.p[b] = L.b[b].pitch; }
+	// (a compacted pool's level-0 bands are expanded into the scratch arena)
+	for (int b = 0; b < 3; b++) {
+		a.d[b] = (const TB*)((scratch && L.b[b].off < lo ? scratch : arena) + L.b[b].off);
+		a.p[b] = L.b[b].pitch;
+	}
 	// split arenas (ZFrames): the LL input from scratch when it lies in region C
 	a.ll = (const TB*)((scratch && lls.off >= split ? scratch : arena) + lls.off); a.pl = lls.pitch;
 	a.out = (TO*)out; a.po = po;
@@ -2553,10 +2557,11 @@ namespace {
 // generic kernel (k_fwdq_gen), else the packed ring forms.
 // scratch (split arenas, ZFrames): offsets from P.b_end on (region C) there
 FqArgs fq_args(const Pyramid& P, int l, const void* src, long sp, int vec8, int vec16, const QuantParams& qp,
-               char* arena, bool gen, char* scratch = nullptr)
+               char* arena, bool gen, char* scratch = nullptr, size_t lo = 0)
 {
 	const Level& L = P.L[l];
-	auto at = [&](size_t off) { return (scratch && off >= P.b_end ? scratch : arena) + off; };
+	// (lo: a compacted pool's level-0 bands go to the scratch arena too)
+	auto at = [&](size_t off) { return (scratch && (off >= P.b_end || off < lo) ? scratch : arena) + off; };
 	FqArgs a;
 	memset(&a, 0, sizeof a);   // (padding too: batched launches compare argument images)
 	a.wgt = nullptr;
@@ -2685,7 +2690,7 @@ int launch_fwdq_level_z(const Pyramid& P, int l, const ZFrames& fr, int vec8, in
 	std::vector<FqArgs> v(fr.nz);
 	for (int f = 0; f < fr.nz; f++) {
 		v[f] = fq_args(P, l, (const char*)fr.src + f * fr.sstride, fr.sp, vec8, vec16, qp, fr.arena + f * fr.astride, false,
-		               fr.scratch ? fr.c_base(f) : nullptr);
+		               fr.scratch ? fr.c_base(f) : nullptr, fr.lo);
 		v[f].nseg = (L.h + S - 1) / S;
 	}
 	if (zargs_put(z, v.data(), v.size() * sizeof(FqArgs), st)) return -1;
@@ -2718,7 +2723,7 @@ int launch_fwdq_gen_level_z(const Pyramid& P, int l, const ZFrames& fr, int vec8
 	std::vector<FqArgs> v(fr.nz);
 	for (int f = 0; f < fr.nz; f++) {
 		v[f] = fq_args(P, l, (const char*)fr.src + f * fr.sstride, fr.sp, vec8, 0, qp, fr.arena + f * fr.astride, true,
-		               fr.scratch ? fr.c_base(f) : nullptr);
+		               fr.scratch ? fr.c_base(f) : nullptr, fr.lo);
 		v[f].nseg = nseg;
 	}
 	if (zargs_put(z, v.data(), v.size() * sizeof(FqArgs), st)) return -1;
@@ -2758,7 +2763,7 @@ int inv_launch_z(const Level& L, const Band& lls, const ZFrames& fr, int nz, con
 	std::vector<InvArgs<TB, TB, TO>> v(nz);
 	for (int f = 0; f < nz; f++)
 		v[f] = inv_args<TB, TO>(L, lls, fr.arena + f * fr.astride, (char*)fr.out + f * fr.ostride, fr.po,
-		                        q ? q + 4 * f : nullptr, S, fr.scratch ? fr.c_base(f) : nullptr, fr.split);
+		                        q ? q + 4 * f : nullptr, S, fr.scratch ? fr.c_base(f) : nullptr, fr.split, fr.lo);
 	if (zargs_put(z, v.data(), v.size() * sizeof(v[0]), st)) return -1;
 	const dim3 grid((L.w + kStripValid - 1) / kStripValid, (v[0].nseg + kWavesPerBlock - 1) / kWavesPerBlock, nz);
 	hipLaunchKernelGGL((k_inv_z<TRANS, TB, TB, TO, S>), grid, dim3(256), 0, st, (const InvArgs<TB, TB, TO>*)z.dev);

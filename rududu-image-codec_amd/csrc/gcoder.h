@@ -17,7 +17,19 @@ struct GBandDesc {
 	int high;            // finest level (HIGH Huffman tables, k >= 1)
 	int has_pin;         // has a parent level (not the coarsest)
 	int par;             // decoder: index into b[] of the parent band, or -1
+	// the compacted pool (GEncArgs::cmp_rel): 1 + the band's index in the
+	// compact block (level 0's V, H, D: DcmpLayout), or 0 (dense at off).
+	// The encoder reads the values at the set bits of each block's record mask
+	// from the block's value stream; the decoder writes that stream, each
+	// block's mask (u16 at cmask_off, walk order) and each chunk's value count
+	// before it (u32 at ccoff_off), relative to the compact block.
+	int cmp;
+	uint32_t cmask_off, ccoff_off;
 };
+// The compact block of a plane (GEncArgs / GDecArgs::cmp_rel != 0): at the
+// plane's arena base + cmp_rel, DcmpLayout (compact.h): u32 nval[3] (written
+// by the decoder), the masks, the chunk offsets, then the values of V, H, D
+// back to back from cvals_off, at most cvcap of them.
 
 // Frames f = 0..n-1 (blockIdx.x): arena + f * astride, out + f * ostride.
 // b[] in coding order: coarsest level first, V, H, D (CodeBand order).
@@ -31,12 +43,14 @@ struct GEncArgs {
 	uint8_t* out;
 	size_t ostride;
 	size_t cap;                      // bytes available at each out
-	uint32_t* res;                   // per frame: file length, status (0 ok, 1 capacity, 2 ring timeout)
+	uint32_t* res;                   // per frame: file length, status (0 ok, 1 capacity, 2 ring timeout, 3 guard, 4 over a compacted pool's capacity)
 	uint32_t status_off;
 	int prio;                        // issue priority by progress: 0 off, 1 or 2 (prio_band, gcoder.hip)
 	const uint32_t* yield;           // the batch stream's level-kernel flag (coder_yield), or null
 	uint64_t* ts;                    // diagnostics: 4 words per frame: the wave's start, end (s_memrealtime, 100 MHz), HW_ID | XCC_ID << 32; or null
 	int w, h, q, trans;
+	long long cmp_rel;               // compacted pool: the compact block's offset from the plane's base; 0: dense
+	uint32_t cvals_off, cvcap;
 	int nb;
 	GBandDesc ll;
 	GBandDesc b[3 * kMaxLevels];
@@ -62,6 +76,8 @@ struct GDecArgs {
 	const uint32_t* yield;           // as GEncArgs::yield
 	const uint32_t* etab;            // the enumDecode<16> pattern table (gc_enum16_table())
 	int w, h;
+	long long cmp_rel;               // as GEncArgs
+	uint32_t cvals_off, cvcap;
 	int nb;
 	GBandDesc ll;
 	GBandDesc b[3 * kMaxLevels];
@@ -96,6 +112,7 @@ inline void gc_bands(const Pyramid& P, GBandDesc& ll, GBandDesc* b, int& nb)
 	auto desc = [&](const Band& B, GBandDesc& d) {
 		d.off = (uint32_t)B.off; d.dx = B.dx; d.dy = B.dy; d.pitch = B.pitch; d.is_int = B.is_int;
 		d.rec_off = d.pin_off = 0; d.high = 0; d.has_pin = 0; d.par = -1;
+		d.cmp = 0; d.cmask_off = d.ccoff_off = 0;
 	};
 	desc(P.L[P.nlev - 1].b[BL], ll);
 	nb = 0;
@@ -111,6 +128,18 @@ inline void gc_bands(const Pyramid& P, GBandDesc& ll, GBandDesc* b, int& nb)
 			d.par = l + 1 < P.nlev ? nb - 3 : -1;
 			nb++;
 		}
+}
+
+// the compacted pool: level 0's three bands (coding order V, H, D) read from
+// / written to the compact block of layout L (compact.h dcmp_layout)
+inline void gc_bands_compact(GBandDesc* b, int nb, const size_t* mask_off, const size_t* coff_off)
+{
+	for (int k = 0; k < 3; k++) {
+		GBandDesc& d = b[nb - 3 + k];
+		d.cmp = 1 + k;
+		d.cmask_off = (uint32_t)mask_off[k];
+		d.ccoff_off = (uint32_t)coff_off[k];
+	}
 }
 
 }  // namespace ric

@@ -509,25 +509,61 @@ GC_DI RecChunk fetch_recs(const uint64_t* rec, const uint8_t* pin, int dx, int d
 // The coefficients of one block: unary + raw remainder + sign each, one
 // geometric context (CGeomCodec::code, geomcodec.h:41-57; block_enum's
 // coefficient loop, bandcodec.cpp:392-401).
+// rank: lane k of cv holds the k-th coefficient of the mask (a compacted
+// pool's value stream), else lane i the coefficient at bit i
 template <typename E>
-GC_DI void code_coefs(E& e, const GTabs& T, uint32_t& geo, uint32_t gc, uint32_t mask, uint32_t cv, uint32_t cb)
+GC_DI void code_coefs(E& e, const GTabs& T, uint32_t& geo, uint32_t gc, uint32_t mask, uint32_t cv, uint32_t cb,
+                      bool rank = false)
 {
 	GGeoCtx g;
 	g.load(geo, gc, T);
+	uint32_t k = 0;
 	while (mask) {
 		const uint32_t i = (uint32_t)__builtin_ctz(mask);
 		mask &= mask - 1;
-		const uint32_t u = lget(cv, cb + i);
+		const uint32_t u = lget(cv, rank ? k++ : cb + i);
 		g.code<true>(e, T, (u >> 1) - 1, u & 1);
 	}
 	geo = lset(geo, gc, g.packed());
 }
 
+// lane-exclusive prefix sum over the wave of popcount(m) (m: 16 bits), and
+// the total: per bit, a ballot and the lane's count of lower lanes that have it
+// (mbcnt) -- a few registers, no shuffles
+GC_DI uint32_t wave_excl_popc(uint32_t m, uint32_t& total)
+{
+	uint32_t o = 0, t = 0;
+	RIC_UNROLL
+	for (int b = 0; b < 16; b++) {
+		const uint64_t bb = __ballot((m >> b) & 1u);
+		o += __builtin_amdgcn_mbcnt_hi((uint32_t)(bb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bb, 0u));
+		t += (uint32_t)__builtin_popcountll(bb);
+	}
+	total = t;
+	return o;
+}
+
+// a compacted pool's value stream: the 64 lanes' loads of values v0 .. v0 +
+// 1023 (zero-extended, as unpack_coef gives a short band's value), none at
+// or past vcap
+GC_DI void fetch_cvals(const int16_t* cv, uint32_t v0, uint32_t vcap, uint32_t (&cn)[16])
+{
+	const uint32_t l = lane_id();
+	RIC_UNROLL
+	for (int g = 0; g < 16; g++) {
+		const uint32_t i = v0 + (uint32_t)g * 64 + l;
+		cn[g] = i < vcap ? (uint32_t)(uint16_t)gld(cv)[i] : 0u;
+	}
+}
+
 // CBandCodec::tree<encode> over the GPU block records (encoder.cpp
 // tree_rec_fast; bandcodec.cpp:484-589 with block_enum :346-478).  high: the
 // finest level (HIGH tables); par: the band has a parent level.
+// cvals (a compacted pool's band, B.cmp): the plane's value stream, vrun the
+// band's first value (advanced past the band's values on return)
 template <typename E>
-GC_DI void tree_enc(E& e, const GTabs& T, const GBandDesc& B, const char* arena, const uint32_t* yield)
+GC_DI void tree_enc(E& e, const GTabs& T, const GBandDesc& B, const char* arena, const uint32_t* yield,
+                    const int16_t* cvals = nullptr, uint32_t vcap = 0, uint32_t* vrun = nullptr)
 {
 	const bool high = B.high, par = B.has_pin;
 	const uint64_t* rec = (const uint64_t*)(arena + B.rec_off);
@@ -552,20 +588,37 @@ GC_DI void tree_enc(E& e, const GTabs& T, const GBandDesc& B, const char* arena,
 	// 16 groups of 4 blocks' coefficients) are issued when chunk c starts and
 	// consumed a whole chunk later, in one wait; chunk c's coefficients then
 	// sit in LDS (g_coef), one 16-lane row per block.
+	// A compacted band (cvals): chunk c's values are the stream's next n_c (the
+	// popcounts of its blocks' record masks, propagated blocks included, as
+	// k_cmp_write lays them out); the 1024 values from chunk c + 1's first are
+	// loaded when chunk c starts, block j's at g_coef[boff_j ..].
+	const bool cmp = cvals != nullptr;
+	uint32_t vpos = cmp ? *vrun : 0u, boff = 0;
 	RecChunk rn = fetch_recs(rec, pin, dx, dy, nblk, 0);
 	uint32_t cn[16], half = 0;
-	RIC_UNROLL
-	for (int g = 0; g < 16; g++) cn[g] = fetch_group(band, is_int, st, dx, dy, nblk, 4 * g, g, half);
+	if (cmp) fetch_cvals(cvals, vpos, vcap, cn);
+	else {
+		RIC_UNROLL
+		for (int g = 0; g < 16; g++) cn[g] = fetch_group(band, is_int, st, dx, dy, nblk, 4 * g, g, half);
+	}
 	for (int s0 = 0; s0 < nblk; s0 += 64) {
 		coder_yield(yield);
 		const RecChunk rc = rn;
 		RIC_UNROLL
-		for (int g = 0; g < 16; g++) g_coef[g * 64 + l] = unpack_coef(cn[g], is_int, half, g);
+		for (int g = 0; g < 16; g++) g_coef[g * 64 + l] = cmp ? cn[g] : unpack_coef(cn[g], is_int, half, g);
+		if (cmp) {
+			uint32_t nc;
+			boff = wave_excl_popc(BlockRec::mask((uint64_t)rc.lo | (uint64_t)rc.hi << 32), nc);
+			vpos += nc;
+		}
 		if (s0 + 64 < nblk) {
 			rn = fetch_recs(rec, pin, dx, dy, nblk, s0 + 64);
 			half = 0;
-			RIC_UNROLL
-			for (int g = 0; g < 16; g++) cn[g] = fetch_group(band, is_int, st, dx, dy, nblk, s0 + 64 + 4 * g, g, half);
+			if (cmp) fetch_cvals(cvals, vpos, vcap, cn);
+			else {
+				RIC_UNROLL
+				for (int g = 0; g < 16; g++) cn[g] = fetch_group(band, is_int, st, dx, dy, nblk, s0 + 64 + 4 * g, g, half);
+			}
 		}
 		const int nj = nblk - s0 < 64 ? nblk - s0 : 64;
 		for (int j = 0; j < nj; j++) {
@@ -577,8 +630,8 @@ GC_DI void tree_enc(E& e, const GTabs& T, const GBandDesc& B, const char* arena,
 				bord.code(e, T, ins, 0);
 				if (ins) continue;
 				e.bits(BlockRec::raw(r), BlockRec::rawlen(r));
-				const uint32_t cv = g_coef[j * 16 + (l & 15)];
-				code_coefs(e, T, geo, BlockRec::gctx(r), mask, cv, 0);
+				const uint32_t cv = g_coef[(cmp ? lget(boff, li) : (uint32_t)j * 16) + (l & 15)];
+				code_coefs(e, T, geo, BlockRec::gctx(r), mask, cv, 0, cmp);
 			} else {
 				uint32_t ctx = 15;
 				if (par) {
@@ -588,20 +641,21 @@ GC_DI void tree_enc(E& e, const GTabs& T, const GBandDesc& B, const char* arena,
 				}
 				tree.code(e, T, ins, ctx);
 				if (ins) continue;
-				const uint32_t cv = g_coef[j * 16 + (l & 15)];
+				const uint32_t cv = g_coef[(cmp ? lget(boff, li) : (uint32_t)j * 16) + (l & 15)];
 				const uint32_t k = BlockRec::k(r);
 				const uint32_t km = lget(kmean, ctx);
 				const uint32_t idx = (km + (1u << 9)) >> 10;
 				const uint32_t h = g_huff[hbase + idx * hrow + k + hoff];
 				const uint32_t rl = BlockRec::rawlen(r);
 				e.bits(((h >> 5) << rl) | BlockRec::raw(r), (h & 31) + rl);
-				code_coefs(e, T, geo, k - 1, mask, cv, 0);
+				code_coefs(e, T, geo, k - 1, mask, cv, 0, cmp);
 				const uint32_t kk = high ? k - 1 : k;
 				kmean = lset(kmean, ctx, (km + (kk << 7) - (km >> 3)) & 0xFFFFu);
 			}
 		}
 		e.maybe_flush();
 	}
+	if (cmp) *vrun = vpos;
 }
 
 // One frame's stream per workgroup (one wave): the reference's CompressImage
@@ -619,7 +673,8 @@ GC_DI void load_huff()
 
 // frame f's whole stream; *end: the coder's end offset (file length 9 + end -
 // 9), the status: 0 ok, 1 capacity, 2 a fused level kernel's ring timeout, 3
-// the LDS ring overran / a guard
+// the LDS ring overran / a guard, 4 the frame's level-0 values exceed a
+// compacted pool's capacity (nothing coded: the caller codes it elsewhere)
 template <uint32_t RING>
 GC_DI uint32_t enc_frame(const GEncArgs& a, int f, uint32_t& end_out)
 {
@@ -627,6 +682,8 @@ GC_DI uint32_t enc_frame(const GEncArgs& a, int f, uint32_t& end_out)
 	uint8_t* out = a.out + (size_t)f * a.ostride;
 	int32_t status = 0;
 	for (int p = 0; p < a.nplanes; p++) status |= *gld((const int32_t*)(arena + p * a.pstride + a.status_off));
+	status = __builtin_amdgcn_readfirstlane(status);
+	if (status & 4) { end_out = 0; return 4; }          // (not coded: over a compacted pool's capacity)
 	GTabs T;
 	T.init();
 	GEnc<RING> e;
@@ -638,9 +695,12 @@ GC_DI uint32_t enc_frame(const GEncArgs& a, int f, uint32_t& end_out)
 		const char* pa = arena + p * a.pstride;
 		if (a.ll.is_int) pred_enc<int32_t>(e, T, a.ll, pa);
 		else pred_enc<int16_t>(e, T, a.ll, pa);
+		const int16_t* cvals = a.cmp_rel ? (const int16_t*)(pa + a.cmp_rel + a.cvals_off) : nullptr;
+		uint32_t vrun = 0;                               // the compacted bands' running value index
 		for (int b = 0; b < a.nb; b++) {
 			if (p + 1 == a.nplanes) prio_band(a.prio, false, b, a.nb);
-			tree_enc(e, T, a.b[b], pa, a.yield);
+			if (a.b[b].cmp && cvals) tree_enc(e, T, a.b[b], pa, a.yield, cvals, a.cvcap, &vrun);
+			else tree_enc(e, T, a.b[b], pa, a.yield);
 		}
 	}
 	const uint32_t end = e.end();
@@ -1177,10 +1237,15 @@ GC_DI uint32_t block_info(const GBandDesc& B, const GBandDesc* P, const char* ar
 // chunks of 64 blocks in scan order; each chunk's values are built in LDS and
 // stored by the lanes (every position of every block, so no Clear() pass), the
 // parent anchors the chunk consumed are cleared by the lanes too.
+// cblk (a compacted pool's band, B.cmp): the plane's compact block; the
+// chunk's blocks go there as masks + values (vpos: the plane's values so far,
+// advanced past the band's), at most vcap values (a stream that decodes more,
+// a corrupt one, is flagged)
 template <bool ETAB>
 GC_DI void tree_dec(GDec& d, const GTabs& T, const GBandDesc& B, const GBandDesc* P, char* arena,
                     const uint32_t (&cnk)[2], const uint32_t (&binom)[2], const uint32_t* etab, const uint32_t* yield,
-                    bool prio_half = false)
+                    bool prio_half = false, char* cblk = nullptr, uint32_t cvals_off = 0, uint32_t vcap = 0,
+                    uint32_t* vpos = nullptr)
 {
 	const bool high = B.high;
 	char* band = arena + B.off;
@@ -1199,6 +1264,7 @@ GC_DI void tree_dec(GDec& d, const GTabs& T, const GBandDesc& B, const GBandDesc
 	const uint32_t hbase = high ? 0u : 256u, hn = high ? 16u : 17u;
 	const uint32_t lmax = is_int ? (1u << 20) : (1u << 15);
 	const int s_half = prio_half ? (nblk / 2) & ~63 : -1;
+	uint32_t cnt_band = 0;                              // (compacted) the band's values so far
 	for (int s0 = 0; s0 < nblk; s0 += 64) {
 		coder_yield(yield);
 		if (s0 == s_half) set_prio<0>(1);
@@ -1263,13 +1329,46 @@ GC_DI void tree_dec(GDec& d, const GTabs& T, const GBandDesc& B, const GBandDesc
 		}
 		__threadfence_block();
 		// the lanes store the chunk
-		if (s0 + (int)l < nblk) {
+		if (cblk) {
+			// compacted: each block's mask (its non-zero positions, raster over
+			// its w x h corner) and those values in that order, the blocks' values
+			// back to back (k_dcmp_expand scatters them into the dense band)
+			const int w = (int)((info >> 8) & 3) + 1, h = (int)((info >> 10) & 3) + 1;
+			const bool in = s0 + (int)l < nblk;
+			uint32_t m = 0;
+			if (in)
+				for (int r = 0; r < h; r++)
+					for (int q = 0; q < w; q++) m |= (g_blk[l * 16 + r * 4 + q] != 0 ? 1u : 0u) << (r * w + q);
+			uint32_t nc;
+			const uint32_t o = wave_excl_popc(m, nc);
+			const uint32_t v0 = *vpos + cnt_band;
+			if (l == 0) gst((uint32_t*)(cblk + B.ccoff_off))[s0 >> 6] = cnt_band;
+			if (in) {
+				gst((uint16_t*)(cblk + B.cmask_off))[s0 + (int)l] = (uint16_t)m;
+				GAS int16_t* vals = gst((int16_t*)(cblk + cvals_off));
+				uint32_t k = v0 + o;
+				for (int r = 0; r < h; r++)
+					for (int q = 0; q < w; q++) {
+						const int v = g_blk[l * 16 + r * 4 + q];
+						if (v == 0) continue;
+						if (k < vcap) vals[k] = (int16_t)v;
+						k++;
+					}
+				if (((info >> 7) & 1) && P) stc(arena + P->off, P->is_int, (long)(by * 2) * P->pitch + bx * 2, 0);
+			}
+			if (v0 + nc > vcap) d.ovf |= 1;
+			cnt_band += nc;
+		} else if (s0 + (int)l < nblk) {
 			const int w = (int)((info >> 8) & 3) + 1, h = (int)((info >> 10) & 3) + 1;
 			for (int r = 0; r < h; r++)
 				for (int q = 0; q < w; q++) stc(band, is_int, (long)(by * 4 + r) * st + bx * 4 + q, g_blk[l * 16 + r * 4 + q]);
 			if (((info >> 7) & 1) && P) stc(arena + P->off, P->is_int, (long)(by * 2) * P->pitch + bx * 2, 0);
 		}
 		d.refill();
+	}
+	if (cblk) {
+		if (lane_id() == 0) gst((uint32_t*)cblk)[B.cmp - 1] = cnt_band;     // nval[k]
+		*vpos += cnt_band;
 	}
 	__threadfence();
 }
@@ -1311,9 +1410,11 @@ GC_DI uint32_t dec_frame(const GDecArgs& a, int f, uint32_t len)
 	for (int p = 0; p + 1 < a.nplanes; p++) {          // colour: Y, Co before the last plane (ric.cpp:207-225)
 		char* pa = arena + p * a.pstride;
 		pred_dec(d, T, a.ll, pa);
+		uint32_t vpos = 0;
 		for (int b = 0; b < a.nb; b++) {
 			const GBandDesc& B = a.b[b];
-			tree_dec<ETAB>(d, T, B, B.par >= 0 ? &a.b[B.par] : nullptr, pa, cnk, binom, a.etab, a.yield);
+			tree_dec<ETAB>(d, T, B, B.par >= 0 ? &a.b[B.par] : nullptr, pa, cnk, binom, a.etab, a.yield, false,
+			               a.cmp_rel && B.cmp ? pa + a.cmp_rel : nullptr, a.cvals_off, a.cvcap, &vpos);
 		}
 	}
 	arena += (a.nplanes - 1) * a.pstride;              // the last (or only) plane, with the diagnostics
@@ -1324,11 +1425,13 @@ GC_DI uint32_t dec_frame(const GDecArgs& a, int f, uint32_t len)
 		for (int i = (int)l; i < B.dx * B.dy && i < 1024; i += 64)
 			gst(a.dbg)[(size_t)f * 2048 + 1024 + i] = (uint32_t)ldc(arena + B.off, B.is_int, (long)(i / B.dx) * B.pitch + i % B.dx);
 	}
+	uint32_t vpos = 0;
 	for (int b = 0; b < a.nb; b++) {
 		const GBandDesc& B = a.b[b];
 		prio_band(a.prio, true, b, a.nb);
 		tree_dec<ETAB>(d, T, B, B.par >= 0 ? &a.b[B.par] : nullptr, arena, cnk, binom, a.etab, a.yield,
-		               a.prio == 3 && b == a.nb - 1);
+		               a.prio == 3 && b == a.nb - 1, a.cmp_rel && B.cmp ? arena + a.cmp_rel : nullptr, a.cvals_off, a.cvcap,
+		               &vpos);
 		dump(b + 1);
 	}
 	// status in bits 0-3; on a staging overrun, the read position (diagnostic)

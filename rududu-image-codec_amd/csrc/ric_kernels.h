@@ -82,6 +82,10 @@ struct ZFrames {
 	// of frame f at arena + f * astride, region C (intermediate LL planes, pRD)
 	// at scratch + f * scstride.  scratch null: one arena per frame.
 	char* scratch = nullptr; size_t scstride = 0; size_t split = 0;
+	// the compacted pool (ric_batch_hybrid_config_ex): the offsets below `lo`
+	// (level 0's three bands) are in the scratch arena as well -- the pool
+	// holds them compacted, not at their pyramid offsets
+	size_t lo = 0;
 	char* c_base(int f) const { return scratch ? scratch + (size_t)f * scstride : arena + (size_t)f * astride; }
 };
 // Per-frame argument array of one batched launch, on the device; re-uploaded

@@ -105,6 +105,7 @@ def lib():
         "ric_batch_encode_gpu": (_I, [_P, _P, _I, _I, _I, _P, ctypes.c_size_t, ctypes.c_size_t, _P]),
         "ric_batch_set_digests": (_I, [_P, _P, ctypes.c_long]),
         "ric_batch_hybrid_config": (_I, [_P, _I, ctypes.c_size_t]),
+        "ric_batch_hybrid_config_ex": (_I, [_P, _I, ctypes.c_size_t, ctypes.c_long]),
         "ric_batch_hybrid_times": (_I, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
         "ric_batch_decode_gpu": (_I, [_P, _P, ctypes.c_size_t, _P, _I, _P]),
         "ric_diag_gdec_dbg": (_I, [_P]),
@@ -608,9 +609,10 @@ class Batch:
         _chk(lib().ric_batch_set_ready(self.h, words.ctypes.data if n else None, n), "ric_batch_set_ready")
         self._ready = words if n else None
 
-    def hybrid_config(self, pool_frames, stream_cap):
-        """Pool of the GPU stream coder (ric_batch_hybrid_config)."""
-        _chk(lib().ric_batch_hybrid_config(self.h, pool_frames, stream_cap), "ric_batch_hybrid_config")
+    def hybrid_config(self, pool_frames, stream_cap, value_cap=-1):
+        """Pool of the GPU stream coder (ric_batch_hybrid_config_ex): value_cap
+        the finest bands' compacted capacity per plane (-1 the default, 0 dense)."""
+        _chk(lib().ric_batch_hybrid_config_ex(self.h, pool_frames, stream_cap, value_cap), "ric_batch_hybrid_config_ex")
 
     def hybrid_times(self):
         """(host side, GPU side) end of the last roundtrip_hybrid, ms from its start."""
