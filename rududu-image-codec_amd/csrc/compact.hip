@@ -115,32 +115,56 @@ __global__ __launch_bounds__(1024) void k_cmp_scan(const CmpArgs* __restrict__ a
 	}
 }
 
+// Each wave gathers its chunk's values into LDS (a lane loads its block's
+// rows as 8-byte words, its values go to the chunk's slots from its prefix),
+// then writes the chunk's run out with consecutive lanes on consecutive values:
+// one coalesced store per 64 values instead of a lane-strided store per value.
 __global__ __launch_bounds__(64 * kCmpWaves) void k_cmp_write(const CmpArgs* __restrict__ ap)
 {
 	const CmpArgs& a = *ap;
 	const int f = blockIdx.z;
 	const char* arena = a.arena + (size_t)f * a.astride;
+	const char* bsrc = a.bsrc ? a.bsrc + (size_t)f * a.bstride : arena;
 	int16_t* out = (int16_t*)(a.out + (size_t)f * a.ostride);
+	__shared__ int16_t stage[kCmpWaves][64 * 16];
+	int16_t* sv = stage[threadIdx.x >> 6];
+	const int l = lane64();
 	for (int c = wave_gid(); c < a.nchunk; c += wave_count()) {
 		const int b = band_of(a, c);
 		const CmpBand& B = a.band[b];
-		const int s = (c - B.chunk0) * 64 + lane64();
+		const int s = (c - B.chunk0) * 64 + l;
 		uint32_t m = block_mask(a, arena, b, s);
-		int tot;
-		const int ex = wave_excl(__popc(m), tot);
-		uint32_t o = a.cnt[(size_t)f * a.cstride + c] + (uint32_t)ex;
-		if (!m) continue;
-		if (a.vcap && o + (uint32_t)__popc(m) > a.vcap) continue;   // over the pool's capacity: flagged by k_cmp_scan
-		int bx, by;
-		scan_block(s, B.dx, B.dy, bx, by);
-		const int w = B.dx - bx * 4 < 4 ? B.dx - bx * 4 : 4;
-		const char* bsrc = a.bsrc ? a.bsrc + (size_t)f * a.bstride : arena;
-		const int16_t* band = (const int16_t*)(bsrc + B.off) + (long)by * 4 * B.pitch + bx * 4;
-		while (m) {                                  // the walk's order: ctz, raster over the w-wide block
-			const int i = __builtin_ctz(m);
-			m &= m - 1;
-			out[o++] = band[(long)(i / w) * B.pitch + i % w];
+		// exclusive prefix of the popcounts: per bit, a ballot and the lanes below
+		uint32_t o = 0, tot = 0;
+#pragma unroll
+		for (int i = 0; i < 16; i++) {
+			const uint64_t bb = __ballot((m >> i) & 1u);
+			o += __builtin_amdgcn_mbcnt_hi((uint32_t)(bb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bb, 0u));
+			tot += (uint32_t)__popcll(bb);
 		}
+		const uint32_t base = a.cnt[(size_t)f * a.cstride + c];
+		if (a.vcap && base + tot > a.vcap) continue;    // over the pool's capacity: flagged by k_cmp_scan
+		if (m) {
+			int bx, by;
+			scan_block(s, B.dx, B.dy, bx, by);
+			const int w = B.dx - bx * 4 < 4 ? B.dx - bx * 4 : 4;
+			const int16_t* band = (const int16_t*)(bsrc + B.off) + (long)by * 4 * B.pitch + bx * 4;
+			// rows of the block (an 8-byte word each: the row pitch keeps the
+			// block's 4 columns inside the row's allocation), values in raster
+			// order over the w-wide block
+			uint32_t k = o;
+			for (int r = 0; r < 4 && m; r++) {
+				const uint32_t rm = m & ((1u << w) - 1u);
+				m >>= w;
+				if (!rm) continue;
+				const uint64_t v = *(const uint64_t*)(band + (long)r * B.pitch);
+				for (uint32_t q = rm; q; q &= q - 1) sv[k++] = (int16_t)(v >> (16 * __builtin_ctz(q)));
+			}
+		}
+		__builtin_amdgcn_wave_barrier();
+		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+		for (uint32_t i = (uint32_t)l; i < tot; i += 64) out[base + i] = sv[i];
+		__builtin_amdgcn_wave_barrier();
 	}
 }
 
