@@ -647,12 +647,13 @@ def main():
         if os.path.exists(sqf) and a.workload == "C3":
             try:
                 sq = json.load(open(sqf))
-                run = sq["runs"]["r4g_v2"]
+                rn = sq.get("default_run", "r4g_v2")
+                run = sq["runs"][rn]
                 coder["issue"] = {k: run[k] for k in ("kernel_s", "SQ_INSTS_SALU", "SQ_INSTS_VALU", "salu_share",
                                                        "instr_per_simd_per_4_cycles", "salu_per_cu_cycle", "wait_frac")
                                   if k in run}
-                coder["issue"]["source"] = "profiles/r04_stream_coder_sq.json runs.r4g_v2 (per stream, %d streams in " \
-                                           "one k_gc_roundtrip launch)" % sq["streams"]
+                coder["issue"]["source"] = "profiles/r04_stream_coder_sq.json runs.%s (per stream, %d streams in " \
+                                           "one k_gc_roundtrip launch)" % (rn, run.get("streams", sq["streams"]))
             except (OSError, ValueError, KeyError):
                 pass
         if balance:

@@ -2009,7 +2009,9 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 	for (int h = 0; h < 2; h++)
 		if (c.st[h]) (void)hipStreamSynchronize(c.st[h]);
 	const bool ok = !bfail(hipStreamSynchronize(b->st), "hipStreamSynchronize");
-	if (trace) fprintf(stderr, "[hybrid] %d coder-frame groups harvested while the launch ran\n", hv_early);
+	if (trace)
+		fprintf(stderr, "[hybrid] %d coder-frame groups harvested while the launch ran; %d frames left to the host "
+		                "(over the compacted pool's value capacity)\n", hv_early, n_fallback);
 	tr("end", rc);
 	for (auto& e : evs) (void)hipEventDestroy(e);
 	if (rc == RIC_E_HIP) clear_status(b);
