@@ -523,21 +523,23 @@ def main():
             # trip group) and the GPU side (its last coder batch) finished; the
             # host share is scaled so both end together (a little before the GPU)
             th, tg = b.hybrid_times()
+            # host round trips per step, not a whole number per thread: the host
+            # pool takes them in groups, so a step may give some threads one more
             if th > 0 and tg > 0:
                 t_eff = th / per_warm                       # host wall ms per round trip per thread
-                per = int(per_warm * (tg - 150.0) / th)
+                nh = int(threads * per_warm * (tg - 150.0) / th)
             else:
                 t_eff = 1.08 * t_host
-                per = int(t_gpu / t_eff)
-            per = max(1, min(per, host_frames_room(a, threads) // threads))
-        per = int(allreduce(per, "min"))      # one split for every rank: the slowest rank's
-        n_host = min(per * threads, nfr - n_gpu)
+                nh = int(threads * t_gpu / t_eff)
+            per = max(threads, min(nh, host_frames_room(a, threads))) / threads
+        per = allreduce(per, "min")           # one split for every rank: the slowest rank's
+        n_host = min(int(round(per * threads)), nfr - n_gpu)
         nstep = n_host + n_gpu
         balance = {"host_round_trip_ms": round(t_host, 1), "host_wall_ms_per_frame": round(t_eff, 1),
                    "gpu_launch_pair_ms": round(t_gpu, 1), "warmup_step_ms": round(t_warm, 1),
                    "warmup_host_side_ms": round(th, 1), "warmup_gpu_side_ms": round(tg, 1),
-                   "host_frames_per_thread": per}
-        progress("balance: host side %.0f ms, GPU side %.0f ms in the last warmup step -> %d host frames per thread"
+                   "host_frames_per_thread": round(per, 2)}
+        progress("balance: host side %.0f ms, GPU side %.0f ms in the last warmup step -> %.2f host frames per thread"
                  % (th, tg, per))
     if b is not None:
         b.prof_enable(True)
