@@ -271,8 +271,8 @@ def test_hybrid_roundtrip_colour(ric, port, w, h, q, t, n, n_host, pool, slots, 
             assert np.array_equal(outs[i].numpy(), port.decode_ric(r)[0].reshape(3, h, w)), (rep, i)
 
 
-@pytest.mark.parametrize("gpu_decode", [1, 0])
-def test_hybrid_compacted_pool_capacity(ric, port, gpu_decode):
+@pytest.mark.parametrize("gpu_decode,c", [(1, 1), (0, 1), (1, 3)])
+def test_hybrid_compacted_pool_capacity(ric, port, gpu_decode, c):
     """The compacted pool (ric_batch_hybrid_config_ex): level 0 held as its
     non-zero values + block masks, the encoder reading and the decoder writing
     that form, the harvest expanding it.  The default capacity, the dense pool
@@ -281,12 +281,12 @@ def test_hybrid_compacted_pool_capacity(ric, port, gpu_decode):
     the same bytes, ready word and pixel digest."""
     import shard
     w, h, n = 256, 192, 7
-    host = [np.full((1, h, w), 100 + i, np.uint8) if i % 2 else ric.synth(w, h, 1, 400 + i) for i in range(n)]
+    host = [np.full((c, h, w), 100 + i, np.uint8) if i % 2 else ric.synth(w, h, c, 400 + i) for i in range(n)]
     frames = [ric.DeviceArray.from_numpy(x) for x in host]
     want = [port.encode_ric(x, 9, 0) for x in host]
     for vc in (-1, 0, 200):
-        b = ric.Batch(w, h, 1, slots=3, threads=2)
-        b.hybrid_config(3, (w * h * 2 + 65536 + 15) // 16 * 16, vc)
+        b = ric.Batch(w, h, c, slots=3, threads=2)
+        b.hybrid_config(3, (w * h * c * 2 + 65536 + 15) // 16 * 16, vc)
         outs = [f.empty_like() for f in frames]
         words = np.zeros(n, np.uint32)
         dig = ric.DeviceArray(n, np.uint64, zero=True)
@@ -300,5 +300,5 @@ def test_hybrid_compacted_pool_capacity(ric, port, gpu_decode):
         for i in range(n):
             assert b.stream(i) == want[i], (vc, i)
             px = outs[i].numpy()
-            assert np.array_equal(px, port.decode_ric(want[i])[0]), (vc, i)
+            assert np.array_equal(px.reshape(-1), port.decode_ric(want[i])[0].reshape(-1)), (vc, i)
             assert d[i] == shard.digest_bytes(px), (vc, i)
