@@ -301,6 +301,18 @@ struct YieldFlag {
 	~YieldFlag() { (void)lower(); }
 };
 
+// RIC_GC_YIELD 2 (the default): the coder waves yield only around the host
+// frames' forward level 0, not around their other levels and inverse levels
+// (those run beside the coder waves unpaused); 1: around all of them; 0:
+// never.  C3 step, 3072 coder streams (profiles/r04_yield_ab.json): 1 10491,
+// 2 10561-10576, 0 10624 Mpix/s, with level 0 in the step at 0.35 / 0.34 /
+// 0.25 of HBM peak.
+bool yield_level0_only()
+{
+	static const bool v = [] { const char* e = getenv("RIC_GC_YIELD"); return !e || atoi(e) == 2; }();
+	return v;
+}
+
 int quant_of(int q, int p) { return q ? quants(q + 20 + (p ? 8 : 0)) : 0; }    // Y, then chroma +C_Q_BOOST (ric.cpp:164-168)
 int lambda_of(int q, int p) { return q ? quants(q + 13 + (p ? 8 : 0)) : 0; }
 
@@ -325,8 +337,9 @@ int gpu_encode_plane(ric_batch* b, int set, int n, int p, const uint8_t* const* 
                      int abase = -1, int amul = 1, uint32_t* yflag = nullptr, char* pool = nullptr, size_t pstr = 0,
                      size_t lo = 0)
 {
+	const bool y0only = yield_level0_only();
 	YieldFlag yf(yflag, b->st);
-	if (yf.raise()) return RIC_E_HIP;
+	if (!y0only && yf.raise()) return RIC_E_HIP;
 	Pyramid& P = b->P;
 	const int s0 = set * b->slots;
 	if (abase < 0) abase = s0;
@@ -373,6 +386,8 @@ int gpu_encode_plane(ric_batch* b, int set, int n, int p, const uint8_t* const* 
 		const int mode = fwdq_mode(P.L[l], trans, qp, vec16);
 		fused[l] = mode != FQ_NONE;
 		auto sp = b->prof.begin(B_FWD + std::min(l, 7), n, b->st);
+		if (y0only && l == 0 && yf.raise()) return RIC_E_HIP;
+		if (y0only && l == 1 && yf.lower()) return RIC_E_HIP;
 		if (mode == FQ_PACKED) {
 			// the batch's planes are 8-bit pixels after the level shift (in8)
 			if (launch_fwdq_level_z(P, l, fr, vec8, vec16, qp, b->zf[set][l], b->st, 1)) return RIC_E_HIP;
@@ -516,7 +531,7 @@ int gpu_decode_plane(ric_batch* b, int set, int n, int p, const int* qs, int tra
 		if (r) return r;
 	}
 	P.set_weight(trans);
-	YieldFlag yf(yflag, b->st);
+	YieldFlag yf(yield_level0_only() ? nullptr : yflag, b->st);
 	if (yf.raise()) return RIC_E_HIP;                                    // (after the copies)
 	std::vector<int> qf(4 * n);
 	for (int l = P.nlev - 1; l >= 0; l--) {
