@@ -219,15 +219,20 @@ def cpu_baseline(W, H, q, trans, threads, per_thread=2):
     lat = run(1, 1)
     points = [run(threads, per_thread)]
     node_share = (hi["nproc"] or 0) // 8
-    if node_share > threads:
-        points.append(run(node_share, 1))
+    quota = hi["cgroup_cpu_quota"]
+    # the CPUs this process is actually granted: the affinity mask and the
+    # cgroup quota (more threads than that only time-share the same CPUs)
+    granted = min(x for x in (hi["affinity_cpus"] or node_share or threads, int(quota) if quota else None, 1 << 30)
+                  if x)
+    if node_share > threads and granted > threads:
+        points.append(run(min(node_share, granted), 1))
     best = max(points, key=lambda p: p["roundtrip_mpix_s"])
-    return {"value": best["roundtrip_mpix_s"], "unit": "Mpixel/s", "cores": best["threads"], "kind": kind,
+    return {"value": best["roundtrip_mpix_s"], "unit": "Mpixel/s", "cores": min(best["threads"], granted), "kind": kind,
             "sample": "%dx%d gray q%d frames, encode then decode: 1 frame on 1 thread (latency); %s (throughput); "
                       "value = the best throughput point (%d threads)"
                       % (W, H, q, ", ".join("%d frames on %d threads (%.1f s)" % (p["frames"], p["threads"], p["wall_s"])
                                             for p in points), best["threads"]),
-            "headline_cores": "%d threads: %s%s" % (best["threads"], "this GPU's CPU share (OMP_NUM_THREADS)"
+            "headline_cores": "%d threads on %d granted CPUs: %s%s" % (best["threads"], min(best["threads"], granted), "this GPU's CPU share (OMP_NUM_THREADS)"
                                                     if best["threads"] == threads else
                                                     "the node's per-GPU share of its cores (nproc / 8)",
                                                     "; the process's cgroup CPU quota is %s CPUs" % hi["cgroup_cpu_quota"]
@@ -627,7 +632,11 @@ def main():
     dec_ms = sum(inv) if all(inv) else None
     t_l0 = per_frame.get("fwd_l0")
     achieved = l0_bytes / (t_l0 * 1e-3) / 1e9 if t_l0 else None
-    traffic = None
+    # the whole 5-level encode (DWT + quantiser over every
+    # level, the headline roofline): the model bytes of a frame over the sum of
+    # its level launches' per-frame times
+    enc_achieved = enc_bytes / (enc_ms * 1e-3) / 1e9 if enc_ms else None
+    traffic = traffic_enc = None
     pmc = os.path.join(REPO, "profiles", "pmc_fwd_l0_batch.json")
     if os.path.exists(pmc):
         try:
@@ -636,6 +645,24 @@ def main():
                 traffic = p.get("hbm_bytes_per_frame")
         except Exception:
             traffic = None
+    pmc_all = os.path.join(REPO, "profiles", "pmc_fwd_levels_batch.json")
+    if os.path.exists(pmc_all):
+        try:
+            p = json.load(open(pmc_all))
+            if p.get("W") == W and p.get("H") == H:
+                traffic_enc = p.get("hbm_bytes_per_frame_all_levels")
+        except Exception:
+            traffic_enc = None
+    # the pool / host payload compaction and the pool's expansion (compact.hip):
+    # GPU work of this path outside the wavelet model.  Model bytes per frame:
+    # compaction reads level 0's three dense 16-bit bands and their block
+    # records (the value stream it writes is not counted); the expansion
+    # writes the dense bands and reads the block masks (its values not counted)
+    l0c = sum(((bx + 3) // 4) * ((by + 3) // 4) for bx, by in
+              ((W // 2, H // 2), (W // 2, H // 2), (W // 2, H // 2)))
+    l0coef = 3 * (W // 2) * (H // 2)
+    cmp_bytes = 2 * l0coef + 8 * l0c
+    dexp_bytes = 2 * l0coef + 2 * l0c
 
     # ---- the stream coder's launches (per launch: kernel time = a wave's time
     # to code one whole stream, with every stream of the launch in flight)
@@ -677,8 +704,12 @@ def main():
             t_iso = pi["fwd_l0"][0] / pi["fwd_l0"][1]
             ach = l0_bytes / (t_iso * 1e-3) / 1e9
             fi = [pi["fwd_l%d" % l][0] / pi["fwd_l%d" % l][1] for l in range(nlev) if pi["fwd_l%d" % l][1]]
-            iso = {"avg_launch_ms": round(pi["fwd_l0"][0] / pi["fwd_l0"][2], 4), "achieved": round(ach, 1),
-                   "frac": round(ach / HBM_PEAK_GBS, 4), "gpu_wavelet_encode": _frac(sum(fi), enc_bytes),
+            we = _frac(sum(fi), enc_bytes)
+            iso = {"avg_launch_ms": round(sum(fi) * slots, 4), "achieved": we.get("GBps"), "frac": we.get("frac"),
+                   "level0": {"avg_launch_ms": round(pi["fwd_l0"][0] / pi["fwd_l0"][2], 4), "achieved": round(ach, 1),
+                              "frac": round(ach / HBM_PEAK_GBS, 4)},
+                   "per_level_us_per_frame": [round(x * 1e3, 2) for x in fi],
+                   "gpu_wavelet_encode": we,
                    "note": "GPU stages alone (ric_batch_diag_gpu), %d frames per launch, 3 iterations, after the "
                            "timed region" % slots}
 
@@ -778,15 +809,29 @@ def main():
         "verified": verified,
         "verified_against": vnote,
         "roofline": {"bound": "hbm",
-                     "kernel": "k_fwdq_pc_z level 0 (fused forward 9/7 DWT + RD quantiser + block records, "
-                               "%d frames per launch)" % slots,
-                     "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                     "traffic": traffic * slots if traffic else None,
-                     "algorithmic_bytes_per_launch": l0_bytes * slots,
-                     "avg_launch_ms": round(per_launch["fwd_l0"], 4) if "fwd_l0" in per_launch else None},
+                     "kernel": "the 5-level forward wavelet encode (SURVEY.md §8(d) DWT + quantiser): k_fwdq_pc_z "
+                               "level 0, k_fwdq_pc2_z levels 1-2, k_fwdq_gen_z levels 3-4 (+ LL TSUQ), fused DWT + "
+                               "RD quantiser + block records, %d frames per launch; per launch = the five level "
+                               "launches of one group" % slots,
+                     "achieved": round(enc_achieved, 1) if enc_achieved else None, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(enc_achieved / HBM_PEAK_GBS, 4) if enc_achieved else None,
+                     "traffic": traffic_enc * slots if traffic_enc else None,
+                     "algorithmic_bytes_per_launch": enc_bytes * slots,
+                     "avg_launch_ms": round(enc_ms * slots, 4) if enc_ms else None,
+                     "level0": {"kernel": "k_fwdq_pc_z level 0", "achieved": round(achieved, 1) if achieved else None,
+                                "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+                                "traffic": traffic * slots if traffic else None,
+                                "algorithmic_bytes_per_launch": l0_bytes * slots,
+                                "avg_launch_ms": round(per_launch["fwd_l0"], 4) if "fwd_l0" in per_launch else None}},
         "gpu_wavelet_encode": _frac(enc_ms, enc_bytes),
         "gpu_wavelet_decode": _frac(dec_ms, dec_bytes),
+        "compaction": {"write": _frac(per_frame.get("compact"), cmp_bytes),
+                       "expand": _frac(per_frame.get("dcmp_expand"), dexp_bytes),
+                       "vs_level0": round((per_frame.get("compact", 0) + per_frame.get("dcmp_expand", 0)) / t_l0, 3)
+                       if t_l0 else None,
+                       "note": "k_cmp_count/scan/write (pool frames and host frames) and k_dcmp_expand, per frame "
+                               "they ran on; bytes: the dense level-0 bands + block records (masks) they read or "
+                               "write, value streams not counted; vs_level0: their time over level 0's"},
         "per_level_us_per_frame": {"fwd": [round(x * 1e3, 2) if x else None for x in fwd],
                                    "inv": [round(x * 1e3, 2) if x else None for x in inv]},
         "stage_ms_per_frame": {k: round(v, 4) for k, v in per_frame.items()},

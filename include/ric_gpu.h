@@ -367,7 +367,11 @@ int ric_video_motion(ric_video* v, uint32_t* mv);
 /* HBM buffers from this library's own HIP runtime (no reference counterpart:
  * the reference is host-only).  Callers that have no HIP runtime of their own
  * (the ctypes binding, the tests, the benchmark) use these, so only this
- * library's runtime is ever mapped into the process.  Copies are synchronous. */
+ * library's runtime is ever mapped into the process.  Copies, memsets and
+ * digests are synchronous to the caller and run on a per-device side stream
+ * of their own: they never wait for the library's kernels in flight (e.g. the
+ * stream coder's launch), and never synchronise the device.  ric_device_free
+ * (hipFree) does synchronise the device: keep it out of a running step. */
 #define RIC_COPY_H2D 1
 #define RIC_COPY_D2H 2
 #define RIC_COPY_D2D 3
@@ -384,6 +388,14 @@ int ric_host_free(void* p);
  * host_out[i] */
 int ric_device_digests(int device, const uint8_t* base, int n, const size_t* off, const size_t* len,
                        unsigned long long* host_out);
+/* the same digest over n host byte runs base + off[i], len[i] bytes each */
+int ric_host_digests(const uint8_t* base, int n, const size_t* off, const size_t* len, unsigned long long* out);
+/* n host byte runs src[i] (len[i] bytes) packed at dst + off[i] on the device
+ * (the gaps between runs zeroed, up to the last run's end): one copy through a
+ * pinned staging buffer of the library's (sized once, >= 64 MiB); dig_out
+ * (optional): each run's digest, taken from its source on the way */
+int ric_device_pack_h2d(int device, uint8_t* dst, int n, const uint8_t* const* src, const size_t* len, const size_t* off,
+                        unsigned long long* dig_out);
 
 /* ------------------------------------------------------------ ric_comm */
 /* The path's one exchange across GPUs: the .ric streams

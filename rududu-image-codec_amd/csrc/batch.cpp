@@ -90,7 +90,7 @@ private:
 // time, frames = streams).
 // B_D2HV: the compacted values of host-coded frames, written into the host mirrors by k_cmp_to_host
 enum { B_PIXIN = 0, B_FWD = 1, B_D2H = 9, B_HENC = 10, B_HDEC = 11, B_H2D = 12, B_INV = 13, B_PIXOUT = 21, B_GENC = 22, B_GDEC = 23,
-       B_D2HV = 24, B_GRT = 25, B_DEXP = 26, B_COUNT = 27 };   // B_DEXP: k_dcmp_expand (part of B_H2D)   // B_GRT: the stream coder's encode + decode as one kernel
+       B_D2HV = 24, B_GRT = 25, B_DEXP = 26, B_CMP = 27, B_COUNT = 28 };   // B_CMP: k_cmp_count / scan / write (pool and host payloads)   // B_DEXP: k_dcmp_expand (part of B_H2D)   // B_GRT: the stream coder's encode + decode as one kernel
 
 struct BProf {
 	bool on = false;
@@ -158,9 +158,9 @@ struct BProf {
 }  // namespace
 
 struct ric_batch {
-	// level 0's hand-off form (ZFrames::ring): the hybrid step runs beside
-	// the stream coder's waves and takes the double buffer (less LDS)
-	int fq_ring = 1;
+	// level 0's hand-off form (ZFrames::ring): the double buffer (0) everywhere
+	// (RIC_FQZ_ASYNC=1: the ring form)
+	int fq_ring = 0;
 	// The host encoder's payload compacted on the GPU (compact.hip): the
 	// 16-bit bands' values in walk order instead of the dense bands.  Per
 	// slot: the stream (d_cmp), chunk counts / offsets, its value count (also
@@ -440,7 +440,11 @@ int d2h_slots(ric_batch* b, int set, int n)
 		// no per-frame copy on another stream: the host tasks find them there
 		// once the group's event has passed); their counts and the dense rest
 		// (int bands, LL, region B) by copies
-		if (launch_compact(b->d_cmp_args + set, b->cmp_nchunk, n, b->st)) return bfail(hipGetLastError(), "compact") ? RIC_E_HIP : RIC_E_HIP;
+		{
+			auto sc = b->prof.begin(B_CMP, n, b->st);
+			if (launch_compact(b->d_cmp_args + set, b->cmp_nchunk, n, b->st)) return bfail(hipGetLastError(), "compact") ? RIC_E_HIP : RIC_E_HIP;
+			b->prof.end(sc);
+		}
 		BCHK(hipMemcpyAsync(b->h_cmp_total + s0, b->d_cmp_total + s0, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, b->st));
 		{
 			auto sv = b->prof.begin(B_D2HV, n, b->st);
@@ -1371,17 +1375,12 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 	// colour frames round-tripped or decoded on the host keep each plane's
 	// bands in a slot of its own: a host group is slots / 3 frames
 	const int C = b->channels;
-	if (C == 3 && b->slots < 3 && (n_host > 0 || gpu_decode != 1)) return RIC_E_ARG;
+	// (a compacted pool can leave any frame to a host round trip: over its value capacity)
+	if (C == 3 && b->slots < 3 && (n_host > 0 || gpu_decode != 1 || b->cp.vcap)) return RIC_E_ARG;
 	if (n == 0) return RIC_OK;
 	if (!outputs_distinct(out, n))
 		return set_last_error("ric_batch_roundtrip_hybrid: out[] buffers must be distinct"), RIC_E_ARG;
 	if (set_dev(b->device)) return RIC_E_HIP;
-	// level 0 beside the coder waves: the double-buffered hand-off for this call
-	struct RingGuard {
-		ric_batch* b;
-		~RingGuard() { b->fq_ring = 1; }
-	} ring_guard{b};
-	b->fq_ring = 0;
 	auto& c = b->cp;
 	Pyramid& P = b->P;
 	const int S = b->slots;
@@ -1547,8 +1546,12 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 				                         kbase(h, g0) + (size_t)p * c.abstride, c.fstride, c.lo);
 				if (r) return r;
 				// a compacted pool: level 0's values (from the arenas) into each frame's compact block
-				if (c.vcap && launch_compact(c.d_pcmp + ((size_t)h * c.pcmp_groups + g0 / S) * C + p, pcmp_nch, gm, b->st))
-					return bfail(hipGetLastError(), "pool compaction") ? RIC_E_HIP : RIC_E_HIP;
+				if (c.vcap) {
+					auto sc = b->prof.begin(B_CMP, gm, b->st);
+					if (launch_compact(c.d_pcmp + ((size_t)h * c.pcmp_groups + g0 / S) * C + p, pcmp_nch, gm, b->st))
+						return bfail(hipGetLastError(), "pool compaction") ? RIC_E_HIP : RIC_E_HIP;
+					b->prof.end(sc);
+				}
 			}
 		}
 		BCHK(hipEventRecord(c.ev_fwd[h], b->st));
@@ -1670,14 +1673,16 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 				x.chunk0[3] = ch;
 				x.vals_off = (uint32_t)c.dl.vals_off;
 				x.vcap = c.vcap;
+				auto sx = b->prof.begin(B_DEXP, gm, b->st);
 				if (launch_dcmp_expand(x, gm, b->st)) return bfail(hipGetLastError(), "k_dcmp_expand") ? RIC_E_HIP : RIC_E_HIP;
+				b->prof.end(sx);
 			}
 			int r = gpu_decode_plane(b, 0, gm, p, qs.data(), trans, false, -1, 1, nullptr,
 			                         kbase(h, g0) + (size_t)p * c.abstride, c.fstride, c.lo);
 			if (r) return r;
 		}
 		const int r = gpu_pix_out(b, 0, gm, qs.data(), pix_out + f0 + g0, 1, f0 + g0);
-		hv_done[j][g0 / S] = 1;
+		if (r == RIC_OK) hv_done[j][g0 / S] = 1;          // a failed group is not taken for harvested
 		return r;
 	};
 	// While the fused launch runs: a group whose frames have all posted their

@@ -15,7 +15,9 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -51,6 +53,65 @@ int on_device(int device)
 	if (device < 0 || device >= n) return RIC_E_ARG;
 	DCHK(hipSetDevice(device));
 	return RIC_OK;
+}
+
+// The per-device side stream of the calls below: every copy, memset and
+// digest runs on it and waits only for itself.  Never the legacy null stream
+// or an implicit device-wide synchronisation (hipFree, hipHostFree): the
+// gather calls these while the stream coder's kernel (seconds) is in flight
+// (round 4 did a hipMalloc + hipFree per digest call; hipFree waits for the
+// whole device).  Scratch only grows; the first use sizes it for a gather
+// chunk (kStageMin), so a step never reallocates.
+constexpr size_t kStageMin = 64u << 20;
+struct Aux {
+	std::mutex mu;
+	hipStream_t st = nullptr;
+	unsigned long long* d_dig = nullptr;   // kDigestRuns words
+	unsigned long long* h_dig = nullptr;   // pinned
+	uint8_t* h_stage = nullptr;            // pinned staging of ric_device_pack_h2d
+	size_t stage_n = 0;
+};
+constexpr int kMaxDev = 64;
+Aux g_aux[kMaxDev];
+
+// (device already current)
+int aux_ready(Aux& a)
+{
+	if (!a.st) DCHK(hipStreamCreateWithFlags(&a.st, hipStreamNonBlocking));
+	if (!a.d_dig) DCHK(hipMalloc(&a.d_dig, sizeof(unsigned long long) * kDigestRuns));
+	if (!a.h_dig) DCHK(hipHostMalloc(&a.h_dig, sizeof(unsigned long long) * kDigestRuns, 0));
+	return RIC_OK;
+}
+
+int aux_stage(Aux& a, size_t bytes)
+{
+	if (a.stage_n >= bytes) return RIC_OK;
+	if (a.h_stage) DCHK(hipHostFree(a.h_stage));   // (growth only: once per size class)
+	a.h_stage = nullptr;
+	a.stage_n = 0;
+	const size_t n = std::max(kStageMin, (bytes + (16u << 20) - 1) / (16u << 20) * (16u << 20));
+	DCHK(hipHostMalloc(&a.h_stage, n, 0));
+	a.stage_n = n;
+	return RIC_OK;
+}
+
+// the digest of one host byte run (the formula of launch_digest): blocks of
+// 4096 bytes, whose position-weighted sum fits 32 bits (255 * 4095 * 4096 / 2)
+unsigned long long host_digest(const uint8_t* p, size_t n)
+{
+	constexpr unsigned long long kMul = 0x9E3779B97F4A7C15ull;
+	unsigned long long s1 = 0, s2 = 0;
+	for (size_t k = 0; k < n; k += 4096) {
+		const size_t m = std::min<size_t>(4096, n - k);
+		uint32_t b1 = 0, b2 = 0;
+		for (size_t j = 0; j < m; j++) {
+			b1 += p[k + j];
+			b2 += (uint32_t)j * p[k + j];
+		}
+		s1 += b1;
+		s2 += b2 + (unsigned long long)k * b1;
+	}
+	return s2 * kMul + s1;
 }
 
 }  // namespace
@@ -110,7 +171,11 @@ int ric_device_copy(int device, void* dst, const void* src, size_t bytes, int ki
 	if (int rc = on_device(device)) return rc;
 	const hipMemcpyKind k = kind == RIC_COPY_H2D ? hipMemcpyHostToDevice
 	                        : kind == RIC_COPY_D2H ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
-	DCHK(hipMemcpy(dst, src, bytes, k));
+	Aux& a = g_aux[device % kMaxDev];
+	std::lock_guard<std::mutex> g(a.mu);
+	if (int rc = aux_ready(a)) return rc;
+	DCHK(hipMemcpyAsync(dst, src, bytes, k, a.st));
+	DCHK(hipStreamSynchronize(a.st));
 	return RIC_OK;
 }
 
@@ -119,7 +184,11 @@ int ric_device_memset(int device, void* p, int value, size_t bytes)
 	if (!p && bytes) return RIC_E_ARG;
 	if (!bytes) return RIC_OK;
 	if (int rc = on_device(device)) return rc;
-	DCHK(hipMemset(p, value, bytes));
+	Aux& a = g_aux[device % kMaxDev];
+	std::lock_guard<std::mutex> g(a.mu);
+	if (int rc = aux_ready(a)) return rc;
+	DCHK(hipMemsetAsync(p, value, bytes, a.st));
+	DCHK(hipStreamSynchronize(a.st));
 	return RIC_OK;
 }
 
@@ -136,16 +205,58 @@ int ric_device_digests(int device, const uint8_t* base, int n, const size_t* off
 	if (n < 0 || (n && (!base || !off || !len || !host_out))) return RIC_E_ARG;
 	if (!n) return RIC_OK;
 	if (int rc = on_device(device)) return rc;
-	unsigned long long* d = nullptr;
-	DCHK(hipMalloc(&d, sizeof(unsigned long long) * (size_t)n));
-	int rc = RIC_OK;
-	if (dfail(hipMemset(d, 0, sizeof(unsigned long long) * (size_t)n), "hipMemset")) rc = RIC_E_HIP;
-	for (int i = 0; i < n && !rc; i++) launch_digest(base + off[i], len[i], d + i, nullptr);
-	if (!rc && dfail(hipGetLastError(), "k_digest")) rc = RIC_E_HIP;
-	if (!rc && dfail(hipMemcpy(host_out, d, sizeof(unsigned long long) * (size_t)n, hipMemcpyDeviceToHost), "hipMemcpy"))
-		rc = RIC_E_HIP;
-	(void)hipFree(d);
-	return rc;
+	Aux& a = g_aux[device % kMaxDev];
+	std::lock_guard<std::mutex> g(a.mu);
+	if (int rc = aux_ready(a)) return rc;
+	for (int i0 = 0; i0 < n; i0 += kDigestRuns) {
+		const int m = std::min(kDigestRuns, n - i0);
+		DCHK(hipMemsetAsync(a.d_dig, 0, sizeof(unsigned long long) * (size_t)m, a.st));
+		launch_digests(base, off + i0, len + i0, m, a.d_dig, a.st);
+		DCHK(hipGetLastError());
+		DCHK(hipMemcpyAsync(a.h_dig, a.d_dig, sizeof(unsigned long long) * (size_t)m, hipMemcpyDeviceToHost, a.st));
+		DCHK(hipStreamSynchronize(a.st));
+		memcpy(host_out + i0, a.h_dig, sizeof(unsigned long long) * (size_t)m);
+	}
+	return RIC_OK;
+}
+
+int ric_host_digests(const uint8_t* base, int n, const size_t* off, const size_t* len, unsigned long long* out)
+{
+	if (n < 0 || (n && (!base || !off || !len || !out))) return RIC_E_ARG;
+	for (int i = 0; i < n; i++) out[i] = host_digest(base + off[i], len[i]);
+	return RIC_OK;
+}
+
+int ric_device_pack_h2d(int device, uint8_t* dst, int n, const uint8_t* const* src, const size_t* len, const size_t* off,
+                        unsigned long long* dig_out)
+{
+	if (n < 0 || (n && (!dst || !src || !len || !off))) return RIC_E_ARG;
+	size_t total = 0;
+	for (int i = 0; i < n; i++) {
+		if (len[i] && !src[i]) return RIC_E_ARG;
+		total = std::max(total, off[i] + len[i]);
+	}
+	if (!n) return RIC_OK;
+	if (int rc = on_device(device)) return rc;
+	Aux& a = g_aux[device % kMaxDev];
+	std::lock_guard<std::mutex> g(a.mu);
+	if (int rc = aux_ready(a)) return rc;
+	if (int rc = aux_stage(a, total)) return rc;
+	// the runs into pinned staging (the gaps zeroed: the payload is shipped
+	// whole), each run's digest taken from its source on the way
+	size_t at = 0;
+	std::vector<int> ord(n);
+	for (int i = 0; i < n; i++) ord[i] = i;
+	std::sort(ord.begin(), ord.end(), [&](int x, int y) { return off[x] < off[y]; });
+	for (int i : ord) {
+		if (off[i] > at) memset(a.h_stage + at, 0, off[i] - at);
+		memcpy(a.h_stage + off[i], src[i], len[i]);
+		if (dig_out) dig_out[i] = host_digest(src[i], len[i]);
+		at = std::max(at, off[i] + len[i]);
+	}
+	DCHK(hipMemcpyAsync(dst, a.h_stage, total, hipMemcpyHostToDevice, a.st));
+	DCHK(hipStreamSynchronize(a.st));
+	return RIC_OK;
 }
 
 // ------------------------------------------------------------------ ric_comm

@@ -1783,11 +1783,15 @@ void fq_launch_pc(FqArgs& a, hipStream_t st)
 		if (async2) hipLaunchKernelGGL(k_fwdq_pc2<true>, grid2, dim3(320), 0, st, a, S, dbg2 & ~128);
 		else hipLaunchKernelGGL(k_fwdq_pc2<false>, grid2, dim3(320), 0, st, a, S, dbg2);
 	} else {
-		static const int async = [] { const char* e = getenv("RIC_FQ_ASYNC"); return e ? atoi(e) : 1; }();
+		// the double-buffered hand-off by default: the ring form's consumer
+		// state spills to scratch under the 128-VGPR bound of four waves per
+		// SIMD (28 bytes per lane; measured round 5: 58 against 71 us per 8K frame)
+		static const int async = [] { const char* e = getenv("RIC_FQ_ASYNC"); return e ? atoi(e) : 0; }();
 		const dim3 grid = onewg ? dim3(1, 1) : dim3(nstrip, a.nseg);
 		if (onewg) dbg |= 4;
 		if (async && a.in8) hipLaunchKernelGGL((k_fwdq_pc<true, false>), grid, dim3(256), 0, st, a, S, dbg & ~128);
 		else if (async) hipLaunchKernelGGL((k_fwdq_pc<true, true>), grid, dim3(256), 0, st, a, S, dbg & ~128);
+		else if (a.in8) hipLaunchKernelGGL((k_fwdq_pc<false, false>), grid, dim3(256), 0, st, a, S, dbg);
 		else hipLaunchKernelGGL((k_fwdq_pc<false, true>), grid, dim3(256), 0, st, a, S, dbg);
 	}
 }

@@ -1503,11 +1503,12 @@ __global__ void __launch_bounds__(64) k_gc_roundtrip(const GEncArgs* __restrict_
 	// the decoded bands are the harvest's input, read by kernels the host
 	// launches while this one still runs (on any XCD): written back (agent-scope
 	// release) before the word that announces them.  posted_dec[f] = the decoder's
-	// result (0x80: the encode failed) | 0x100 | tag << 12
+	// status (its low 7 bits; a diagnostic read position stays in res[f] only;
+	// 0x80: the encode failed) | 0x100 | tag << 12
 	if (posted_dec) {
 		__threadfence();
 		if (lane_id() == 0)
-			__hip_atomic_store(posted_dec + f, (rc ? 0x80u : r) | 0x100u | tag << 12, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+			__hip_atomic_store(posted_dec + f, (rc ? 0x80u : (r & 0x7Fu)) | 0x100u | tag << 12, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 	}
 }
 }  // namespace

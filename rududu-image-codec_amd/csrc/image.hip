@@ -3,6 +3,7 @@
 // the unshift/clip (:237-240) and YCoCgtoRGB (:93-112).  All arithmetic is the
 // reference's `short` arithmetic.
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include "ric_types.h"
 #include "ric_image.h"
 
@@ -264,6 +265,56 @@ __global__ __launch_bounds__(256) void k_digest(const uint8_t* __restrict__ p, s
 	if (threadIdx.x == 0) atomicAdd(out, part[0] + part[1] + part[2] + part[3]);
 }
 }  // namespace
+
+namespace {
+// ric_device_digests: one launch over a gather chunk's streams (blockIdx.y =
+// run), each workgroup striding over its run 16 bytes per thread; the run's
+// workgroups reduce through one 64-bit atomic each into a zeroed word
+struct DigestRuns {
+	const uint8_t* base;
+	size_t off[kDigestRuns], len[kDigestRuns];
+};
+__global__ __launch_bounds__(256) void k_digests(DigestRuns r, unsigned long long* out)
+{
+	const int run = (int)blockIdx.y;
+	const size_t n = r.len[run];
+	const uint8_t* p = r.base + r.off[run];
+	unsigned long long s = 0;
+	for (size_t i0 = ((size_t)blockIdx.x * 256 + threadIdx.x) * 16; i0 < n; i0 += (size_t)gridDim.x * 256 * 16) {
+		if (i0 + 16 <= n && ((uintptr_t)(p + i0) & 15) == 0) {
+			const uint4 v = *(const uint4*)(p + i0);
+			const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+			for (int k = 0; k < 16; k++) s += (unsigned long long)((w[k >> 2] >> (8 * (k & 3))) & 255u) * ((i0 + k) * kDigestMul + 1);
+		} else {
+			for (size_t i = i0; i < i0 + 16 && i < n; i++) s += (unsigned long long)p[i] * (i * kDigestMul + 1);
+		}
+	}
+#pragma unroll
+	for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+	__shared__ unsigned long long part[4];
+	if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+	__syncthreads();
+	if (threadIdx.x == 0 && (part[0] | part[1] | part[2] | part[3])) atomicAdd(out + run, part[0] + part[1] + part[2] + part[3]);
+}
+}  // namespace
+
+void launch_digests(const uint8_t* base, const size_t* off, const size_t* len, int n, unsigned long long* out, hipStream_t st)
+{
+	if (n <= 0) return;
+	DigestRuns r;
+	r.base = base;
+	size_t mx = 0;
+	for (int i = 0; i < kDigestRuns; i++) {
+		r.off[i] = i < n ? off[i] : 0;
+		r.len[i] = i < n ? len[i] : 0;
+		mx = std::max(mx, r.len[i]);
+	}
+	if (!mx) return;
+	// at most 64 workgroups per run (a 64 MiB chunk of 64 streams: 4096)
+	const size_t gx = std::min<size_t>(64, (mx + 16 * 256 - 1) / (16 * 256));
+	hipLaunchKernelGGL(k_digests, dim3((unsigned)gx, (unsigned)n), dim3(256), 0, st, r, out);
+}
 
 void launch_digest(const uint8_t* p, size_t n, unsigned long long* out, hipStream_t st)
 {

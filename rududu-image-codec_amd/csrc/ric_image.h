@@ -15,4 +15,8 @@ void launch_pix_out(const int16_t* planes_in, long pi, int w, int h, int channel
 // mod 2^64, added into *out (zero it first): an order-free checksum of a
 // decoded frame (ric_batch_set_digests)
 void launch_digest(const uint8_t* p, size_t n, unsigned long long* out, hipStream_t st);
+// the same over up to kDigestRuns runs base + off[i] (len[i] bytes each) in one
+// launch, run i's digest to out[i] (written, not added)
+constexpr int kDigestRuns = 64;
+void launch_digests(const uint8_t* base, const size_t* off, const size_t* len, int n, unsigned long long* out, hipStream_t st);
 }  // namespace ric

@@ -74,9 +74,10 @@ struct ZFrames {
 	void* out = nullptr; size_t ostride = 0; long po = 0;
 	int nz = 0;
 	// level 0 of the fused forward: the LDS ring hand-off (1, 32 KiB per
-	// workgroup) or the double buffer (0, 20 KiB: more workgroups fit beside
-	// the stream coder's waves)
-	int ring = 1;
+	// workgroup) or the double buffer (0, the default: 20 KiB, so more
+	// workgroups fit beside the stream coder's waves, and no scratch spills --
+	// the ring form's consumers spill 28 bytes per lane at 128 VGPRs)
+	int ring = 0;
 	// Split arenas (the GPU stream coder's pool): regions A and B (bands,
 	// status word, records, parent info: offsets below `split` = Pyramid::b_end)
 	// of frame f at arena + f * astride, region C (intermediate LL planes, pRD)

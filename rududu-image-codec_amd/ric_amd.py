@@ -127,6 +127,8 @@ def lib():
         "ric_device_memset": (_I, [_I, _P, _I, _S]),
         "ric_device_sync": (_I, [_I]),
         "ric_device_digests": (_I, [_I, _P, _I, _P, _P, _P]),
+        "ric_host_digests": (_I, [_P, _I, _P, _P, _P]),
+        "ric_device_pack_h2d": (_I, [_I, _P, _I, _P, _P, _P, _P]),
         "ric_comm_unique_id": (_I, [_P, _S]),
         "ric_comm_create": (_I, [ctypes.POINTER(_P), _P, _I, _I, _I]),
         "ric_comm_destroy": (None, [_P]),
@@ -279,6 +281,34 @@ def device_digests(device, base, offs, lens):
         _chk(lib().ric_device_digests(device, _ptr(base), n, o.ctypes.data, ln.ctypes.data, out.ctypes.data),
              "ric_device_digests")
     return out
+
+
+def host_digests(base, offs, lens):
+    """ric_host_digests: the same digest over host byte runs of `base` (a numpy
+    array or a pointer)."""
+    n = len(offs)
+    o = np.ascontiguousarray(offs, np.uint64)
+    ln = np.ascontiguousarray(lens, np.uint64)
+    out = np.zeros(n, np.uint64)
+    if n:
+        _chk(lib().ric_host_digests(_ptr(base), n, o.ctypes.data, ln.ctypes.data, out.ctypes.data), "ric_host_digests")
+    return out
+
+
+def device_pack_h2d(device, dst, srcs, offs):
+    """ric_device_pack_h2d: host byte runs srcs[i] (numpy uint8 arrays or bytes)
+    packed at device dst + offs[i] in one copy; returns their digests."""
+    n = len(srcs)
+    arrs = [np.frombuffer(x, np.uint8) if not isinstance(x, np.ndarray) else np.ascontiguousarray(x).reshape(-1)
+            for x in srcs]
+    ptrs = (ctypes.c_void_p * max(n, 1))(*[a.ctypes.data for a in arrs])
+    ln = np.ascontiguousarray([a.size for a in arrs], np.uint64)
+    o = np.ascontiguousarray(offs, np.uint64)
+    dig = np.zeros(n, np.uint64)
+    if n:
+        _chk(lib().ric_device_pack_h2d(device, _ptr(dst), n, ptrs, ln.ctypes.data, o.ctypes.data, dig.ctypes.data),
+             "ric_device_pack_h2d")
+    return dig
 
 
 class Comm:
@@ -489,7 +519,7 @@ class Wavelet2D:
 
 
 BATCH_STAGES = (["pix_in"] + ["fwd_l%d" % l for l in range(8)] + ["d2h", "host_enc", "host_dec", "h2d"] +
-                ["inv_l%d" % l for l in range(8)] + ["pix_out", "gpu_enc", "gpu_dec", "d2h_values", "gpu_rt", "dcmp_expand"])
+                ["inv_l%d" % l for l in range(8)] + ["pix_out", "gpu_enc", "gpu_dec", "d2h_values", "gpu_rt", "dcmp_expand", "compact"])
 
 
 def _ptrs(xs):

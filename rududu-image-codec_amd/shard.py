@@ -90,6 +90,20 @@ def digest_bytes(a):
         return np.uint64(s2 * _DMUL + s1)
 
 
+def _host_digests(buf, offs, lens):
+    """Digests of host byte runs: the library's native loop (ric_host_digests,
+    no GPU needed) when it loads, else numpy."""
+    try:
+        import ric_amd
+        return ric_amd.host_digests(buf, offs, lens)
+    except (ImportError, OSError):
+        return np.array([digest_bytes(buf[o:o + n]) for o, n in zip(offs, lens)], np.uint64)
+
+
+def _as_u8(data):
+    return np.frombuffer(data, np.uint8) if not isinstance(data, np.ndarray) else data.reshape(-1)
+
+
 class GlooTransport:
     """The gather's CPU transport: torch.distributed (gloo) point-to-point on
     host buffers (numpy uint8 arrays)."""
@@ -101,8 +115,19 @@ class GlooTransport:
         return np.zeros(max(int(nbytes), 16), np.uint8)
 
     def put(self, buf, off, data):
-        src = np.frombuffer(data, np.uint8) if not isinstance(data, np.ndarray) else data.reshape(-1)
+        src = _as_u8(data)
         buf[off:off + src.size] = src
+
+    def put_many(self, buf, srcs, offs):
+        """Streams into buf at offs (the gaps zeroed); returns their digests."""
+        at = 0
+        for x, o in zip(srcs, offs):
+            x = _as_u8(x)
+            if o > at:
+                buf[at:o] = 0
+            buf[o:o + x.size] = x
+            at = o + x.size
+        return _host_digests(buf, offs, [_as_u8(x).size for x in srcs])
 
     def get(self, buf, off, n):
         return buf[off:off + n]
@@ -119,13 +144,17 @@ class GlooTransport:
             r.wait()
 
     def digests(self, buf, offs, lens):
-        return np.array([digest_bytes(buf[o:o + n]) for o, n in zip(offs, lens)], np.uint64)
+        return _host_digests(buf, offs, lens)
 
 
 class RcclTransport:
     """The gather's GPU transport: the library's RCCL communicator (ric_comm,
-    xGMI between the GPUs of a node) on device buffers; streams are staged
-    from their host buffers into a device chunk, digested on the device."""
+    xGMI between the GPUs of a node) on device buffers.  A chunk's streams go
+    from their host buffers to the device in one copy through the library's
+    pinned staging (ric_device_pack_h2d, digests taken on the way); rank 0
+    digests what it received on the device (ric_device_digests).  Every copy
+    and digest runs on the library's side stream and RCCL on the
+    communicator's: none waits for the stream coder's kernel in flight."""
 
     def __init__(self, comm, device=0):
         import ric_amd
@@ -138,10 +167,13 @@ class RcclTransport:
         return self.R.DeviceArray(max(int(nbytes), 16), np.uint8, self.device)
 
     def put(self, buf, off, data):
-        src = np.frombuffer(data, np.uint8) if not isinstance(data, np.ndarray) else data.reshape(-1)
+        src = _as_u8(data)
         if src.size:
             self.R._chk(self.R.lib().ric_device_copy(self.device, buf.data_ptr() + off, src.ctypes.data, src.size,
                                                      self.R.RIC_COPY_H2D), "gather H2D")
+
+    def put_many(self, buf, srcs, offs):
+        return self.R.device_pack_h2d(self.device, buf, srcs, offs)
 
     def get(self, buf, off, n):
         # into one pinned sink buffer, reused every round (rank 0 holds no more)
@@ -165,12 +197,14 @@ class StreamGather:
     A round: every sender still active sends one chunk -- a header (round,
     count, done, payload bytes, then per stream: its index, length and
     digest) and the payload (whole streams back to back at 16-byte offsets,
-    at most `chunk_bytes`, at most MAX_PER_CHUNK streams) -- and rank 0
-    receives them all, checks each stream's digest against the sender's, and
-    hands each stream to `on_stream(rank, index, bytes)` from its sink buffer.
-    A sender takes into a chunk the streams that are ready (any order) and
-    waits only when none is; its last chunk carries `done`.  Rank 0's memory:
-    one chunk buffer per peer on the transport, whatever the number of streams.
+    at most `chunk_bytes`, at most MAX_PER_CHUNK streams), as one group -- and
+    rank 0 receives the headers, then the payloads, checks each stream's
+    digest against the sender's, and hands each stream to
+    `on_stream(rank, index, bytes)` from its sink buffer.  A sender takes into
+    a chunk the streams that are ready (any order) and waits only when none
+    is; its last chunk carries `done`.  Rank 0's memory: one chunk buffer per
+    peer on the transport, whatever the number of streams; a peer whose chunk
+    is larger (its header announces the payload's size) grows that buffer.
     """
 
     def __init__(self, transport, rank, world, chunk_bytes=64 << 20):
@@ -180,14 +214,17 @@ class StreamGather:
         self.hdr = [self.t.alloc(HDR_WORDS * 8) for _ in range(max(world - 1, 1))]
         if rank == 0:
             self.bufs = [self.t.alloc(self.chunk) for _ in range(world - 1)]
+            self.cap = [self.chunk] * max(world - 1, 1)
         else:
             self.bufs = [self.t.alloc(self.chunk)]
+            self.cap = [self.chunk]
         self.stats = {}
 
     # ---- sender
-    def send(self, n, words, data, poll_s=0.0005, stop=None):
+    def send(self, n, words, data, poll_s=0.0005, stop=None, bias=0):
         """Ship streams 0..n-1 of this rank.  words: a uint32 array whose
-        word i becomes stream i's length once it is ready (ric_batch_set_ready;
+        word i becomes stream i's length + bias once it is ready
+        (ric_batch_set_ready: bias 0, every .ric file is at least 9 bytes;
         0 until then); data(i, length) -> its bytes (host).  stop(): an
         optional check that raises when the producer failed."""
         import time
@@ -200,7 +237,7 @@ class StreamGather:
             while True:
                 cand = np.flatnonzero(pending & (words[:n] != 0)) if left else []
                 for i in cand[:MAX_PER_CHUNK]:
-                    ln = int(words[i])
+                    ln = int(words[i]) - bias
                     if ln > self.chunk:
                         raise ValueError("stream %d (%d bytes) larger than the gather chunk (%d)" % (i, ln, self.chunk))
                     o = (off + 15) & ~15
@@ -217,17 +254,14 @@ class StreamGather:
             for i, _ in take:
                 pending[i] = False
             left -= len(take)
-            for (i, ln), o in zip(take, offs):
-                self.t.put(self.bufs[0], o, data(i, ln))
-            dg = np.asarray(self.t.digests(self.bufs[0], offs, [ln for _, ln in take]), np.uint64)
+            dg = np.asarray(self.t.put_many(self.bufs[0], [data(i, ln) for i, ln in take], offs), np.uint64)
             hdr[:] = 0
             hdr[0], hdr[1], hdr[2], hdr[3] = rnd, len(take), int(left == 0), off
             for k, (i, ln) in enumerate(take):
                 hdr[4 + 3 * k], hdr[5 + 3 * k] = i, ln
             hdr[6:6 + 3 * len(take):3] = dg.view(np.int64)
             self.t.put(self.hdr[0], 0, hdr.view(np.uint8))
-            self.t.sendrecv([(0, True, self.hdr[0], HDR_WORDS * 8)])
-            self.t.sendrecv([(0, True, self.bufs[0], off)])
+            self.t.sendrecv([(0, True, self.hdr[0], HDR_WORDS * 8), (0, True, self.bufs[0], off)])
             sent += len(take)
             nbytes += off
             rnd += 1
@@ -241,18 +275,25 @@ class StreamGather:
         """Receive every peer's streams; returns per-rank counts and bytes and
         the digest mismatches.  to_host: every chunk also lands in the
         transport's host sink (where a server would write the files out)."""
+        import time
         active = list(range(1, self.world))
         counts = [0] * self.world
         nbytes = [0] * self.world
         bad = []
         rnd = 0
+        t_busy = 0.0
         while active:
             self.t.sendrecv([(r, False, self.hdr[r - 1], HDR_WORDS * 8) for r in active])
+            t0 = time.perf_counter()
             heads = {}
             for r in active:
                 h = np.frombuffer(bytes(self.t.get(self.hdr[r - 1], 0, HDR_WORDS * 8)), np.int64).copy()
-                if h[0] != rnd or h[1] > MAX_PER_CHUNK or h[3] > self.chunk:
+                if h[0] != rnd or h[1] > MAX_PER_CHUNK or h[3] < 0:
                     raise RuntimeError("gather: bad chunk header from rank %d (round %d): %s" % (r, rnd, h[:4]))
+                if h[3] > self.cap[r - 1]:
+                    # a peer with a larger chunk (e.g. gather_streams' per-rank sizes)
+                    self.bufs[r - 1] = self.t.alloc(int(h[3]))
+                    self.cap[r - 1] = int(h[3])
                 heads[r] = h
             self.t.sendrecv([(r, False, self.bufs[r - 1], int(heads[r][3])) for r in active])
             for r in active:
@@ -277,18 +318,22 @@ class StreamGather:
                             on_stream(r, int(idx[j]), sink[offs[j]:offs[j] + int(ln[j])])
                 counts[r] += k
                 nbytes[r] += int(h[3])
+            t_busy += time.perf_counter() - t0
             active = [r for r in active if not heads[r][2]]
             rnd += 1
-        self.stats = {"rounds": rnd, "streams": counts, "bytes": nbytes, "digest_mismatches": bad}
+        self.stats = {"rounds": rnd, "streams": counts, "bytes": nbytes, "digest_mismatches": bad,
+                      "rank0_busy_s": t_busy}
         return self.stats
 
 
 def gather_streams(local, transport, rank, world, chunk_bytes=1 << 20):
     """One-shot gather of byte streams (e.g. C4's tiles): rank 0 gets every
-    rank's list in rank order (its own first), others None."""
+    rank's list in rank order (its own first), others None.  Each sender's
+    chunk fits its own longest stream; rank 0 grows a peer's buffer to what
+    that peer's header announces.  Empty streams are shipped too."""
     g = StreamGather(transport, rank, world, max(chunk_bytes, max([len(s) for s in local] + [16]) + 16))
     if rank != 0:
-        g.send(len(local), np.array([len(x) for x in local], np.uint32), lambda i, n: local[i])
+        g.send(len(local), np.array([len(x) + 1 for x in local], np.uint32), lambda i, n: local[i], bias=1)
         return None
     got = [dict() for _ in range(world)]
     g.receive(lambda r, i, b: got[r].__setitem__(i, bytes(b)))
@@ -300,28 +345,27 @@ def gather_streams(local, transport, rank, world, chunk_bytes=1 << 20):
 def scatter_streams(per_rank, transport, rank, world):
     """The decode side of gather_streams: rank 0 holds one list of byte
     streams per rank (`per_rank`, ignored elsewhere); every rank gets its own
-    list.  Per peer a header (count, lengths) then the payload, point to point."""
+    list.  Per peer: a count, the lengths, then the payload, point to point."""
     if rank == 0:
         for r in range(1, world):
             lst = per_rank[r]
-            hdr = np.zeros(HDR_WORDS, np.int64)
-            if len(lst) > MAX_PER_CHUNK:
-                raise ValueError("scatter: at most %d streams per rank" % MAX_PER_CHUNK)
-            hdr[0] = len(lst)
-            hdr[1:1 + len(lst)] = [len(x) for x in lst]
+            cnt = np.array([len(lst)], np.int64)
+            lens = np.array([len(x) for x in lst] or [0], np.int64)
             payload = b"".join(lst)
-            hb = transport.alloc(HDR_WORDS * 8)
-            transport.put(hb, 0, hdr.view(np.uint8))
+            cb = transport.alloc(8)
+            transport.put(cb, 0, cnt.view(np.uint8))
+            lb = transport.alloc(lens.nbytes)
+            transport.put(lb, 0, lens.view(np.uint8))
             pb = transport.alloc(len(payload))
             transport.put(pb, 0, payload)
-            transport.sendrecv([(r, True, hb, HDR_WORDS * 8)])
-            transport.sendrecv([(r, True, pb, len(payload))])
+            transport.sendrecv([(r, True, cb, 8), (r, True, lb, 8 * len(lst)), (r, True, pb, len(payload))])
         return list(per_rank[0])
-    hb = transport.alloc(HDR_WORDS * 8)
-    transport.sendrecv([(0, False, hb, HDR_WORDS * 8)])
-    hdr = np.frombuffer(bytes(transport.get(hb, 0, HDR_WORDS * 8)), np.int64)
-    k = int(hdr[0])
-    lens = [int(x) for x in hdr[1:1 + k]]
+    cb = transport.alloc(8)
+    transport.sendrecv([(0, False, cb, 8)])
+    k = int(np.frombuffer(bytes(transport.get(cb, 0, 8)), np.int64)[0])
+    lb = transport.alloc(8 * max(k, 1))
+    transport.sendrecv([(0, False, lb, 8 * k)])
+    lens = [int(x) for x in np.frombuffer(bytes(transport.get(lb, 0, 8 * k)), np.int64)] if k else []
     pb = transport.alloc(sum(lens))
     transport.sendrecv([(0, False, pb, sum(lens))])
     data = bytes(transport.get(pb, 0, sum(lens)))

@@ -199,3 +199,59 @@ def test_digest_matches_device_formula():
     import bench
     a = np.random.default_rng(3).integers(0, 256, 100003, dtype=np.uint8)
     assert shard.digest_bytes(a) == bench.pixel_digest(a)
+
+
+def test_host_digests_native():
+    """ric_host_digests (the gloo transport's and the RCCL sender's digest) is
+    the same formula: runs longer than its 4096-byte blocks, odd offsets,
+    empty runs."""
+    import ric_amd
+    rng = np.random.default_rng(5)
+    buf = rng.integers(0, 256, 300000, dtype=np.uint8)
+    buf[1000:20000] = 255                     # the 32-bit block sums at their largest
+    offs = [0, 1, 17, 4095, 4096, 8191, 100, 0]
+    lens = [0, 1, 5000, 4097, 70000, 123456, 19000, 300000]
+    got = ric_amd.host_digests(buf, offs, lens)
+    want = [shard.digest_bytes(buf[o:o + n]) for o, n in zip(offs, lens)]
+    assert [int(x) for x in got] == [int(x) for x in want]
+
+
+def test_put_many_packs_and_digests():
+    t = shard.GlooTransport(None)
+    buf = t.alloc(1 << 16)
+    buf[:] = 7
+    srcs = [b"abc", np.arange(100, dtype=np.uint8), b"", b"xyz" * 50]
+    offs = [0, 16, 128, 128]
+    dg = t.put_many(buf, srcs, offs)
+    assert bytes(buf[:3]) == b"abc" and not buf[3:16].any()
+    assert np.array_equal(buf[16:116], np.arange(100, dtype=np.uint8)) and not buf[116:128].any()
+    assert bytes(buf[128:278]) == b"xyz" * 50
+    assert [int(x) for x in dg] == [int(shard.digest_bytes(np.frombuffer(s, np.uint8) if isinstance(s, bytes) else s))
+                                    for s in srcs]
+
+
+def _worker_big(rank, world, port, q):
+    """gather_streams with a peer whose streams are larger than rank 0's (and
+    than 1 MiB), empty streams included; scatter_streams of more than 64
+    streams per rank."""
+    dist = _init(rank, world, port)
+    import shard as S
+    t = S.GlooTransport(dist)
+    rng = np.random.default_rng(rank)
+    sizes = {0: [100, 0], 1: [3 << 20, 0, 1500000, 7], 2: [0]}[rank]
+    local = [rng.integers(0, 256, n, dtype=np.uint8).tobytes() for n in sizes]
+    got = S.gather_streams(local, t, rank, world)
+    per_rank = None
+    if rank == 0:
+        per_rank = [[bytes([r, i % 256]) * (i % 5) for i in range(70 + r)] for r in range(world)]
+    back = S.scatter_streams(per_rank, t, rank, world)
+    q.put((rank, (local, got, back)))
+    dist.destroy_process_group()
+
+
+def test_gather_big_and_empty_streams_scatter_many_gloo():
+    out = _spawn(_worker_big, 3)
+    got = out[0][1]
+    assert [g for g in got] == [out[r][0] for r in range(3)]
+    for r in range(3):
+        assert out[r][2] == [bytes([r, i % 256]) * (i % 5) for i in range(70 + r)]
