@@ -356,13 +356,20 @@ int gpu_encode_plane(ric_batch* b, int set, int n, int p, const uint8_t* const* 
 		}
 		if (direct) BCHK(hipMemset2DAsync(pool + P.status_off, pstr, 0, sizeof(int32_t), n, b->st));
 	}
-	if (p == 0) {
+	const int quant = quant_of(q, p), lambda = lambda_of(q, p);
+	P.set_weight(trans);
+	// a gray frame's level 0 reads its u8 pixels itself (k_fwdq_pc_z8, the
+	// level shift fused): no coding plane written or read (RIC_PIX8=0: off)
+	static const bool pix8_on = [] { const char* e = getenv("RIC_PIX8"); return !e || atoi(e) != 0; }();
+	int q0 = quant;
+	bool u8 = pix8_on && p == 0 && b->channels == 1 && n <= 32 && (b->w & 7) == 0 &&
+	          fwdq_mode(P.L[0], trans, level_qp(P, 0, q0, lambda), 1) == FQ_PACKED;
+	for (int i = 0; i < n && u8; i++) u8 = ((uintptr_t)pix[i] & 7) == 0;
+	if (p == 0 && !u8) {
 		auto sp = b->prof.begin(B_PIXIN, n, b->st);
 		for (int i = 0; i < n; i++) launch_pix_in(pix[i], b->plane(s0 + i, 0), b->w, b->h, b->pitch, b->channels, q, b->st);
 		b->prof.end(sp);
 	}
-	const int quant = quant_of(q, p), lambda = lambda_of(q, p);
-	P.set_weight(trans);
 	bool fused[kMaxLevels] = {};
 	bool ll_done = false;
 	int qin = quant;
@@ -376,6 +383,7 @@ int gpu_encode_plane(ric_batch* b, int set, int n, int p, const uint8_t* const* 
 		}
 		if (l == 0) {
 			fr.src = b->plane(s0, p); fr.sstride = b->pstride; fr.sp = b->pitch;
+			if (u8) { fr.pix8 = pix; fr.sh8 = q ? 4 : 0; }   // SHIFT, src/ric/ric.cpp:39,144-148
 		} else {
 			const Band& LL = P.L[l - 1].b[BL];
 			fr.src = b->arena(abase) + LL.off; fr.sstride = ast; fr.sp = LL.pitch;

@@ -273,55 +273,26 @@ struct GeoM {                                                   // CGeomCodec
 // not re-read from memory after every coefficient store (a band store may
 // alias the uint16_t model words for the compiler).
 struct GeoReg {
-	// the context's idx-dependent parameters kept ready (k, the adaptation
-	// shift s, its two thresholds), reloaded only when idx moves
-	uint32_t freq, idx, k, s, th0, span;
-	RIC_AI void params()
-	{
-		k = kGeoK[idx]; s = kGeoShift[idx];
-		th0 = kGeoThres[s - 1]; span = (uint32_t)(kGeoThres[s] - kGeoThres[s - 1]);
-	}
-	RIC_AI void load(const GeoM& g, int c) { freq = g.freq[c]; idx = g.idx[c]; params(); }
+	uint32_t freq, idx;
+	RIC_AI void load(const GeoM& g, int c) { freq = g.freq[c]; idx = g.idx[c]; }
 	RIC_AI void store(GeoM& g, int c) const { g.freq[c] = (uint16_t)freq; g.idx[c] = (uint8_t)idx; }
 	template <uint32_t LMAX>
 	RIC_AI int decode_signed(DecCore& d)                         // GeoM::decode_signed
 	{
-		const uint32_t f = freq, sh = 3 + s;
+		const uint32_t k = kGeoK[idx], f = freq;
+		const int s = kGeoShift[idx];
 		uint32_t fr = freq, l = 0;
-		// The unary run's first two bins decoded without a branch on their
-		// values (every bin of the run has the same probability f): only a run
-		// of two or more, or a normalisation due before the second bin, takes
-		// the loop.
-		if (__builtin_expect(d.range <= 4096u, 0)) d.norm();
-		const uint32_t t0 = (d.range * f) >> 12;
-		const uint32_t m0 = (uint32_t)(d.low < t0) - 1u;             // ~0: the bin is 1
-		const uint32_t low1 = d.low - (t0 & m0);
-		const uint32_t range1 = t0 + ((d.range - 2 * t0) & m0);
-		const uint32_t t1 = (range1 * f) >> 12;
-		const uint32_t m1 = (uint32_t)(low1 < t1) - 1u;
-		if (__builtin_expect((m0 & (m1 | ((uint32_t)(range1 <= 4096u) * ~0u))) != 0, 0)) {
-			d.low = low1;
-			d.range = range1;
-			fr -= fr >> sh;
-			l = 1;
-			while (d.get_bit(f)) {
-				fr -= fr >> sh;
-				if (++l > LMAX) break;                  // corrupt-stream guard
-			}
-		} else {
-			d.range = (range1 & ~m0) | (t1 & m0);
-			d.low = low1;
-			fr -= (fr >> sh) & m0;
-			l = m0 & 1u;
+		while (d.get_bit(f)) {
+			fr -= fr >> (3 + s);
+			if (++l > LMAX) break;                  // corrupt-stream guard
 		}
 		const uint32_t v = d.bits(k + 1);
 		const uint32_t sym = (l << k) | (v >> 1);
-		fr = (uint16_t)(fr + ((4096 - fr) >> sh));                  // adapt
-		if (__builtin_expect((uint16_t)(fr - th0) > span, 0)) {
-			if (fr < th0) { if (idx < 24) idx++; }
+		fr = (uint16_t)(fr + ((4096 - fr) >> (3 + s)));             // adapt
+		if ((uint16_t)(fr - kGeoThres[s - 1]) > kGeoThres[s] - kGeoThres[s - 1]) {
+			if (fr < kGeoThres[s - 1]) { if (idx < 24) idx++; }
 			else if (idx > 0) idx--;
 			if (idx >= 9) fr = 2048;
-			params();
 		}
 		freq = fr;
 		const int mag = (int)sym + 1;

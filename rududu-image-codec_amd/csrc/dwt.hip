@@ -865,6 +865,27 @@ __device__ __forceinline__ PRow8 prow8_from(const uint4& u)
 	r.q[3] = as_v2(__builtin_amdgcn_perm(u.w, u.z, 0x07060302u));
 	return r;
 }
+// The same row from 8 u8 pixels (a gray frame's level 0, k_fwdq_pc_z<.., U8>):
+// the ric level shift of k_gray_in8 applied on the way, (p - 128) << sh
+// (src/ric/ric.cpp:144-148: sh 4 lossy, 0 lossless), so the coding plane is
+// never written or read.  u.x = pixels c3 c2 c1 c0 (c0 the low byte).
+__device__ __forceinline__ PRow8 prow8_from_u8(const uint2& u, int sh)
+{
+	PRow8 r;
+	const v2s b = {128, 128}, s = {(short)sh, (short)sh};
+	r.q[0] = (as_v2(__builtin_amdgcn_perm(0u, u.x, 0x0c020c00u)) - b) << s;
+	r.q[2] = (as_v2(__builtin_amdgcn_perm(0u, u.x, 0x0c030c01u)) - b) << s;
+	r.q[1] = (as_v2(__builtin_amdgcn_perm(0u, u.y, 0x0c020c00u)) - b) << s;
+	r.q[3] = (as_v2(__builtin_amdgcn_perm(0u, u.y, 0x0c030c01u)) - b) << s;
+	return r;
+}
+// a gray batch's u8 pixels for level 0 (kernel argument: one pointer per frame)
+constexpr int kPixZ = 32;
+struct PixSrc {
+	const uint8_t* p[kPixZ];
+	long sp;                           // bytes per row
+	int sh;                            // the level shift
+};
 // the odd left neighbours of the evens: (lm, c1), (c3, c5)
 __device__ __forceinline__ void left_odd8(const PRow8& r, v2s& l0, v2s& l1)
 {
@@ -1099,11 +1120,14 @@ struct NoStage {
 
 // stage(): called once the prologue row loads are in flight (k_fwdq_pc
 // stages the format tables there, so their latency overlaps the loads')
-template <bool EDGE, bool PC = false, bool X = true, typename Stage = NoStage>
+// U8: the input rows are u8 pixels at src8 (sp8 bytes per row), level-shifted
+// on load (prow8_from_u8)
+template <bool EDGE, bool PC = false, bool X = true, typename Stage = NoStage, bool U8 = false>
 __device__ __forceinline__ void fq_seg(const FqArgs& a, const int (*thr)[16], const uint32_t (*tpk)[17 * 8],
                                        const FqTables& F, int x, int lane, int y0, int kx, const FqBorder& m, int S,
                                        uint2 (*pcbuf)[3][4][kLanes] = nullptr, int dbg = 0, uint64_t* tr = nullptr,
-                                       const Stage& stage = Stage(), int* hring = nullptr)
+                                       const Stage& stage = Stage(), int* hring = nullptr,
+                                       const uint8_t* src8 = nullptr, long sp8 = 0, int sh8 = 0)
 {
 	const bool out_lane = lane >= 1 && lane <= kLanes - 2 && (!EDGE || x < a.W);
 	int16_t* pL = a.d[BL] + (long)(y0 >> 1) * a.p[BL] + (x >> 1);
@@ -1118,7 +1142,8 @@ __device__ __forceinline__ void fq_seg(const FqArgs& a, const int (*thr)[16], co
 	// prefetch depth in loop iterations (8 rows each): the producer of the
 	// PC form has the registers for two
 	constexpr int DEPTH = PC ? 2 : 1;
-	uint4 ring[DEPTH][2 * PF];
+	using RowRaw = typename std::conditional<U8, uint2, uint4>::type;
+	RowRaw ring[DEPTH][2 * PF];
 	int yl = y0 - 4;
 	// Every row load is unconditional, from a wave-uniform clamped row (the
 	// refills past the segment re-read its last row, an L2 hit): a load under
@@ -1128,9 +1153,10 @@ __device__ __forceinline__ void fq_seg(const FqArgs& a, const int (*thr)[16], co
 	// image when the row is consumed.
 	const int ylast = min(y0 + S + 3, a.H - 1);
 	const int xcl = EDGE ? min(max(x, 0), a.W - 8) : x;
-	auto load_next = [&](uint4& dst) {
+	auto load_next = [&](RowRaw& dst) {
 		const int yc = min(max(yl, 0), ylast);
-		dst = *reinterpret_cast<const uint4*>(a.src + (long)yc * a.sp + xcl);
+		if constexpr (U8) dst = *reinterpret_cast<const uint2*>(src8 + (long)yc * sp8 + xcl);
+		else dst = *reinterpret_cast<const uint4*>(a.src + (long)yc * a.sp + xcl);
 		yl++;
 	};
 #pragma unroll
@@ -1169,7 +1195,7 @@ __device__ __forceinline__ void fq_seg(const FqArgs& a, const int (*thr)[16], co
 		fq_block_regs(a, thr[BV], tpk[BV], F, BV, bV, kx, ky, out_lane);
 		__builtin_amdgcn_sched_barrier(0);
 	};
-	auto iteration = [&](int it, uint4 (&rg)[2 * PF]) {
+	auto iteration = [&](int it, RowRaw (&rg)[2 * PF]) {
 		const bool last = it + 1 == nit;
 		if (PC && hring) {
 			// block row it - 1 goes to slot (it - 1) % kRing, free once every
@@ -1188,10 +1214,19 @@ __device__ __forceinline__ void fq_seg(const FqArgs& a, const int (*thr)[16], co
 		for (int k = 0; k < PF; k++) {
 			if (EDGE && last && k >= kend) break;
 			const int e = y0 - 4 + 2 * (it * PF + k);   // the pair's even row
-			uint4 u0 = rg[2 * k], u1 = rg[2 * k + 1];
-			if (EDGE && !m.ld) { u0 = make_uint4(0, 0, 0, 0); u1 = u0; }
-			w4 = prow8_from(u0);
-			w5 = prow8_from(u1);
+			if constexpr (U8) {
+				w4 = prow8_from_u8(rg[2 * k], sh8);
+				w5 = prow8_from_u8(rg[2 * k + 1], sh8);
+				if (EDGE && !m.ld) {
+#pragma unroll
+					for (int q = 0; q < 4; q++) { w4.q[q] = z; w5.q[q] = z; }
+				}
+			} else {
+				uint4 u0 = rg[2 * k], u1 = rg[2 * k + 1];
+				if (EDGE && !m.ld) { u0 = make_uint4(0, 0, 0, 0); u1 = u0; }
+				w4 = prow8_from(u0);
+				w5 = prow8_from(u1);
+			}
 			load_next(rg[2 * k]);
 			load_next(rg[2 * k + 1]);
 			if (EDGE && e < 0) continue;                 // above the image (top segment)
@@ -1399,8 +1434,9 @@ constexpr int kWgTraceMax = 8192;
 // producers on distinct SIMDs by HW_ID made no measurable difference, and a
 // role known before the first barrier lets the producer issue its prologue
 // row loads before the workgroup stages the format tables.
-template <bool ASYNC, bool X = true>
-__device__ __forceinline__ void fwdq_pc_body(const FqArgs& a, int S, int dbg)
+template <bool ASYNC, bool X = true, bool U8 = false>
+__device__ __forceinline__ void fwdq_pc_body(const FqArgs& a, int S, int dbg, const uint8_t* src8 = nullptr, long sp8 = 0,
+                                             int sh8 = 0)
 {
 	__shared__ int s_thres[3][16];
 	__shared__ FqTables s_F __attribute__((aligned(16)));
@@ -1450,11 +1486,11 @@ __device__ __forceinline__ void fwdq_pc_body(const FqArgs& a, int S, int dbg)
 			m.eL0 = x == 0 ? 0x0000FFFFu : 0u;
 			m.oR3 = x + 7 == a.W - 1 ? 0xFFFF0000u : 0u;
 			m.ld = x >= 0 && x < a.W;
-			fq_seg<true, true, X>(a, s_thres, s_tpk, s_F, x, lane, y0, kx, m, S, s_buf, dbg, wgt ? wgt + 8 : nullptr, stage,
-			                   ASYNC ? s_ring : nullptr);
+			fq_seg<true, true, X, decltype(stage), U8>(a, s_thres, s_tpk, s_F, x, lane, y0, kx, m, S, s_buf, dbg,
+			                                           wgt ? wgt + 8 : nullptr, stage, ASYNC ? s_ring : nullptr, src8, sp8, sh8);
 		} else {
-			fq_seg<false, true, X>(a, s_thres, s_tpk, s_F, x, lane, y0, kx, m, S, s_buf, dbg, wgt ? wgt + 8 : nullptr, stage,
-			                    ASYNC ? s_ring : nullptr);
+			fq_seg<false, true, X, decltype(stage), U8>(a, s_thres, s_tpk, s_F, x, lane, y0, kx, m, S, s_buf, dbg,
+			                                            wgt ? wgt + 8 : nullptr, stage, ASYNC ? s_ring : nullptr, src8, sp8, sh8);
 		}
 	} else {
 		const int b = wave - 1;
@@ -1494,6 +1530,12 @@ template <bool ASYNC, bool X>
 __global__ void __launch_bounds__(256, 4) k_fwdq_pc_z(const FqArgs* __restrict__ az, int S, int dbg)
 {
 	fwdq_pc_body<ASYNC, X>(az[blockIdx.z], S, dbg);
+}
+// the same over a gray batch's u8 pixels (the level shift fused, no coding plane)
+template <bool ASYNC>
+__global__ void __launch_bounds__(256, 4) k_fwdq_pc_z8(const FqArgs* __restrict__ az, int S, int dbg, PixSrc px)
+{
+	fwdq_pc_body<ASYNC, false, true>(az[blockIdx.z], S, dbg, px.p[blockIdx.z], px.sp, px.sh);
 }
 
 // ------------------------------------ two-producer fused level (k_fwdq_pc2)
@@ -2707,7 +2749,16 @@ int launch_fwdq_level_z(const Pyramid& P, int l, const ZFrames& fr, int vec8, in
 	// RIC_FQZ_ASYNC=0/1 overrides)
 	static const int async_env = [] { const char* e = getenv("RIC_FQZ_ASYNC"); return e ? atoi(e) : -1; }();
 	const int async = async_env >= 0 ? async_env : fr.ring;
-	if (l <= pc1 && l == 0 && in8 && !async) hipLaunchKernelGGL((k_fwdq_pc_z<false, false>), grid, dim3(256), 0, st, d, S, 0);
+	if (l == 0 && in8 && fr.pix8) {
+		if (fr.nz > kPixZ) return -1;
+		PixSrc px;
+		for (int f = 0; f < kPixZ; f++) px.p[f] = f < fr.nz ? fr.pix8[f] : nullptr;
+		px.sp = L.w;
+		px.sh = fr.sh8;
+		if (async) hipLaunchKernelGGL(k_fwdq_pc_z8<true>, grid, dim3(256), 0, st, d, S, 0, px);
+		else hipLaunchKernelGGL(k_fwdq_pc_z8<false>, grid, dim3(256), 0, st, d, S, 0, px);
+	}
+	else if (l <= pc1 && l == 0 && in8 && !async) hipLaunchKernelGGL((k_fwdq_pc_z<false, false>), grid, dim3(256), 0, st, d, S, 0);
 	else if (l <= pc1 && l == 0 && in8) hipLaunchKernelGGL((k_fwdq_pc_z<true, false>), grid, dim3(256), 0, st, d, S, 0);
 	else if (l <= pc1) hipLaunchKernelGGL((k_fwdq_pc_z<true, true>), grid, dim3(256), 0, st, d, S, 0);
 	else hipLaunchKernelGGL(k_fwdq_pc2_z<true>, grid, dim3(320), 0, st, d, S, 0);

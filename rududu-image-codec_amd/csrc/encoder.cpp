@@ -206,27 +206,35 @@ struct GeoE {                                             // CGeomCodec::code
 // One CGeomCodec context in registers for the run of a block's magnitudes
 // (they share one context): no model reload after every band access.
 struct GeoRegE {
-	uint32_t freq, idx;
-	RIC_AI void load(const GeoE& g, int c) { freq = g.freq[c]; idx = g.idx[c]; }
+	// the context's idx-dependent parameters kept ready (k, the adaptation
+	// shift, its two thresholds), reloaded only when idx moves
+	uint32_t freq, idx, k, sh, th0, span;
+	RIC_AI void params()
+	{
+		const int s = kGeoShift[idx];
+		k = kGeoK[idx]; sh = 3 + s;
+		th0 = kGeoThres[s - 1]; span = (uint32_t)(kGeoThres[s] - kGeoThres[s - 1]);
+	}
+	RIC_AI void load(const GeoE& g, int c) { freq = g.freq[c]; idx = g.idx[c]; params(); }
 	RIC_AI void store(GeoE& g, int c) const { g.freq[c] = (uint16_t)freq; g.idx[c] = (uint8_t)idx; }
 	template <typename Core>
 	RIC_AI void code_signed(Core& e, uint32_t sym, uint32_t sign)   // GeoE::code_signed
 	{
-		const uint32_t k = kGeoK[idx], f = freq;
-		const int s = kGeoShift[idx];
+		const uint32_t f = freq;
 		uint32_t fr = freq;
 		for (uint32_t l = sym >> k; l > 0; l--) {
 			e.bin(f, 1);
-			fr -= fr >> (3 + s);
+			fr -= fr >> sh;
 		}
 		e.bin(f, 0);
 		RIC_STAT(1, 1); RIC_STAT(2, k);
 		e.bits(((sym & ((1u << k) - 1)) << 1) | sign, k + 1);
-		fr = (uint16_t)(fr + ((4096 - fr) >> (3 + s)));
-		if ((uint16_t)(fr - kGeoThres[s - 1]) > kGeoThres[s] - kGeoThres[s - 1]) {
-			if (fr < kGeoThres[s - 1]) { if (idx < 24) idx++; }
+		fr = (uint16_t)(fr + ((4096 - fr) >> sh));
+		if (__builtin_expect((uint16_t)(fr - th0) > span, 0)) {
+			if (fr < th0) { if (idx < 24) idx++; }
 			else if (idx > 0) idx--;
 			if (idx >= 9) fr = 2048;
+			params();
 		}
 		freq = fr;
 	}

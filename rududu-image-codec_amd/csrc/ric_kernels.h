@@ -78,6 +78,11 @@ struct ZFrames {
 	// workgroups fit beside the stream coder's waves, and no scratch spills --
 	// the ring form's consumers spill 28 bytes per lane at 128 VGPRs)
 	int ring = 0;
+	// level 0 of a gray batch straight from its u8 pixels (k_fwdq_pc_z8, the
+	// ric level shift fused): one device pointer per frame (W bytes per row,
+	// 8-byte aligned), sh8 the shift; null: from src (the coding planes)
+	const uint8_t* const* pix8 = nullptr;
+	int sh8 = 0;
 	// Split arenas (the GPU stream coder's pool): regions A and B (bands,
 	// status word, records, parent info: offsets below `split` = Pyramid::b_end)
 	// of frame f at arena + f * astride, region C (intermediate LL planes, pRD)
