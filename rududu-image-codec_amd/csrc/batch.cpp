@@ -158,9 +158,22 @@ struct BProf {
 }  // namespace
 
 struct ric_batch {
-	// level 0's hand-off form (ZFrames::ring): the double buffer (0) everywhere
-	// (RIC_FQZ_ASYNC=1: the ring form)
-	int fq_ring = 0;
+	// The level kernels' forms (ZFrames::ring, ::pc1): beside the stream
+	// coder's waves level 0 takes the double-buffered hand-off (20 KiB of LDS,
+	// two workgroups per CU fit beside them) and level 1 the two-producer
+	// kernel; alone on the chip (the step's front, before the coder launch;
+	// the diagnostics) the LDS ring hand-off and the one-producer level 1 are
+	// faster (C3, 16 frames: level 0 61.6 against 67.3 us per frame, level 1
+	// 20.4 against 23.2).  RIC_FQZ_ALONE=0: the beside forms everywhere.
+	// Every call but the serving step (ric_batch_roundtrip_hybrid) runs its
+	// level kernels alone.
+	int fq_ring = 1, fq_pc1 = 1;
+	void alone(bool on)
+	{
+		static const bool en = [] { const char* e = getenv("RIC_FQZ_ALONE"); return !e || atoi(e) != 0; }();
+		fq_ring = fq_pc1 = on && en ? 1 : 0;
+	}
+	ric_batch() { alone(true); }
 	// The host encoder's payload compacted on the GPU (compact.hip): the
 	// 16-bit bands' values in walk order instead of the dense bands.  Per
 	// slot: the stream (d_cmp), chunk counts / offsets, its value count (also
@@ -200,9 +213,27 @@ struct ric_batch {
 	int16_t* d_planes = nullptr;
 	uint8_t* d_stage = nullptr;                    // host pixels in / out, w*h*channels per slot
 	hipStream_t st = nullptr;
+	// non-blocking streams for the device -> host copies made while a coder
+	// launch runs (the stream copier, host-decoded streams): never the null
+	// stream, which waits for every blocking stream of the process
+	hipStream_t cst[4] = {nullptr, nullptr, nullptr, nullptr};
 	ZArgs zf[2][kMaxLevels], zi[2][kMaxLevels];    // per set: forward / inverse argument arrays
 	std::vector<Mux> enc, dec;                     // per slot
 	Pool* pool = nullptr;
+	// The band-parallel encoder (encode_bands_split, encoder.cpp) for calls
+	// with fewer frames in flight than half the host threads (C4's tiles, C5
+	// frames over many ranks): a frame's bands are modelled on bpool's threads
+	// while its own task writes the stream.  evb: per slot, the bands' event lists.
+	Pool* bpool = nullptr;
+	bool split = false;
+	std::vector<std::vector<EvBuf>> evb;
+	void set_split(int frames_in_flight)
+	{
+		static const bool en = [] { const char* e = getenv("RIC_BATCH_SPLIT"); return !e || atoi(e) != 0; }();
+		split = en && pool && frames_in_flight * 2 <= pool->size();
+		if (split && !bpool) bpool = new Pool(pool->size());
+		if (split && evb.size() < (size_t)nslot()) evb.resize(nslot());
+	}
 	BProf prof;
 	// GPU stream coder (gcoder.hip): argument block, per-slot results
 	GEncArgs genc{};
@@ -377,6 +408,7 @@ int gpu_encode_plane(ric_batch* b, int set, int n, int p, const uint8_t* const* 
 		ZFrames fr;
 		fr.arena = b->arena(abase); fr.astride = ast; fr.nz = n;
 		fr.ring = b->fq_ring;
+		fr.pc1 = b->fq_pc1;
 		if (direct) {
 			fr.arena = pool; fr.astride = pstr;
 			fr.scratch = b->arena(abase); fr.scstride = ast; fr.split = P.b_end; fr.lo = lo;
@@ -634,15 +666,40 @@ int host_encode_plane(ric_batch* b, int s, int p, int q, int trans, uint8_t* out
 		cp = (const int16_t*)b->harena(s);
 	}
 	const double t0 = now_ms();
-	pred_encode(m, b->view(s, P.coarsest_ll()));
-	for (int l = P.nlev - 1; l >= 0; l--) {
-		const int order[3] = {BV, BH, BD};
-		for (int k = 0; k < 3; k++) {
-			const Band& B = P.L[l].b[order[k]];
-			const uint64_t* rec = (const uint64_t*)(b->harena(s) + P.rec_off[l][order[k]]);
-			const uint8_t* pin = l + 1 < P.nlev ? (const uint8_t*)(b->harena(s) + P.pin_off[l][order[k]]) : nullptr;
-			if (cp && !B.is_int) tree_encode_records_compact(m, rec, pin, b->view(s, B), l == 0, &cp);
-			else tree_encode_records_fast(m, rec, pin, b->view(s, B), l == 0);
+	if (b->split && b->bpool) {
+		// the bands modelled in parallel (a compacted band's values start where
+		// the walk's previous compacted bands' end), the stream written here
+		BandRecs bands[3 * kMaxLevels];
+		int nb = 0;
+		const int16_t* c0 = cp;
+		for (int l = P.nlev - 1; l >= 0; l--) {
+			const int order[3] = {BV, BH, BD};
+			for (int k = 0; k < 3; k++) {
+				const Band& B = P.L[l].b[order[k]];
+				BandRecs& r = bands[nb++];
+				r.rec = (const uint64_t*)(b->harena(s) + P.rec_off[l][order[k]]);
+				r.pin = l + 1 < P.nlev ? (const uint8_t*)(b->harena(s) + P.pin_off[l][order[k]]) : nullptr;
+				r.v = b->view(s, B);
+				r.high = l == 0;
+				r.cvals = nullptr;
+				if (c0 && !B.is_int) {
+					r.cvals = c0;
+					c0 += band_value_count(r.rec, r.v);
+				}
+			}
+		}
+		encode_bands_split(m, *b->bpool, b->evb[ms < 0 ? s : ms], b->view(s, P.coarsest_ll()), bands, nb);
+	} else {
+		pred_encode(m, b->view(s, P.coarsest_ll()));
+		for (int l = P.nlev - 1; l >= 0; l--) {
+			const int order[3] = {BV, BH, BD};
+			for (int k = 0; k < 3; k++) {
+				const Band& B = P.L[l].b[order[k]];
+				const uint64_t* rec = (const uint64_t*)(b->harena(s) + P.rec_off[l][order[k]]);
+				const uint8_t* pin = l + 1 < P.nlev ? (const uint8_t*)(b->harena(s) + P.pin_off[l][order[k]]) : nullptr;
+				if (cp && !B.is_int) tree_encode_records_compact(m, rec, pin, b->view(s, B), l == 0, &cp);
+				else tree_encode_records_fast(m, rec, pin, b->view(s, B), l == 0);
+			}
 		}
 	}
 	if (p + 1 == b->channels) {
@@ -729,6 +786,15 @@ bool outputs_distinct(uint8_t* const* out, int n)
 	return std::adjacent_find(v.begin(), v.end()) == v.end();
 }
 
+// a device -> host copy on one of the batch's copy streams (lane: any
+// integer), waited for on that stream alone
+hipError_t d2h(ric_batch* b, long lane, void* dst, const void* src, size_t n)
+{
+	hipStream_t st = b->cst[lane & 3];
+	const hipError_t e = hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, st);
+	return e != hipSuccess ? e : hipStreamSynchronize(st);
+}
+
 // frame f's .ric file is complete in its host buffer (ric_batch_set_ready)
 void mark_ready(ric_batch* b, long f, size_t len)
 {
@@ -792,6 +858,10 @@ int ric_batch_create(ric_batch** out, int w, int h, int channels, int slots, int
 	    bfail(hipMalloc(&b->d_planes, ns * b->pstride), "hipMalloc batch planes") ||
 	    bfail(hipMalloc(&b->d_stage, ns * (size_t)w * h * channels), "hipMalloc batch staging") ||
 	    bfail(hipStreamCreateWithFlags(&b->st, hipStreamNonBlocking), "hipStreamCreate") ||
+	    bfail(hipStreamCreateWithFlags(&b->cst[0], hipStreamNonBlocking), "hipStreamCreate") ||
+	    bfail(hipStreamCreateWithFlags(&b->cst[1], hipStreamNonBlocking), "hipStreamCreate") ||
+	    bfail(hipStreamCreateWithFlags(&b->cst[2], hipStreamNonBlocking), "hipStreamCreate") ||
+	    bfail(hipStreamCreateWithFlags(&b->cst[3], hipStreamNonBlocking), "hipStreamCreate") ||
 	    bfail(hipMemsetAsync(b->d_arena, 0, ns * b->astride, b->st), "hipMemset batch arena") ||
 	    bfail(hipStreamSynchronize(b->st), "hipStreamSynchronize")) {
 		ric_batch_destroy(b);
@@ -850,6 +920,7 @@ void ric_batch_destroy(ric_batch* b)
 {
 	if (!b) return;
 	delete b->pool;
+	delete b->bpool;
 	(void)hipSetDevice(b->device);
 	if (b->st) (void)hipStreamSynchronize(b->st);
 	for (int s = 0; s < 2; s++)
@@ -891,6 +962,8 @@ void ric_batch_destroy(ric_batch* b)
 		}
 	}
 	if (b->st) (void)hipStreamDestroy(b->st);
+	for (hipStream_t& x : b->cst)
+		if (x) (void)hipStreamDestroy(x);
 	delete b;
 }
 
@@ -901,6 +974,8 @@ int ric_batch_encode(ric_batch* b, const uint8_t* const* pix, int n, int pix_on_
 		return RIC_E_ARG;
 	if (n == 0) return RIC_OK;
 	if (set_dev(b->device)) return RIC_E_HIP;
+	b->set_split(n);
+	struct SplitGuard { ric_batch* b; ~SplitGuard() { b->split = false; } } split_guard{b};
 	std::vector<const uint8_t*> dpix;
 	int rc = stage_pixels(b, 0, n, pix, pix_on_device, dpix);
 	if (rc) return rc;
@@ -973,6 +1048,8 @@ int ric_batch_roundtrip(ric_batch* b, const uint8_t* const* pix, int n, int q, i
 	if (set_dev(b->device)) return RIC_E_HIP;
 	const int S = b->slots;
 	const int G = (n + S - 1) / S;
+	b->set_split(std::min(n, 2 * S));                    // (two groups in flight)
+	struct SplitGuard { ric_batch* b; ~SplitGuard() { b->split = false; } } split_guard{b};
 	if (b->channels != 1) {
 		// colour: plane-sequential groups (each plane's host coding needs the
 		// previous plane's bands out of the mirror first)
@@ -1389,6 +1466,14 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 	if (!outputs_distinct(out, n))
 		return set_last_error("ric_batch_roundtrip_hybrid: out[] buffers must be distinct"), RIC_E_ARG;
 	if (set_dev(b->device)) return RIC_E_HIP;
+	// the level kernels run beside the stream coder's waves (the step's front,
+	// before the coder launch, switches to the alone forms)
+	struct FormGuard {
+		ric_batch* b;
+		~FormGuard() { b->alone(true); }
+	} form_guard{b};
+	b->alone(false);
+	b->split = false;                                      // every host thread codes frames of its own here
 	auto& c = b->cp;
 	Pyramid& P = b->P;
 	const int S = b->slots;
@@ -1532,8 +1617,7 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 				if ((st_k & 0xFFu) == 4) continue;                    // left to the host (harvest)
 				const uint32_t len_k = __atomic_load_n(po + 2 * k, __ATOMIC_RELAXED);
 				if ((st_k & 0xFFu) || len_k > cap[f0 + k]) break;   // harvest reports it
-				if (bfail(hipMemcpy(out[f0 + k], c.d_out + ((size_t)h * c.n + k) * c.ocap, len_k, hipMemcpyDeviceToHost),
-				          "hipMemcpy stream"))
+				if (bfail(d2h(b, j, out[f0 + k], c.d_out + ((size_t)h * c.n + k) * c.ocap, len_k), "hipMemcpy stream"))
 					r = RIC_E_HIP;
 				else
 					mark_ready(b, f0 + k, len_k);
@@ -1730,9 +1814,8 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 			// per kernel: waves' end times from the kernel's first start, ms (p0 p10 p50 p90 p100),
 			// the mean wave duration, and the waves per SIMD they ran beside (this launch's own)
 			std::vector<uint64_t> t(8 * (size_t)m);
-			BCHK(hipMemcpy(t.data(), c.d_ts + (size_t)h * 4 * c.n, sizeof(uint64_t) * 4 * m, hipMemcpyDeviceToHost));
-			BCHK(hipMemcpy(t.data() + 4 * m, c.d_ts + (size_t)8 * c.n + (size_t)h * 4 * c.n, sizeof(uint64_t) * 4 * m,
-			               hipMemcpyDeviceToHost));
+			BCHK(d2h(b, j, t.data(), c.d_ts + (size_t)h * 4 * c.n, sizeof(uint64_t) * 4 * m));
+			BCHK(d2h(b, j, t.data() + 4 * m, c.d_ts + (size_t)8 * c.n + (size_t)h * 4 * c.n, sizeof(uint64_t) * 4 * m));
 			static std::mutex ts_mu;
 			std::lock_guard<std::mutex> g(ts_mu);
 			// RIC_GC_TSTAMP_FILE: every wave as a line (call, batch, kernel, frame, start, end, HW_ID, XCC_ID)
@@ -1899,8 +1982,7 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 				std::atomic<long>* pdec_n = &dec_n;
 				b->pool->submit([=] {
 					int r1 = set_dev(b->device);
-					if (!r1) r1 = bfail(hipMemcpy(out[f], src, len[f], hipMemcpyDeviceToHost), "hipMemcpy stream") ? RIC_E_HIP
-					                                                                                            : RIC_OK;
+					if (!r1) r1 = bfail(d2h(b, (int)f, out[f], src, len[f]), "hipMemcpy stream") ? RIC_E_HIP : RIC_OK;
 					if (!r1) mark_ready(b, f, len[f]);
 					cl->done();
 					// the set's mirrors: the previous group's H2D from them has passed
@@ -1982,7 +2064,8 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 		if (fwd_ahead && kicked == 0 && nbatch >= 2) {
 			// the step's start: the first host groups' and both coder batches'
 			// forward levels, then both coder launches (level 0 runs alone on
-			// the CUs, not beside the coder waves)
+			// the CUs, not beside the coder waves: the alone forms)
+			b->alone(true);
 			while (rc == RIC_OK && fl.size() < 2 && !ready_host.empty()) {
 				const HGroup g = ready_host.front();
 				ready_host.pop_front();
@@ -1990,6 +2073,7 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 			}
 			if (rc == RIC_OK) rc = kick_fwd(0);
 			if (rc == RIC_OK) rc = kick_fwd(1);
+			b->alone(false);                       // the coder's waves from here on
 			if (rc == RIC_OK && merge && gpu_decode == 1) {
 				rc = kick_both();
 				running[0] = running[1] = rc == RIC_OK;

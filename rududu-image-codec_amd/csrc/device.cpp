@@ -16,6 +16,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -74,10 +75,25 @@ struct Aux {
 constexpr int kMaxDev = 64;
 Aux g_aux[kMaxDev];
 
+// The side and communicator streams, at the device's greatest stream
+// priority (RIC_SIDE_PRIO=0: the default priority): the runtime gives each a
+// hardware queue of its own instead of one of the GPU_MAX_HW_QUEUES shared
+// round robin by the process's other streams, where a packet queued behind
+// the stream coder's launch would wait for it (a digest kernel queued there
+// waited ~0.5 s for a 0.9 s launch; profiles/r05_gather_ops_during_launch.log)
+hipError_t side_stream_create(hipStream_t* st)
+{
+	static const int prio = [] { const char* e = getenv("RIC_SIDE_PRIO"); return e ? atoi(e) : 1; }();
+	int least = 0, greatest = 0;
+	if (prio && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
+		return hipStreamCreateWithPriority(st, hipStreamNonBlocking, greatest);
+	return hipStreamCreateWithFlags(st, hipStreamNonBlocking);
+}
+
 // (device already current)
 int aux_ready(Aux& a)
 {
-	if (!a.st) DCHK(hipStreamCreateWithFlags(&a.st, hipStreamNonBlocking));
+	if (!a.st) DCHK(side_stream_create(&a.st));
 	if (!a.d_dig) DCHK(hipMalloc(&a.d_dig, sizeof(unsigned long long) * kDigestRuns));
 	if (!a.h_dig) DCHK(hipHostMalloc(&a.h_dig, sizeof(unsigned long long) * kDigestRuns, 0));
 	return RIC_OK;
@@ -278,7 +294,7 @@ int ric_comm_create(ric_comm** out, const uint8_t* id, int nranks, int rank, int
 	c->device = device; c->nranks = nranks; c->rank = rank;
 	ncclUniqueId u;
 	memcpy(u.internal, id, NCCL_UNIQUE_ID_BYTES);
-	if (dfail(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking), "hipStreamCreate") ||
+	if (dfail(side_stream_create(&c->st), "hipStreamCreate") ||
 	    nfail(ncclCommInitRank(&c->comm, nranks, u, rank), "ncclCommInitRank")) {
 		ric_comm_destroy(c);
 		return RIC_E_HIP;

@@ -1825,10 +1825,10 @@ void fq_launch_pc(FqArgs& a, hipStream_t st)
 		if (async2) hipLaunchKernelGGL(k_fwdq_pc2<true>, grid2, dim3(320), 0, st, a, S, dbg2 & ~128);
 		else hipLaunchKernelGGL(k_fwdq_pc2<false>, grid2, dim3(320), 0, st, a, S, dbg2);
 	} else {
-		// the double-buffered hand-off by default: the ring form's consumer
-		// state spills to scratch under the 128-VGPR bound of four waves per
-		// SIMD (28 bytes per lane; measured round 5: 58 against 71 us per 8K frame)
-		static const int async = [] { const char* e = getenv("RIC_FQ_ASYNC"); return e ? atoi(e) : 0; }();
+		// the ring hand-off (the single-frame calls run alone on the chip:
+		// measured round 5 at C3, 63.0 against 65.0 us per frame for the
+		// double buffer, despite the ring form's 20-28 bytes of scratch per lane)
+		static const int async = [] { const char* e = getenv("RIC_FQ_ASYNC"); return e ? atoi(e) : 1; }();
 		const dim3 grid = onewg ? dim3(1, 1) : dim3(nstrip, a.nseg);
 		if (onewg) dbg |= 4;
 		if (async && a.in8) hipLaunchKernelGGL((k_fwdq_pc<true, false>), grid, dim3(256), 0, st, a, S, dbg & ~128);
@@ -2744,7 +2744,8 @@ int launch_fwdq_level_z(const Pyramid& P, int l, const ZFrames& fr, int vec8, in
 	const dim3 grid((L.w + kFqStrip - 1) / kFqStrip, v[0].nseg, fr.nz);
 	// the one-producer form on level 0 (VALU-bound), two producers above (see
 	// fq_launch_pc); knob RIC_FQZ_PC1 = the last level on one producer
-	static const int pc1 = [] { const char* e = getenv("RIC_FQZ_PC1"); return e ? atoi(e) : 0; }();
+	static const int pc1_env = [] { const char* e = getenv("RIC_FQZ_PC1"); return e ? atoi(e) : -1; }();
+	const int pc1 = pc1_env >= 0 ? pc1_env : fr.pc1;
 	// the ring or the double-buffered hand-off (ZFrames::ring; knob
 	// RIC_FQZ_ASYNC=0/1 overrides)
 	static const int async_env = [] { const char* e = getenv("RIC_FQZ_ASYNC"); return e ? atoi(e) : -1; }();

@@ -329,6 +329,16 @@ size_t tree_model_disp(EvBuf& ev, const uint64_t* rec, const uint8_t* pin, const
 	return e.finish();
 }
 
+// the same over a compacted band's values
+template <bool HIGH>
+size_t tree_model_cmp(EvBuf& ev, const uint64_t* rec, const uint8_t* pin, const BandView& b, const int16_t* cv)
+{
+	EvCore e(ev);
+	if (pin) tree_rec_core<EvCore, int16_t, HIGH, true, true>(e, rec, pin, b, &cv);
+	else tree_rec_core<EvCore, int16_t, HIGH, false, true>(e, rec, pin, b, &cv);
+	return e.finish();
+}
+
 }  // namespace
 
 void tree_encode_records_fast(Mux& m, const uint64_t* rec, const uint8_t* pin, const BandView& b, bool high)
@@ -355,6 +365,14 @@ size_t tree_model_records(EvBuf& ev, const uint64_t* rec, const uint8_t* pin, co
 {
 	if (b.is_int) return high ? tree_model_disp<int32_t, true>(ev, rec, pin, b) : tree_model_disp<int32_t, false>(ev, rec, pin, b);
 	return high ? tree_model_disp<int16_t, true>(ev, rec, pin, b) : tree_model_disp<int16_t, false>(ev, rec, pin, b);
+}
+
+size_t band_value_count(const uint64_t* rec, const BandView& b)
+{
+	const long n = (long)((b.dx + 3) >> 2) * ((b.dy + 3) >> 2);
+	size_t c = 0;
+	for (long i = 0; i < n; i++) c += (size_t)__builtin_popcount(BlockRec::mask(rec[i]));
+	return c;
 }
 
 void replay_events(Mux& m, const uint64_t* ev, size_t n)
@@ -391,7 +409,12 @@ void encode_bands_split(Mux& m, Pool& pool, std::vector<EvBuf>& bufs, const Band
 	for (int k = 0; k < n; k++) {
 		const int i = big[k];
 		pool.submit([&, i] {
-			cnt[i] = tree_model_records(bufs[i], bands[i].rec, bands[i].pin, bands[i].v, bands[i].high);
+			const BandRecs& B = bands[i];
+			if (B.cvals && !B.v.is_int)
+				cnt[i] = B.high ? tree_model_cmp<true>(bufs[i], B.rec, B.pin, B.v, B.cvals)
+				                : tree_model_cmp<false>(bufs[i], B.rec, B.pin, B.v, B.cvals);
+			else
+				cnt[i] = tree_model_records(bufs[i], B.rec, B.pin, B.v, B.high);
 			done[i].store(1, std::memory_order_release);
 		});
 	}

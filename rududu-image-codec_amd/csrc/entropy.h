@@ -252,7 +252,13 @@ struct BandRecs {
 	const uint8_t* pin;
 	BandView v;
 	bool high;
+	// a compacted payload (compact.hip): this band's values in walk order,
+	// read in place of the dense band; null: the band itself
+	const int16_t* cvals = nullptr;
 };
+// the values a band's walk consumes from a compacted payload: the popcount of
+// every block's record mask (read or skipped)
+size_t band_value_count(const uint64_t* rec, const BandView& b);
 class Pool;
 void encode_bands_split(Mux& m, Pool& pool, std::vector<EvBuf>& bufs, const BandView& ll, const BandRecs* bands, int n);
 

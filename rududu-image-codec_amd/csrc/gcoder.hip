@@ -35,6 +35,28 @@
 #ifndef RIC_GC_ELOW_V
 #define RIC_GC_ELOW_V 0
 #endif
+// RIC_GC_UCOND: the decoder's state stays in VGPRs (the balanced SALU / VALU
+// mix, see GDec::enum16) but its branch conditions are read from lane 0
+// (v_readfirstlane): scalar branches instead of exec-mask ones
+// Measured (one C3 serving step, 3072 streams, k_gc_roundtrip per launch;
+// r5 g5, two runs each): 0 11348 ms, 1 12727, 2 11210-11215 (the default), 3 11582-11590
+#ifndef RIC_GC_UCOND
+#define RIC_GC_UCOND 2
+#endif
+// RIC_GC_NVGPR: the coder kernels' VGPR budget as amdgpu_num_vgpr takes it
+// on gfx950 (half the unified VGPR + AGPR count: 44 = 88 VGPRs; 0 = none).
+// Three coder waves of 96 VGPRs left a SIMD 224 of its 512 and RCCL's kernel
+// (ncclDevKernel_Generic_1) wants 248 per wave: a send / receive issued
+// during a launch waited until the launch's first coder waves retired.  At
+// 88 three coder waves leave exactly 248 (one spilled dword per kernel).
+#ifndef RIC_GC_NVGPR
+#define RIC_GC_NVGPR 44
+#endif
+#if RIC_GC_NVGPR
+#define GC_KATTR __attribute__((amdgpu_waves_per_eu(1, 5), amdgpu_num_vgpr(RIC_GC_NVGPR)))
+#else
+#define GC_KATTR
+#endif
 
 namespace ric {
 
@@ -53,6 +75,56 @@ template <typename T> GC_DI GAS T* gst(T* p) { return (GAS T*)p; }
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 GC_DI uint32_t lane_id() { return __lane_id(); }
+// a branch operand of the decoder, wave-uniform in fact (RIC_GC_UCOND)
+GC_DI uint32_t ru(uint32_t x)
+{
+#if RIC_GC_UCOND
+	return __builtin_amdgcn_readfirstlane(x);
+#else
+	return x;
+#endif
+}
+// RIC_GC_UCOND 2: the raw-bit reader's state pinned to VGPRs (the VALU does
+// the bit reads while the scalar unit runs the range decoder and the models)
+GC_DI uint32_t vv(uint32_t x)
+{
+#if RIC_GC_UCOND >= 2
+	asm volatile("" : "+v"(x));
+#endif
+	return x;
+}
+// RIC_GC_EFIFO: the encoder's raw-bit FIFO word in VGPRs (its shifts on the
+// VALU; the bit count and every branch stay scalar).  Measured (r5 g6, one C3
+// serving step of 3072 streams): 10955 against 11409 ms per launch (-4.0 %)
+#ifndef RIC_GC_EFIFO
+#define RIC_GC_EFIFO 1
+#endif
+GC_DI uint64_t vf(uint64_t x)
+{
+#if RIC_GC_EFIFO
+	asm volatile("" : "+v"(x));
+#endif
+	return x;
+}
+// RIC_GC_UCOND 4: 2 and the decoder's byte window in VGPRs (the raw-bit
+// reader's fills on the VALU; the range decoder reads its bytes back by lane 0)
+GC_DI uint64_t vw(uint64_t x)
+{
+#if RIC_GC_UCOND == 4
+	asm volatile("" : "+v"(x));
+#endif
+	return x;
+}
+// RIC_GC_UCOND 3: the range decoder's state in VGPRs as well (its bin
+// arithmetic on the VALU), the decoded bin read back from lane 0 for the
+// models, which stay on the scalar unit
+GC_DI uint32_t vr(uint32_t x)
+{
+#if RIC_GC_UCOND == 3
+	asm volatile("" : "+v"(x));
+#endif
+	return x;
+}
 // a wave-uniform value kept in a VGPR (the compiler would give it an SGPR)
 GC_DI uint32_t to_vgpr(uint32_t x) { uint32_t r; asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "s"(x)); return r; }
 // lane arrays: element i of a per-wave array held in lane i of a VGPR
@@ -250,7 +322,7 @@ struct GEnc {
 	GC_DI void bits(uint32_t v, uint32_t len)           // bitsCode, 64-bit FIFO (entropy.h)
 	{
 		if (__builtin_expect(ebits + len > 64, 0)) drain();
-		ebuf = (ebuf << len) | v;
+		ebuf = vf((ebuf << len) | v);
 		ebits += len;
 	}
 	GC_DI void init(uint8_t* o, uint32_t c, uint32_t base)   // init_encoder at out + base
@@ -730,7 +802,7 @@ GC_DI void post_result(uint32_t* posted, uint32_t tag, int f, uint32_t rc, uint3
 }
 
 template <uint32_t RING>
-__global__ void __launch_bounds__(64) k_gc_encode(const GEncArgs* __restrict__ ap, uint32_t* posted, uint32_t tag)
+__global__ void __launch_bounds__(64) GC_KATTR k_gc_encode(const GEncArgs* __restrict__ ap, uint32_t* posted, uint32_t tag)
 {
 	const GEncArgs& a = *ap;
 	const int f = blockIdx.x;
@@ -800,18 +872,18 @@ struct GDec {
 	// normalisation bytes + <= 25 raw bits), the tree bit, k, the enum code).
 	GC_DI void wadvance()
 	{
-		win = (win << 32) | nxt;
+		win = vw((win << 32) | nxt);
 		wf += 4;
 		nxt = rd_dword(wf + 8);
 	}
 	// x + 7 in [wf, wf + 8).  The ring holds the virtual stream: the two bytes
 	// in front and everything past the payload are zeroed when staged.
-	GC_DI uint32_t byte(uint32_t x) const { return (uint32_t)(win >> (56 - ((x + 7) - wf) * 8)) & 255u; }
+	GC_DI uint32_t byte(uint32_t x) const { return ru((uint32_t)(win >> (56 - ((x + 7) - wf) * 8)) & 255u); }
 	GC_DI uint32_t next()
 	{
 		const uint32_t b = byte(p);
 		if (p < limit) p++; else ovf |= 1;
-		if (p + 7 >= wf + 4) wadvance();
+		if (ru(p + 7 - wf) >= 4u) wadvance();
 		return b;
 	}
 	GC_DI u32x4 load_kib(uint32_t off) const
@@ -853,7 +925,7 @@ struct GDec {
 	// the read position, so the ring always keeps the bytes just behind it.
 	GC_DI void ensure()
 	{
-		if (__builtin_expect(st_hi < p + 7 + kDMargin, 0)) stage_now();
+		if (__builtin_expect((int)ru(st_hi - (p + 7 + kDMargin)) < 0, 0)) stage_now();
 	}
 	GC_DI void refill()
 	{
@@ -888,23 +960,27 @@ struct GDec {
 		do {
 			if (((code - low + range - 1) ^ (code - low)) >= 0x01000000u) range = (low - code) & 4095u;
 			const uint32_t b = next();
-			low = (low << 8) | b;
-			code = (code << 8) | b;
-			range <<= 8;
+			low = vr((low << 8) | b);
+			code = vr((code << 8) | b);
+			range = vr(range << 8);
 			if (__builtin_expect(++it > 4, 0)) { ovf |= 1; range = 1u << 16; }   // corrupt stream: no spin
-		} while (range <= 4096u);
+		} while (ru(range) <= 4096u);
 	}
 	GC_DI uint32_t bit(uint32_t freq)                    // getBit, muxcodec.h:205-213
 	{
-		if (__builtin_expect(range <= 4096u, 0)) norm();
+		if (__builtin_expect(ru(range) <= 4096u, 0)) norm();
 		const uint32_t t = (range * freq) >> 12;
 		// low < t as arithmetic (a bool-to-int on the scalar unit would take a
 		// round trip through a VGPR)
 		const uint32_t lt = (uint32_t)(((uint64_t)low - (uint64_t)t) >> 63);
 		const uint32_t tst = lt - 1u;
-		low -= t & tst;
-		range = t + ((range - 2 * t) & tst);
+		low = vr(low - (t & tst));
+		range = vr(t + ((range - 2 * t) & tst));
+#if RIC_GC_UCOND == 3
+		return ru(1u - lt);
+#else
 		return 1u - lt;
+#endif
 	}
 	GC_DI void fill(uint32_t len)                        // fillBuffer, muxcodec.cpp:572-579
 	{
@@ -916,16 +992,16 @@ struct GDec {
 		const uint32_t nb = (len - nbits + 7) >> 3;
 		const uint32_t o = p + 7 - wf;
 		const uint32_t v = (uint32_t)((win << (8 * o)) >> (64 - 8 * nb));
-		buffer = (uint32_t)(((uint64_t)buffer << (8 * nb)) | v);
-		nbits += 8 * nb;
+		buffer = vv((uint32_t)(((uint64_t)buffer << (8 * nb)) | v));
+		nbits = vv(nbits + 8 * nb);
 		p += nb;
 		if (__builtin_expect(p > limit, 0)) { p = limit; ovf |= 1; }
-		if (p + 7 >= wf + 4) wadvance();
+		if (ru(p + 7 - wf) >= 4u) wadvance();
 	}
 	GC_DI uint32_t bits(uint32_t len)                    // bitsDecode, muxcodec.h:233-239
 	{
-		if (nbits < len) fill(len);
-		nbits -= len;
+		if ((int)ru(nbits - len) < 0) fill(len);
+		nbits = vv(nbits - len);
 		return (buffer >> nbits) & ((1u << len) - 1);
 	}
 	// huffDecode (muxcodec.h:241-276): lane s tests code s of the table row
@@ -944,7 +1020,7 @@ struct GDec {
 		if (p > limit) { p = limit; ovf |= 1; }
 		if (nbits < len) buffer = byte(p - 1);
 		nbits = (nbits - len) & 7;
-		while (p + 7 >= wf + 4) wadvance();
+		while (ru(p + 7 - wf) >= 4u) wadvance();
 		return sym;
 	}
 	// enum_code's code part (muxcodec.cpp:391-393); cnk lane i = (n-1)*8 + k-1:
@@ -1071,7 +1147,7 @@ struct GBitD {                                          // CBitCodec::decode, bi
 		freq = (freq + (sym << (9 - sh)) - (freq >> (3 + sh))) & 0xFFFFu;
 		sym ^= mps;
 		const uint32_t th = lget(T.bit_thr, sh), t0 = th & 0xFFFFu, t1 = th >> 16;
-		if (__builtin_expect(((freq - t1) & 0xFFFFu) > t0 - t1, 0)) {
+		if (__builtin_expect((int)ru((t0 - t1) - ((freq - t1) & 0xFFFFu)) < 0, 0)) {
 			if (freq > t0) {
 				if (sh == 0) { mps ^= 1; freq = 4096u - freq; sh = 1; }
 				else sh--;
@@ -1099,12 +1175,12 @@ struct GGeoD {                                          // one CGeomCodec contex
 	{
 		const uint32_t f = freq;
 		uint32_t fr = freq, l = 0;
-		if (__builtin_expect(d.bit(f), 0)) {             // most runs are empty: fall through
+		if (__builtin_expect(ru(d.bit(f)), 0)) {         // most runs are empty: fall through
 			do {
 				fr -= fr >> s3;
 				if (++l > lmax) break;
 				d.ensure();
-			} while (d.bit(f));
+			} while (ru(d.bit(f)));
 		}
 		int out;
 		if (SIGNED) {
@@ -1116,7 +1192,7 @@ struct GGeoD {                                          // one CGeomCodec contex
 			out = (int)l;
 		}
 		fr = (fr + ((4096u - fr) >> s3)) & 0xFFFFu;
-		if (__builtin_expect(((fr - t0) & 0xFFFFu) > span, 0)) {
+		if (__builtin_expect((int)ru(span - ((fr - t0) & 0xFFFFu)) < 0, 0)) {
 			if (fr < t0) { if (idx < 24) idx++; }
 			else if (idx > 0) idx--;
 			if (idx >= 9) fr = 2048;
@@ -1285,7 +1361,7 @@ GC_DI void tree_dec(GDec& d, const GTabs& T, const GBandDesc& B, const GBandDesc
 			if ((in >> 5) & 1) {
 				if ((in >> 6) & 1) continue;                   // propagated
 				const uint32_t ctx = in & 31u;
-				if (tree.decode(d, T, ctx)) {
+				if (ru(tree.decode(d, T, ctx))) {
 					g_blk[ob + 0] = mval; g_blk[ob + 2] = mval; g_blk[ob + 8] = mval; g_blk[ob + 10] = mval;
 					continue;
 				}
@@ -1294,7 +1370,7 @@ GC_DI void tree_dec(GDec& d, const GTabs& T, const GBandDesc& B, const GBandDesc
 				const uint32_t hrow = l < hn ? (uint32_t)g_huff[hbase + idx * hn + l] : 0u;
 				const uint32_t k = d.huff(hrow, hn) + (high ? 1u : 0u);
 				if (high || k != 0) {
-					uint32_t sig = k == 16 ? 0xFFFFu : ETAB ? d.enum16(cnk, T, etab, k) : d.enum_n(cnk, binom, k, 16, true);
+					uint32_t sig = ru(k == 16 ? 0xFFFFu : ETAB ? d.enum16(cnk, T, etab, k) : d.enum_n(cnk, binom, k, 16, true));
 					GGeoD g;
 					g.load(geo, k - 1, T);
 					while (sig) {
@@ -1307,7 +1383,7 @@ GC_DI void tree_dec(GDec& d, const GTabs& T, const GBandDesc& B, const GBandDesc
 				const uint32_t kk = high ? k - 1 : k;
 				kmean = lset(kmean, ctx, (km + (kk << 7) - (km >> 3)) & 0xFFFFu);
 			} else {
-				if (bord.decode(d, T, 0)) continue;
+				if (ru(bord.decode(d, T, 0))) continue;
 				const uint32_t w = ((in >> 8) & 3) + 1, h = ((in >> 10) & 3) + 1, cnt = w * h;
 				uint32_t k = high ? d.max_dec(cnt - 1) + 1 : d.max_dec(cnt);
 				if (k > cnt) k = cnt;
@@ -1452,7 +1528,7 @@ GC_DI uint32_t dec_frame(const GDecArgs& a, int f, uint32_t len)
 }
 
 template <bool ETAB>
-__global__ void __launch_bounds__(64) k_gc_decode(const GDecArgs* __restrict__ ap)
+__global__ void __launch_bounds__(64) GC_KATTR k_gc_decode(const GDecArgs* __restrict__ ap)
 {
 	const GDecArgs& a = *ap;
 	const int f = blockIdx.x;
@@ -1474,7 +1550,7 @@ __global__ void __launch_bounds__(64) k_gc_decode(const GDecArgs* __restrict__ a
 // 1] = status | 0x100.  ea.res / da.res get the words k_gc_encode /
 // k_gc_decode write.  A stream that failed is not decoded (result word 0).
 template <bool ETAB>
-__global__ void __launch_bounds__(64) k_gc_roundtrip(const GEncArgs* __restrict__ eap, const GDecArgs* __restrict__ dap,
+__global__ void __launch_bounds__(64) GC_KATTR k_gc_roundtrip(const GEncArgs* __restrict__ eap, const GDecArgs* __restrict__ dap,
                                                     uint32_t* posted, uint32_t* posted_dec, uint32_t tag)
 {
 	const GEncArgs& ea = *eap;

@@ -73,16 +73,20 @@ struct ZFrames {
 	const void* src = nullptr; size_t sstride = 0; long sp = 0;
 	void* out = nullptr; size_t ostride = 0; long po = 0;
 	int nz = 0;
-	// level 0 of the fused forward: the LDS ring hand-off (1, 32 KiB per
-	// workgroup) or the double buffer (0, the default: 20 KiB, so more
-	// workgroups fit beside the stream coder's waves, and no scratch spills --
-	// the ring form's consumers spill 28 bytes per lane at 128 VGPRs)
+	// level 0 of the fused forward: the LDS ring hand-off (1: 32 KiB per
+	// workgroup, the faster form alone on the chip) or the double buffer (0:
+	// 20 KiB, two workgroups per CU fit beside the stream coder's waves)
 	int ring = 0;
 	// level 0 of a gray batch straight from its u8 pixels (k_fwdq_pc_z8, the
 	// ric level shift fused): one device pointer per frame (W bytes per row,
 	// 8-byte aligned), sh8 the shift; null: from src (the coding planes)
 	const uint8_t* const* pix8 = nullptr;
 	int sh8 = 0;
+	// the last level on the one-producer form (k_fwdq_pc_z; above it the
+	// two-producer k_fwdq_pc2_z): 1 when the level kernels run alone on the
+	// chip (measured at C3: level 1 20.4 against 23.2 us per frame), 0 beside
+	// the stream coder's waves (the one-producer form holds 128 VGPRs)
+	int pc1 = 0;
 	// Split arenas (the GPU stream coder's pool): regions A and B (bands,
 	// status word, records, parent info: offsets below `split` = Pyramid::b_end)
 	// of frame f at arena + f * astride, region C (intermediate LL planes, pRD)

@@ -139,3 +139,26 @@ def test_batch_output_digests(ric, port, w, h, ch):
     for i in range(n):
         want = port.decode_ric(port.encode_ric(host[i], 9, 0))[0]
         assert got[i] == _digest(want), i
+
+
+@pytest.mark.parametrize("w,h,ch,q,t", [(1024, 768, 1, 9, 0), (640, 480, 1, 0, 1), (257, 129, 1, 9, 0),
+                                        (256, 192, 3, 9, 0), (96, 80, 3, 0, 1)])
+def test_batch_band_parallel_encode(ric, port, w, h, ch, q, t):
+    """Fewer frames in flight than half the host threads (C4's tiles, C5 over
+    many ranks): each frame's bands are modelled on the batch's band pool while
+    its task writes the stream (encode_bands_split), over the compacted payload
+    where the bands are 16-bit -- the same bytes as the oracle."""
+    frames = [ric.synth(w, h, ch, 60 + i) for i in range(2)]
+    b = ric.Batch(w, h, ch, slots=4, threads=8)
+    for _ in range(2):
+        got = b.compress(frames, q, t)
+        for f, r in zip(frames, got):
+            assert r == port.encode_ric(f, q, t)
+    if ch == 1:
+        dev = [ric.DeviceArray.from_numpy(f) for f in frames]
+        outs = [d.empty_like() for d in dev]
+        lens = b.roundtrip(dev, outs, q, t)
+        for i, f in enumerate(frames):
+            r = b.stream(i)
+            assert len(r) == lens[i] and r == port.encode_ric(f, q, t)
+            assert np.array_equal(outs[i].numpy(), port.decode_ric(r)[0])
