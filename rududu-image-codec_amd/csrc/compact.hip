@@ -24,6 +24,13 @@
 namespace ric {
 namespace {
 
+// global-address-space views of device pointers: global (not flat) loads and
+// stores, counted by vmcnt alone, so a wave's waits on its LDS and scalar
+// loads do not also wait for the loads it issued ahead
+#define GAS __attribute__((address_space(1)))
+template <typename T> __device__ __forceinline__ const GAS T* gp(const T* p) { return (const GAS T*)p; }
+template <typename T> __device__ __forceinline__ GAS T* gp(T* p) { return (GAS T*)p; }
+
 __device__ __forceinline__ int wave_excl(int v, int& total)
 {
 	// inclusive scan over the 64 lanes by shuffles, then exclusive
@@ -38,10 +45,13 @@ __device__ __forceinline__ int wave_excl(int v, int& total)
 	return x - v;
 }
 
-// the band and chunk of flattened chunk index c (bands in coding order)
-__device__ __forceinline__ int band_of(const CmpArgs& a, int c)
+// the band of flattened chunk index c (bands in coding order), searched from
+// band b0: a wave's chunks only ever move forward, so it passes each band
+// boundary once (a search from band 0 per chunk is a chain of up to 14
+// dependent scalar loads, which bound these kernels)
+__device__ __forceinline__ int band_of(const CmpArgs& a, int c, int b0 = 0)
 {
-	int b = 0;
+	int b = b0;
 	while (b + 1 < a.nb && c >= a.band[b + 1].chunk0) b++;
 	return b;
 }
@@ -52,7 +62,7 @@ __device__ __forceinline__ uint32_t block_mask(const CmpArgs& a, const char* are
 	if (s >= B.nblk) return 0;
 	int bx, by;
 	scan_block(s, B.dx, B.dy, bx, by);
-	const uint64_t r = ((const uint64_t*)(arena + B.rec_off))[(long)by * ((B.dx + 3) >> 2) + bx];
+	const uint64_t r = gp((const uint64_t*)(arena + B.rec_off))[(long)by * ((B.dx + 3) >> 2) + bx];
 	return BlockRec::mask(r);
 }
 
@@ -60,22 +70,42 @@ __device__ __forceinline__ uint32_t block_mask(const CmpArgs& a, const char* are
 // a workgroup per chunk would be hundreds of thousands of tiny dispatches,
 // which crawl when the stream coder's waves fill the CUs.
 constexpr int kCmpWaves = 4;
-__device__ __forceinline__ int wave_gid() { return (int)(blockIdx.x * kCmpWaves + (threadIdx.x >> 6)); }
+// (readfirstlane: the wave's index is uniform, so its chunk index, band and
+// band fields are scalar -- else every band field is a per-lane vector load
+// waited on before the next)
+__device__ __forceinline__ int wave_gid()
+{
+	return (int)(blockIdx.x * kCmpWaves + __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6));
+}
 __device__ __forceinline__ int wave_count() { return (int)(gridDim.x * kCmpWaves); }
 __device__ __forceinline__ int lane64() { return (int)(threadIdx.x & 63); }
 
+// four chunks per step, their record loads issued together
 __global__ __launch_bounds__(64 * kCmpWaves) void k_cmp_count(const CmpArgs* __restrict__ ap)
 {
 	const CmpArgs& a = *ap;
 	const int f = blockIdx.z;
 	const char* arena = a.arena + (size_t)f * a.astride;
-	for (int c = wave_gid(); c < a.nchunk; c += wave_count()) {
-		const int b = band_of(a, c);
-		const int s = (c - a.band[b].chunk0) * 64 + lane64();
-		int n = __popc(block_mask(a, arena, b, s));
+	const int W = wave_count();
+	int bu[4] = {0, 0, 0, 0};
+	for (int c0 = wave_gid(); c0 < a.nchunk; c0 += 4 * W) {
+		int n[4];
 #pragma unroll
-		for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o, 64);
-		if (lane64() == 0) a.cnt[(size_t)f * a.cstride + c] = (uint32_t)n;
+		for (int u = 0; u < 4; u++) {
+			const int c = c0 + u * W;
+			n[u] = 0;
+			if (c < a.nchunk) {
+				const int b = bu[u] = band_of(a, c, bu[u]);
+				n[u] = __popc(block_mask(a, arena, b, (c - a.band[b].chunk0) * 64 + lane64()));
+			}
+		}
+#pragma unroll
+		for (int u = 0; u < 4; u++) {
+			const int c = c0 + u * W;
+#pragma unroll
+			for (int o = 32; o > 0; o >>= 1) n[u] += __shfl_xor(n[u], o, 64);
+			if (c < a.nchunk && lane64() == 0) gp(a.cnt)[(size_t)f * a.cstride + c] = (uint32_t)n[u];
+		}
 	}
 }
 
@@ -115,10 +145,45 @@ __global__ __launch_bounds__(1024) void k_cmp_scan(const CmpArgs* __restrict__ a
 	}
 }
 
-// Each wave gathers its chunk's values into LDS (a lane loads its block's
-// rows as 8-byte words, its values go to the chunk's slots from its prefix),
-// then writes the chunk's run out with consecutive lanes on consecutive values:
-// one coalesced store per 64 values instead of a lane-strided store per value.
+// Each wave gathers its chunk's values into LDS (a lane holds its block's rows
+// as 8-byte words, its values go to the chunk's slots from its prefix), then
+// writes the chunk's run out with consecutive lanes on consecutive values: one
+// coalesced store per 64 values instead of a lane-strided store per value.
+// A wave's loads for its next chunk (record, rows, offset) are issued before
+// it works on the current one: with every load of a chunk independent of the
+// others, a wave keeps two chunks of loads in flight instead of waiting for
+// the record, then the rows, chunk after chunk.
+struct CmpChunk {
+	uint64_t rec;                    // the lane's block record (0: past the band)
+	uint64_t v[4];                   // its rows (valid up to its height)
+	uint32_t base;                   // the chunk's first value
+	int b, s;                        // band, scan position
+};
+
+__device__ __forceinline__ void cmp_load(const CmpArgs& a, const char* arena, const char* bsrc, int f, int c, int b0,
+                                         CmpChunk& L)
+{
+	const int b = band_of(a, c, b0);
+	const CmpBand& B = a.band[b];
+	const int s = (c - B.chunk0) * 64 + lane64();
+	L.b = b; L.s = s;
+	L.base = gp(a.cnt)[(size_t)f * a.cstride + c];
+	L.rec = 0;
+	L.v[0] = L.v[1] = L.v[2] = L.v[3] = 0;
+	if (s < B.nblk) {
+		int bx, by;
+		scan_block(s, B.dx, B.dy, bx, by);
+		L.rec = gp((const uint64_t*)(arena + B.rec_off))[(long)by * ((B.dx + 3) >> 2) + bx];
+		const int h = B.dy - by * 4;
+		// rows of the block: an 8-byte word each (the row pitch keeps the
+		// block's 4 columns inside the row's allocation), rows past the band not read
+		const int16_t* band = (const int16_t*)(bsrc + B.off) + (long)by * 4 * B.pitch + bx * 4;
+#pragma unroll
+		for (int r = 0; r < 4; r++)
+			if (r < h) L.v[r] = *gp((const uint64_t*)(band + (long)r * B.pitch));
+	}
+}
+
 __global__ __launch_bounds__(64 * kCmpWaves) void k_cmp_write(const CmpArgs* __restrict__ ap)
 {
 	const CmpArgs& a = *ap;
@@ -129,11 +194,13 @@ __global__ __launch_bounds__(64 * kCmpWaves) void k_cmp_write(const CmpArgs* __r
 	__shared__ int16_t stage[kCmpWaves][64 * 16];
 	int16_t* sv = stage[threadIdx.x >> 6];
 	const int l = lane64();
-	for (int c = wave_gid(); c < a.nchunk; c += wave_count()) {
-		const int b = band_of(a, c);
-		const CmpBand& B = a.band[b];
-		const int s = (c - B.chunk0) * 64 + l;
-		uint32_t m = block_mask(a, arena, b, s);
+	int c = wave_gid();
+	CmpChunk cur, nxt;
+	if (c < a.nchunk) cmp_load(a, arena, bsrc, f, c, 0, cur);
+	for (; c < a.nchunk; c += wave_count()) {
+		const int cn = c + wave_count();
+		if (cn < a.nchunk) cmp_load(a, arena, bsrc, f, cn, cur.b, nxt);
+		uint32_t m = BlockRec::mask(cur.rec);
 		// exclusive prefix of the popcounts: per bit, a ballot and the lanes below
 		uint32_t o = 0, tot = 0;
 #pragma unroll
@@ -142,65 +209,104 @@ __global__ __launch_bounds__(64 * kCmpWaves) void k_cmp_write(const CmpArgs* __r
 			o += __builtin_amdgcn_mbcnt_hi((uint32_t)(bb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bb, 0u));
 			tot += (uint32_t)__popcll(bb);
 		}
-		const uint32_t base = a.cnt[(size_t)f * a.cstride + c];
-		if (a.vcap && base + tot > a.vcap) continue;    // over the pool's capacity: flagged by k_cmp_scan
-		if (m) {
-			int bx, by;
-			scan_block(s, B.dx, B.dy, bx, by);
-			const int w = B.dx - bx * 4 < 4 ? B.dx - bx * 4 : 4;
-			const int16_t* band = (const int16_t*)(bsrc + B.off) + (long)by * 4 * B.pitch + bx * 4;
-			// rows of the block (an 8-byte word each: the row pitch keeps the
-			// block's 4 columns inside the row's allocation), values in raster
-			// order over the w-wide block
-			uint32_t k = o;
-			for (int r = 0; r < 4 && m; r++) {
-				const uint32_t rm = m & ((1u << w) - 1u);
-				m >>= w;
-				if (!rm) continue;
-				const uint64_t v = *(const uint64_t*)(band + (long)r * B.pitch);
-				for (uint32_t q = rm; q; q &= q - 1) sv[k++] = (int16_t)(v >> (16 * __builtin_ctz(q)));
+		const uint32_t base = cur.base;
+		// over the pool's capacity: flagged by k_cmp_scan, nothing written
+		if (!(a.vcap && base + tot > a.vcap)) {
+			if (m) {
+				const CmpBand& B = a.band[cur.b];
+				int bx, by;
+				scan_block(cur.s, B.dx, B.dy, bx, by);
+				const int w = B.dx - bx * 4 < 4 ? B.dx - bx * 4 : 4;
+				// values in raster order over the w-wide block
+				uint32_t k = o;
+#pragma unroll
+				for (int r = 0; r < 4; r++) {
+					const uint32_t rm = m & ((1u << w) - 1u);
+					m >>= w;
+					for (uint32_t q = rm; q; q &= q - 1) sv[k++] = (int16_t)(cur.v[r] >> (16 * __builtin_ctz(q)));
+				}
 			}
+			__builtin_amdgcn_wave_barrier();
+			__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+			for (uint32_t i = (uint32_t)l; i < tot; i += 64) gp(out)[base + i] = sv[i];
+			__builtin_amdgcn_wave_barrier();
 		}
-		__builtin_amdgcn_wave_barrier();
-		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-		for (uint32_t i = (uint32_t)l; i < tot; i += 64) out[base + i] = sv[i];
-		__builtin_amdgcn_wave_barrier();
+		cur = nxt;
 	}
 }
 
 // the decode side: one wave per chunk of 64 blocks (flattened over the three
-// bands): every position of each block written, a value where its mask bit is set
+// bands), every position of each block written, a value where its mask bit is
+// set.  The chunk's values are contiguous (its offset to the next chunk's, or
+// the band's count): the wave loads them into LDS with consecutive lanes on
+// consecutive values while its masks arrive, then each lane assembles its
+// block's rows and writes each as one 8-byte word (a narrow edge block value
+// by value).  The next chunk's masks and offsets are loaded ahead.
+struct DcmpChunk {
+	uint32_t m;                      // the lane's block mask (loaded)
+	uint32_t o0, tot;                // the chunk's first value and count
+	int b, s;
+};
+
+__device__ __forceinline__ void dcmp_load(const DcmpArgs& a, const char* in, int c, DcmpChunk& L)
+{
+	const uint32_t* nval = (const uint32_t*)in;
+	const int b = c >= a.chunk0[2] ? 2 : c >= a.chunk0[1] ? 1 : 0;
+	const int ch = c - a.chunk0[b];
+	const int s = ch * 64 + lane64();
+	const uint32_t* coff = (const uint32_t*)(in + a.coff_off[b]);
+	uint32_t vbase = 0;
+	for (int k = 0; k < b; k++) vbase += nval[k];
+	L.b = b; L.s = s;
+	L.o0 = vbase + coff[ch];
+	L.tot = (ch + 1 < a.chunk0[b + 1] - a.chunk0[b] ? coff[ch + 1] : nval[b]) - coff[ch];
+	L.m = s < a.nblk[b] ? gp((const uint16_t*)(in + a.mask_off[b]))[s] : 0u;
+}
+
 __global__ __launch_bounds__(64 * kCmpWaves) void k_dcmp_expand(DcmpArgs a)
 {
 	const int f = blockIdx.z;
 	const char* in = a.in + (size_t)f * a.istride;
-	const uint32_t* nval = (const uint32_t*)in;
 	const int16_t* vals = (const int16_t*)(in + a.vals_off);
-	for (int c = wave_gid(); c < a.chunk0[3]; c += wave_count()) {
-		const int b = c >= a.chunk0[2] ? 2 : c >= a.chunk0[1] ? 1 : 0;
-		uint32_t vbase = 0;
-		for (int k = 0; k < b; k++) vbase += nval[k];
-		const int ch = c - a.chunk0[b];
-		const int s = ch * 64 + lane64();
-		const uint32_t m = s < a.nblk[b] ? ((const uint16_t*)(in + a.mask_off[b]))[s] : 0u;
-		int tot;
-		const int ex = wave_excl(__popc(m), tot);
-		if (s >= a.nblk[b]) continue;
-		uint32_t o = vbase + ((const uint32_t*)(in + a.coff_off[b]))[ch] + (uint32_t)ex;
-		int bx, by;
-		scan_block(s, a.dx[b], a.dy[b], bx, by);
-		const int w = a.dx[b] - bx * 4 < 4 ? a.dx[b] - bx * 4 : 4, h = a.dy[b] - by * 4 < 4 ? a.dy[b] - by * 4 : 4;
-		int16_t* band = (int16_t*)(a.arena + (size_t)f * a.astride + a.off[b]) + (long)by * 4 * a.pitch[b] + bx * 4;
-		for (int r = 0; r < h; r++)
-			for (int q = 0; q < w; q++) {
-				const int i = r * w + q;
-				int16_t v = 0;
-				if ((m >> i) & 1) {
-					if (!a.vcap || o < a.vcap) v = vals[o];
-					o++;
-				}
-				band[(long)r * a.pitch[b] + q] = v;
+	__shared__ int16_t stage[kCmpWaves][64 * 16];
+	int16_t* sv = stage[threadIdx.x >> 6];
+	const int l = lane64();
+	int c = wave_gid();
+	DcmpChunk cur, nxt;
+	if (c < a.chunk0[3]) dcmp_load(a, in, c, cur);
+	for (; c < a.chunk0[3]; c += wave_count()) {
+		// the chunk's values into LDS (at most 1024; a value past the pool's
+		// capacity reads as 0 -- a frame the coder left to the host)
+		const uint32_t tot = cur.tot < 1024u ? cur.tot : 1024u;
+		for (uint32_t i = (uint32_t)l; i < tot; i += 64) {
+			const uint32_t o = cur.o0 + i;
+			sv[i] = (!a.vcap || o < a.vcap) ? gp(vals)[o] : (int16_t)0;
+		}
+		const int cn = c + wave_count();
+		if (cn < a.chunk0[3]) dcmp_load(a, in, cn, nxt);
+		const uint32_t m = cur.m;
+		int ptot;
+		uint32_t k = (uint32_t)wave_excl(__popc(m), ptot);
+		__builtin_amdgcn_wave_barrier();
+		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+		const int b = cur.b, s = cur.s;
+		if (s < a.nblk[b]) {
+			int bx, by;
+			scan_block(s, a.dx[b], a.dy[b], bx, by);
+			const int w = a.dx[b] - bx * 4 < 4 ? a.dx[b] - bx * 4 : 4, h = a.dy[b] - by * 4 < 4 ? a.dy[b] - by * 4 : 4;
+			int16_t* band = (int16_t*)(a.arena + (size_t)f * a.astride + a.off[b]) + (long)by * 4 * a.pitch[b] + bx * 4;
+			uint32_t mm = m;
+			for (int r = 0; r < h; r++) {
+				uint64_t word = 0;
+				for (int q = 0; q < w; q++, mm >>= 1)
+					if (mm & 1u) word |= (uint64_t)(uint16_t)sv[k++] << (16 * q);
+				if (w == 4) *gp((uint64_t*)(band + (long)r * a.pitch[b])) = word;
+				else
+					for (int q = 0; q < w; q++) gp(band)[(long)r * a.pitch[b] + q] = (int16_t)(word >> (16 * q));
 			}
+		}
+		__builtin_amdgcn_wave_barrier();
+		cur = nxt;
 	}
 }
 

@@ -49,7 +49,8 @@ def main():
            "pix_in_us": round(p["pix_in"][0] / p["pix_in"][1] * 1e3, 2) if p["pix_in"][1] else 0.0,
            "pix_out_us": round(p["pix_out"][0] / p["pix_out"][1] * 1e3, 2),
            "d2h_us": round(p["d2h"][0] / p["d2h"][1] * 1e3, 1), "h2d_us": round(p["h2d"][0] / p["h2d"][1] * 1e3, 1),
-           "compact_us": round(p["compact"][0] / p["compact"][1] * 1e3, 2) if p["compact"][1] else None}
+           "compact_us": round(p["compact"][0] / p["compact"][1] * 1e3, 2) if p["compact"][1] else None,
+           "dexp_us": round(p["dcmp_expand"][0] / p["dcmp_expand"][1] * 1e3, 2) if p["dcmp_expand"][1] else None}
     print(json.dumps(out))
 
 
