@@ -401,9 +401,10 @@ def main():
         # the stream coder's frames: two launches in flight (or the rest of --frames)
         n_gpu = nfr - n_host if (a.frames or a.batch) else min(a.launches * a.pool, nfr - n_host)
         nstep = n_host + n_gpu
-        # stream capacity: 3 bits per pixel (a q9 C3 stream is 1.7), 16-byte multiple
+        # stream capacity: 3 bits per pixel (a q9 C3 stream is 1.7; lossless q0
+        # up to 10), 16-byte multiple
         pool = min(a.pool, max(n_gpu, 1))
-        scap = (W * H * CH * 3 // 8 + 65536) // 16 * 16
+        scap = (W * H * CH * (10 if a.q == 0 else 3) // 8 + 65536) // 16 * 16
         # the pool holds bands (the finest level compacted) + records + a
         # stream per frame in flight (C3: ~79 MB; 98 MB with dense bands): if
         # it does not fit this GPU's memory, shrink it
@@ -672,7 +673,9 @@ def main():
         # the coder's issue counters (SQ_INSTS_SALU / VALU, SQ_WAIT_ANY, ... per stream)
         # cannot be read inside this process: rocprofv3 --pmc over one serving step
         # of this path at C3 (scripts/gpu_sq.sh), committed under profiles/
-        sqf = os.path.join(REPO, "profiles", "r04_stream_coder_sq.json")
+        sqf = os.path.join(REPO, "profiles", "r05_stream_coder_sq.json")
+        if not os.path.exists(sqf):
+            sqf = os.path.join(REPO, "profiles", "r04_stream_coder_sq.json")
         if os.path.exists(sqf) and a.workload == "C3":
             try:
                 sq = json.load(open(sqf))
@@ -681,8 +684,8 @@ def main():
                 coder["issue"] = {k: run[k] for k in ("kernel_s", "SQ_INSTS_SALU", "SQ_INSTS_VALU", "salu_share",
                                                        "instr_per_simd_per_4_cycles", "salu_per_cu_cycle", "wait_frac")
                                   if k in run}
-                coder["issue"]["source"] = "profiles/r04_stream_coder_sq.json runs.%s (per stream, %d streams in " \
-                                           "one k_gc_roundtrip launch)" % (rn, run.get("streams", sq["streams"]))
+                coder["issue"]["source"] = "profiles/%s runs.%s (per stream, %d streams in one k_gc_roundtrip " \
+                                           "launch)" % (os.path.basename(sqf), rn, run.get("streams", sq["streams"]))
             except (OSError, ValueError, KeyError):
                 pass
         if balance:

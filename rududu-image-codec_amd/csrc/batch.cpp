@@ -1884,7 +1884,6 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 				left[k] = 1;
 				n_fallback++;
 				tr("left to the host (over the pool's value capacity)", f0 + k);
-				ready_host.push_back({f0 + k, 1, false, 0, 0});
 				if (!bgpu[j]) copied[j].done();                    // (no host decode task copies its stream)
 				continue;
 			}
@@ -1902,6 +1901,16 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 				}
 				stream_err |= rd[k] == 1;
 			}
+		}
+		// the frames left to the host go round trip in host groups of up to SG
+		// consecutive frames (a group per frame would hold the host threads to
+		// two frames at a time: the two slot sets)
+		for (int g0 = 0; g0 < m;) {
+			if (!left[g0]) { g0++; continue; }
+			int e = g0;
+			while (e < m && e - g0 < SG && left[e]) e++;
+			ready_host.push_back({f0 + g0, e - g0, false, 0, 0});
+			g0 = e;
 		}
 		if (!bgpu[j]) {
 			enc_ms_est = 0.5 * enc_ms_est + 0.5 * (now_ms() - t_kick[j]);

@@ -8,6 +8,7 @@ import csv
 import glob
 import json
 import os
+import re
 import statistics
 import sys
 
@@ -32,20 +33,23 @@ def main():
         # dispatch order: level 0..4 per group (diag_gpu), groups repeat
         by = {}
         for r in rs:
-            by.setdefault(r["Kernel_Name"].split("(")[0], []).append(float(r["Counter_Value"]))
+            by.setdefault(re.search(r"(k_fwdq\w*(<[^(]*>)?)", r["Kernel_Name"]).group(1), []).append(float(r["Counter_Value"]))
         per[c] = by
     names = list(per["FETCH_SIZE"].keys())
     bm = wavelet_bytes(7680, 4320)
+    # groups of frames: the level-0 kernel runs once per group (levels 3 and 4
+    # may share a kernel name: their dispatches are summed per group)
+    ngroups = min(len(v) for k, v in per["FETCH_SIZE"].items() if k.startswith("k_fwdq_pc_z8") or k == "k_fwdq_pc_z<false, false>")
     tot = 0.0
     for n in names:
-        f = statistics.median(per["FETCH_SIZE"][n]) * 2 * 1024
-        w = statistics.median(per["WRITE_SIZE"][n]) * 1024
-        out["levels"].append({"kernel": n, "dispatches": len(per["FETCH_SIZE"][n]),
+        f = sum(per["FETCH_SIZE"][n]) * 2 * 1024 / ngroups
+        w = sum(per["WRITE_SIZE"][n]) * 1024 / ngroups
+        out["levels"].append({"kernel": n, "dispatches_per_group": len(per["FETCH_SIZE"][n]) / ngroups,
                               "hbm_bytes_per_frame": round((f + w) / slots)})
         tot += (f + w) / slots
     out["hbm_bytes_per_frame_all_levels"] = round(tot)
     out["algorithmic_bytes_per_frame"] = sum(bm["dwt"]) + sum(bm["quant"]) + bm["ll"]
-    out["correction"] = "FETCH_SIZE x2 (gfx950), WRITE_SIZE as is; KiB -> B; medians over the dispatches of each kernel"
+    out["correction"] = "FETCH_SIZE x2 (gfx950), WRITE_SIZE as is; KiB -> B; every dispatch summed, divided by the groups (level-0 dispatches) and the frames per group"
     out["source"] = ("round 5: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, over scripts/kbench_batch.py "
                      "--iters 3 (ric_batch_diag_gpu: the 5 forward levels of 16 C3 frames alone, the level kernels' "
                      "alone forms)")
