@@ -31,6 +31,8 @@ namespace {
 template <typename T> __device__ __forceinline__ const GAS T* gp(const T* p) { return (const GAS T*)p; }
 template <typename T> __device__ __forceinline__ GAS T* gp(T* p) { return (GAS T*)p; }
 
+__device__ __forceinline__ int lane64() { return (int)(threadIdx.x & 63); }
+
 __device__ __forceinline__ int wave_excl(int v, int& total)
 {
 	// inclusive scan over the 64 lanes by shuffles, then exclusive
@@ -56,14 +58,47 @@ __device__ __forceinline__ int band_of(const CmpArgs& a, int c, int b0 = 0)
 	return b;
 }
 
-__device__ __forceinline__ uint32_t block_mask(const CmpArgs& a, const char* arena, int b, int s)
+// the mask of the block at scan position s0 + lane
+__device__ __forceinline__ uint32_t block_mask(const CmpArgs& a, const char* arena, int b, int s0)
 {
 	const CmpBand& B = a.band[b];
-	if (s >= B.nblk) return 0;
+	if (s0 + lane64() >= B.nblk) return 0;
 	int bx, by;
-	scan_block(s, B.dx, B.dy, bx, by);
+	scan_block(s0 + lane64(), B.dx, B.dy, bx, by);
 	const uint64_t r = gp((const uint64_t*)(arena + B.rec_off))[(long)by * ((B.dx + 3) >> 2) + bx];
 	return BlockRec::mask(r);
+}
+
+// exclusive prefix over the wave's lanes of v < 32, and the wave's total: a
+// ballot per bit of v (five), each lane's count of the set lanes below it
+__device__ __forceinline__ uint32_t wave_prefix5(uint32_t v, uint32_t& tot)
+{
+	uint32_t o = 0, t = 0;
+#pragma unroll
+	for (int b = 0; b < 5; b++) {
+		const uint64_t bb = __ballot((v >> b) & 1u);
+		o += __builtin_amdgcn_mbcnt_hi((uint32_t)(bb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bb, 0u)) << b;
+		t += (uint32_t)__popcll(bb) << b;
+	}
+	tot = t;
+	return o;
+}
+
+// (bx, by) of scan position s0 + lane (s0 wave-uniform, scan_block's order):
+// a chunk of a band at least 64 blocks wide spans at most two block rows, so
+// the row is one scalar division per chunk and a compare per lane instead of
+// a division per lane
+__device__ __forceinline__ void chunk_block(int s0, int lane, int dx, int dy, int& bx, int& by)
+{
+	const int bw = (dx + 3) >> 2, nfx = dx >> 2;
+	if (bw < 64) { scan_block(s0 + lane, dx, dy, bx, by); return; }
+	const int by0 = s0 / bw;
+	int p = s0 - by0 * bw + lane;
+	by = by0;
+	if (p >= bw) { p -= bw; by++; }
+	if (!(by & 1)) bx = p;
+	else if (nfx < bw) bx = p == 0 ? nfx : nfx - p;
+	else bx = nfx - 1 - p;
 }
 
 // A few workgroups of 4 waves per frame, each wave striding over the chunks:
@@ -78,7 +113,6 @@ __device__ __forceinline__ int wave_gid()
 	return (int)(blockIdx.x * kCmpWaves + __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6));
 }
 __device__ __forceinline__ int wave_count() { return (int)(gridDim.x * kCmpWaves); }
-__device__ __forceinline__ int lane64() { return (int)(threadIdx.x & 63); }
 
 // four chunks per step, their record loads issued together
 __global__ __launch_bounds__(64 * kCmpWaves) void k_cmp_count(const CmpArgs* __restrict__ ap)
@@ -96,7 +130,7 @@ __global__ __launch_bounds__(64 * kCmpWaves) void k_cmp_count(const CmpArgs* __r
 			n[u] = 0;
 			if (c < a.nchunk) {
 				const int b = bu[u] = band_of(a, c, bu[u]);
-				n[u] = __popc(block_mask(a, arena, b, (c - a.band[b].chunk0) * 64 + lane64()));
+				n[u] = __popc(block_mask(a, arena, b, (c - a.band[b].chunk0) * 64));
 			}
 		}
 #pragma unroll
@@ -158,6 +192,7 @@ struct CmpChunk {
 	uint64_t v[4];                   // its rows (valid up to its height)
 	uint32_t base;                   // the chunk's first value
 	int b, s;                        // band, scan position
+	int bx, by;                      // the lane's block
 };
 
 __device__ __forceinline__ void cmp_load(const CmpArgs& a, const char* arena, const char* bsrc, int f, int c, int b0,
@@ -165,14 +200,15 @@ __device__ __forceinline__ void cmp_load(const CmpArgs& a, const char* arena, co
 {
 	const int b = band_of(a, c, b0);
 	const CmpBand& B = a.band[b];
-	const int s = (c - B.chunk0) * 64 + lane64();
+	const int s0 = (c - B.chunk0) * 64, s = s0 + lane64();
 	L.b = b; L.s = s;
 	L.base = gp(a.cnt)[(size_t)f * a.cstride + c];
 	L.rec = 0;
 	L.v[0] = L.v[1] = L.v[2] = L.v[3] = 0;
+	int bx, by;
+	chunk_block(s0, lane64(), B.dx, B.dy, bx, by);
+	L.bx = bx; L.by = by;
 	if (s < B.nblk) {
-		int bx, by;
-		scan_block(s, B.dx, B.dy, bx, by);
 		L.rec = gp((const uint64_t*)(arena + B.rec_off))[(long)by * ((B.dx + 3) >> 2) + bx];
 		const int h = B.dy - by * 4;
 		// rows of the block: an 8-byte word each (the row pitch keeps the
@@ -184,14 +220,16 @@ __device__ __forceinline__ void cmp_load(const CmpArgs& a, const char* arena, co
 	}
 }
 
-__global__ __launch_bounds__(64 * kCmpWaves) void k_cmp_write(const CmpArgs* __restrict__ ap)
+__global__ __launch_bounds__(64 * kCmpWaves) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_cmp_write(const CmpArgs* __restrict__ ap)
 {
 	const CmpArgs& a = *ap;
 	const int f = blockIdx.z;
 	const char* arena = a.arena + (size_t)f * a.astride;
 	const char* bsrc = a.bsrc ? a.bsrc + (size_t)f * a.bstride : arena;
 	int16_t* out = (int16_t*)(a.out + (size_t)f * a.ostride);
-	__shared__ int16_t stage[kCmpWaves][64 * 16];
+	// a chunk's values, then one dump slot per lane (the writes of the
+	// positions a lane does not keep)
+	__shared__ int16_t stage[kCmpWaves][64 * 16 + 64];
 	int16_t* sv = stage[threadIdx.x >> 6];
 	const int l = lane64();
 	int c = wave_gid();
@@ -201,24 +239,26 @@ __global__ __launch_bounds__(64 * kCmpWaves) void k_cmp_write(const CmpArgs* __r
 		const int cn = c + wave_count();
 		if (cn < a.nchunk) cmp_load(a, arena, bsrc, f, cn, cur.b, nxt);
 		uint32_t m = BlockRec::mask(cur.rec);
-		// exclusive prefix of the popcounts: per bit, a ballot and the lanes below
-		uint32_t o = 0, tot = 0;
-#pragma unroll
-		for (int i = 0; i < 16; i++) {
-			const uint64_t bb = __ballot((m >> i) & 1u);
-			o += __builtin_amdgcn_mbcnt_hi((uint32_t)(bb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bb, 0u));
-			tot += (uint32_t)__popcll(bb);
-		}
+		uint32_t tot;
+		const uint32_t o = wave_prefix5((uint32_t)__popc(m), tot);
 		const uint32_t base = cur.base;
 		// over the pool's capacity: flagged by k_cmp_scan, nothing written
 		if (!(a.vcap && base + tot > a.vcap)) {
-			if (m) {
-				const CmpBand& B = a.band[cur.b];
-				int bx, by;
-				scan_block(cur.s, B.dx, B.dy, bx, by);
-				const int w = B.dx - bx * 4 < 4 ? B.dx - bx * 4 : 4;
-				// values in raster order over the w-wide block
-				uint32_t k = o;
+			const CmpBand& B = a.band[cur.b];
+			const int w = B.dx - cur.bx * 4 < 4 ? B.dx - cur.bx * 4 : 4;
+			uint32_t k = o;
+			if (w == 4) {
+				// the 16 positions in raster order, straight through: a kept
+				// value to its slot, the others to the lane's dump slot
+				const uint32_t dump = 1024u + (uint32_t)l;
+#pragma unroll
+				for (int i = 0; i < 16; i++) {
+					const uint32_t bit = (m >> i) & 1u;
+					sv[bit ? k : dump] = (int16_t)(cur.v[i >> 2] >> (16 * (i & 3)));
+					k += bit;
+				}
+			} else if (m) {
+				// a block cut by the band's right edge: w values per row
 #pragma unroll
 				for (int r = 0; r < 4; r++) {
 					const uint32_t rm = m & ((1u << w) - 1u);
@@ -285,24 +325,42 @@ __global__ __launch_bounds__(64 * kCmpWaves) void k_dcmp_expand(DcmpArgs a)
 		const int cn = c + wave_count();
 		if (cn < a.chunk0[3]) dcmp_load(a, in, cn, nxt);
 		const uint32_t m = cur.m;
-		int ptot;
-		uint32_t k = (uint32_t)wave_excl(__popc(m), ptot);
+		uint32_t ptot;
+		uint32_t k = wave_prefix5((uint32_t)__popc(m), ptot);
 		__builtin_amdgcn_wave_barrier();
 		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 		const int b = cur.b, s = cur.s;
+		int bx, by;
+		chunk_block(s - l, l, a.dx[b], a.dy[b], bx, by);
 		if (s < a.nblk[b]) {
-			int bx, by;
-			scan_block(s, a.dx[b], a.dy[b], bx, by);
 			const int w = a.dx[b] - bx * 4 < 4 ? a.dx[b] - bx * 4 : 4, h = a.dy[b] - by * 4 < 4 ? a.dy[b] - by * 4 : 4;
 			int16_t* band = (int16_t*)(a.arena + (size_t)f * a.astride + a.off[b]) + (long)by * 4 * a.pitch[b] + bx * 4;
-			uint32_t mm = m;
-			for (int r = 0; r < h; r++) {
-				uint64_t word = 0;
-				for (int q = 0; q < w; q++, mm >>= 1)
-					if (mm & 1u) word |= (uint64_t)(uint16_t)sv[k++] << (16 * q);
-				if (w == 4) *gp((uint64_t*)(band + (long)r * a.pitch[b])) = word;
-				else
-					for (int q = 0; q < w; q++) gp(band)[(long)r * a.pitch[b] + q] = (int16_t)(word >> (16 * q));
+			if (w == 4 && h == 4) {
+				// straight through the 16 positions: a kept position takes the
+				// lane's next value, the others read a slot and drop it
+#pragma unroll
+				for (int r = 0; r < 4; r++) {
+					uint64_t word = 0;
+#pragma unroll
+					for (int q = 0; q < 4; q++) {
+						const uint32_t bit = (m >> (4 * r + q)) & 1u;
+						const uint32_t v = (uint16_t)sv[bit ? k : 0u];
+						word |= (uint64_t)(bit ? v : 0u) << (16 * q);
+						k += bit;
+					}
+					*gp((uint64_t*)(band + (long)r * a.pitch[b])) = word;
+				}
+			} else {
+				// a block cut by the band's right or bottom edge
+				uint32_t mm = m;
+				for (int r = 0; r < h; r++) {
+					uint64_t word = 0;
+					for (int q = 0; q < w; q++, mm >>= 1)
+						if (mm & 1u) word |= (uint64_t)(uint16_t)sv[k++] << (16 * q);
+					if (w == 4) *gp((uint64_t*)(band + (long)r * a.pitch[b])) = word;
+					else
+						for (int q = 0; q < w; q++) gp(band)[(long)r * a.pitch[b] + q] = (int16_t)(word >> (16 * q));
+				}
 			}
 		}
 		__builtin_amdgcn_wave_barrier();
