@@ -297,6 +297,10 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
  * for a side with no work).  For splitting frames between the two (no
  * reference counterpart). */
 int ric_batch_hybrid_times(ric_batch* b, double* host_ms, double* gpu_ms);
+/* Frames of the last ric_batch_roundtrip_hybrid that the stream coder left
+ * to a host round trip because they hold more level-0 values than the
+ * compacted pool's capacity (no reference counterpart). */
+int ric_batch_hybrid_fallbacks(ric_batch* b, int* frames);
 /* Stage timers of the batch (no reference counterpart): 0 pixel conversion
  * in, 1..8 forward level 0..7 (fused DWT + quantiser + records), 9 D2H of
  * bands + records, 10 host encode, 11 host decode, 12 H2D of the bands,

@@ -204,6 +204,7 @@ struct ric_batch {
 	long nready = 0;
 	int device = 0, w = 0, h = 0, channels = 1, slots = 0;
 	double hyb_host_ms = 0, hyb_gpu_ms = 0;        // last hybrid call: when each side finished (ms from entry)
+	int hyb_fallback = 0;                          // last hybrid call: frames over the pool's value capacity
 	Pyramid P;
 	size_t astride = 0, hstride = 0, pstride = 0;   // bytes per slot: device arena, host mirror, coding planes
 	long pitch = 0;                                // coding plane row pitch (elements)
@@ -1541,6 +1542,7 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 	};
 	int host_groups_done = 0;
 	b->hyb_host_ms = b->hyb_gpu_ms = 0;
+	b->hyb_fallback = 0;
 	std::deque<HGroup> ready_host, ready_dec;
 	for (int f0 = 0; f0 < n_host; f0 += SG) ready_host.push_back({f0, std::min(SG, n_host - f0), false, 0, 0});
 	const int ng = n - n_host;
@@ -2130,6 +2132,7 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 	for (int h = 0; h < 2; h++)
 		if (c.st[h]) (void)hipStreamSynchronize(c.st[h]);
 	const bool ok = !bfail(hipStreamSynchronize(b->st), "hipStreamSynchronize");
+	b->hyb_fallback = n_fallback;
 	if (trace)
 		fprintf(stderr, "[hybrid] %d coder-frame groups harvested while the launch ran; %d frames left to the host "
 		                "(over the compacted pool's value capacity)\n", hv_early, n_fallback);
@@ -2190,5 +2193,14 @@ int ric_batch_hybrid_times(ric_batch* b, double* host_ms, double* gpu_ms)
 	if (!b || !host_ms || !gpu_ms) return RIC_E_ARG;
 	*host_ms = b->hyb_host_ms;
 	*gpu_ms = b->hyb_gpu_ms;
+	return RIC_OK;
+}
+
+// Frames of the last ric_batch_roundtrip_hybrid the stream coder left to a
+// host round trip (over the compacted pool's value capacity)
+int ric_batch_hybrid_fallbacks(ric_batch* b, int* frames)
+{
+	if (!b || !frames) return RIC_E_ARG;
+	*frames = b->hyb_fallback;
 	return RIC_OK;
 }

@@ -107,6 +107,7 @@ def lib():
         "ric_batch_hybrid_config": (_I, [_P, _I, ctypes.c_size_t]),
         "ric_batch_hybrid_config_ex": (_I, [_P, _I, ctypes.c_size_t, ctypes.c_long]),
         "ric_batch_hybrid_times": (_I, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
+        "ric_batch_hybrid_fallbacks": (_I, [_P, ctypes.POINTER(ctypes.c_int)]),
         "ric_batch_decode_gpu": (_I, [_P, _P, ctypes.c_size_t, _P, _I, _P]),
         "ric_diag_gdec_dbg": (_I, [_P]),
         "ric_batch_roundtrip_hybrid": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
@@ -649,6 +650,13 @@ class Batch:
         hm, gm = ctypes.c_double(), ctypes.c_double()
         _chk(lib().ric_batch_hybrid_times(self.h, ctypes.byref(hm), ctypes.byref(gm)), "ric_batch_hybrid_times")
         return hm.value, gm.value
+
+    def hybrid_fallbacks(self):
+        """Frames of the last roundtrip_hybrid over the pool's value capacity
+        (round-tripped on the host instead)."""
+        n = ctypes.c_int(0)
+        _chk(lib().ric_batch_hybrid_fallbacks(self.h, ctypes.byref(n)), "ric_batch_hybrid_fallbacks")
+        return n.value
 
     def roundtrip_hybrid(self, frames, pix_out, n_host, q=9, trans=0, gpu_decode=False, streams=None,
                          allow_stream_err=False):

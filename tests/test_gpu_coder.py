@@ -304,6 +304,25 @@ def test_hybrid_compacted_pool_capacity(ric, port, gpu_decode, c):
             assert d[i] == shard.digest_bytes(px), (vc, i)
 
 
+@pytest.mark.parametrize("c,slots", [(1, 4), (3, 6)])
+def test_hybrid_capacity_fallback_groups(ric, port, c, slots):
+    """Every stream-coder frame over the compacted pool's capacity (consecutive
+    frames): they go round trip on the host in groups of up to slots / c
+    frames (round 5; one frame per group before), same bytes and pixels."""
+    w, h, n = 192, 128, 10
+    host = [ric.synth(w, h, c, 600 + i) for i in range(n)]
+    frames = [ric.DeviceArray.from_numpy(x) for x in host]
+    want = [port.encode_ric(x, 9, 0) for x in host]
+    b = ric.Batch(w, h, c, slots=slots, threads=3)
+    b.hybrid_config(4, (w * h * c * 2 + 65536 + 15) // 16 * 16, 64)
+    outs = [f.empty_like() for f in frames]
+    lens = b.roundtrip_hybrid(frames, outs, 1, 9, 0, gpu_decode=1)
+    assert b.hybrid_fallbacks() == n - 1
+    for i in range(n):
+        assert lens[i] == len(want[i]) and b.stream(i) == want[i], i
+        assert np.array_equal(outs[i].numpy().reshape(-1), port.decode_ric(want[i])[0].reshape(-1)), i
+
+
 @pytest.mark.parametrize("slots", [1, 2])
 def test_hybrid_colour_small_slots(ric, port, slots):
     """Colour frames need three slots per host-coded frame.  A compacted pool
