@@ -228,6 +228,11 @@ GC_DI void prio_band(int mode, bool dec, int b, int nb)
 // a coder wave that finds it raised at a chunk boundary sleeps (at most ~0.25
 // ms per check, so a flag left raised only slows the coder), leaving the CU's
 // issue slots to the level kernel's waves.
+// RIC_GC_YCHK: blocks between two checks of the yield flag (a power of two
+// <= 64; 64: once per chunk)
+#ifndef RIC_GC_YCHK
+#define RIC_GC_YCHK 64
+#endif
 GC_DI void coder_yield(const uint32_t* flag)
 {
 	if (!flag) return;
@@ -738,6 +743,7 @@ GC_DI void tree_enc(E& e, const GTabs& T, const GBandDesc& B, const char* arena,
 		}
 		const int nj = nblk - s0 < 64 ? nblk - s0 : 64;
 		for (int j = 0; j < nj; j++) {
+			if (RIC_GC_YCHK < 64 && j && !(j & (RIC_GC_YCHK - 1))) coder_yield(yield);
 			const uint32_t li = (uint32_t)j;
 			const uint64_t r = (uint64_t)lget(rc.lo, li) | (uint64_t)lget(rc.hi, li) << 32;
 			const uint32_t ins = BlockRec::insig(r);
@@ -1402,6 +1408,7 @@ GC_DI void tree_dec(GDec& d, const GTabs& T, const GBandDesc& B, const GBandDesc
 		__threadfence_block();
 		const int nj = nblk - s0 < 64 ? nblk - s0 : 64;
 		for (int j = 0; j < nj; j++) {
+			if (RIC_GC_YCHK < 64 && j && !(j & (RIC_GC_YCHK - 1))) coder_yield(yield);
 			const uint32_t in = lget(info, (uint32_t)j);
 			const uint32_t ob = (uint32_t)j * 16;
 			d.ensure();
