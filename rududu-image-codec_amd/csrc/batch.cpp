@@ -205,6 +205,7 @@ struct ric_batch {
 	int device = 0, w = 0, h = 0, channels = 1, slots = 0;
 	double hyb_host_ms = 0, hyb_gpu_ms = 0;        // last hybrid call: when each side finished (ms from entry)
 	int hyb_fallback = 0;                          // last hybrid call: frames over the pool's value capacity
+	bool cmp_dma = false;                          // host frames' compacted values to the host by DMA (d2h_slots)
 	Pyramid P;
 	size_t astride = 0, hstride = 0, pstride = 0;   // bytes per slot: device arena, host mirror, coding planes
 	long pitch = 0;                                // coding plane row pitch (elements)
@@ -489,8 +490,20 @@ int d2h_slots(ric_batch* b, int set, int n)
 		BCHK(hipMemcpyAsync(b->h_cmp_total + s0, b->d_cmp_total + s0, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, b->st));
 		{
 			auto sv = b->prof.begin(B_D2HV, n, b->st);
-			if (launch_cmp_to_host(b->d_cmp + (size_t)s0 * b->cmp_stride, b->cmp_stride, b->h_arena_dev + (size_t)s0 * b->hstride,
-			                       b->hstride, b->d_cmp_total + s0, n, b->st))
+			// In the serving step (cmp_dma): the values' whole capacity by the
+			// copy engine -- about twice the bytes of the values, but no CUs
+			// taken from the stream coder's launch: a kernel writing each frame's
+			// count into the device-mapped mirror held CUs for the PCIe writes
+			// and slowed the launch by 3 % (C3 step: 11,363-11,382 against
+			// 11,168 Mpix/s, profiles/r05_cmp_dma_ab.json).  Elsewhere the kernel
+			// (only the values cross PCIe).  RIC_CMP_DMA=0/1 forces either.
+			static const int dma_env = [] { const char* e = getenv("RIC_CMP_DMA"); return e ? atoi(e) : -1; }();
+			const bool dma = dma_env >= 0 ? dma_env != 0 : b->cmp_dma;
+			if (dma) {
+				BCHK(hipMemcpy2DAsync(b->harena(s0), b->hstride, b->d_cmp + (size_t)s0 * b->cmp_stride, b->cmp_stride,
+				                      std::min(b->cmp_stride, b->hstride), n, hipMemcpyDeviceToHost, b->st));
+			} else if (launch_cmp_to_host(b->d_cmp + (size_t)s0 * b->cmp_stride, b->cmp_stride, b->h_arena_dev + (size_t)s0 * b->hstride,
+			                              b->hstride, b->d_cmp_total + s0, n, b->st))
 				return bfail(hipGetLastError(), "compact to host") ? RIC_E_HIP : RIC_E_HIP;
 			b->prof.end(sv);
 		}
@@ -1471,9 +1484,10 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 	// before the coder launch, switches to the alone forms)
 	struct FormGuard {
 		ric_batch* b;
-		~FormGuard() { b->alone(true); }
+		~FormGuard() { b->alone(true); b->cmp_dma = false; }
 	} form_guard{b};
 	b->alone(false);
+	b->cmp_dma = true;
 	b->split = false;                                      // every host thread codes frames of its own here
 	auto& c = b->cp;
 	Pyramid& P = b->P;
