@@ -153,7 +153,11 @@ __global__ void k_gray_out8(const int16_t* __restrict__ in, long pi, int w, int 
                             int16_t* __restrict__ planes, int rows, unsigned long long* dig)
 {
 	const int x = (blockIdx.x * blockDim.x + threadIdx.x) * 8, y0 = blockIdx.y * rows;
-	unsigned long long s = 0;
+	// the digest sum_k pix[k] (k M + 1) mod 2^64 as M sum_k pix[k] k + sum_k
+	// pix[k]: per 8 pixels at k = i0 + i, sum_k pix[k] k = i0 (sum pix) + sum
+	// pix[i] i -- one 64-bit product per 8 pixels instead of eight
+	unsigned long long s = 0, s2 = 0;
+	uint32_t s1 = 0;
 	if (x < w) {
 		for (int y = y0; y < y0 + rows && y < h; y++) {
 			int16_t v[8];
@@ -167,11 +171,18 @@ __global__ void k_gray_out8(const int16_t* __restrict__ in, long pi, int w, int 
 			if (planes) *reinterpret_cast<uint4*>(planes + i0) = pack8s(v);
 			if (pix) *reinterpret_cast<uint2*>(pix + i0) = pack8b(v);
 			if (DIG) {
+				uint32_t a = 0, t = 0;
 #pragma unroll
-				for (int i = 0; i < 8; i++)
-					s += (unsigned long long)(uint8_t)clip255(v[i]) * ((unsigned long long)(i0 + i) * kDigestMul + 1);
+				for (int i = 0; i < 8; i++) {
+					const uint32_t c = (uint8_t)clip255(v[i]);
+					a += c;
+					t += c * (uint32_t)i;
+				}
+				s2 += (unsigned long long)i0 * a + t;
+				s1 += a;
 			}
 		}
+		if (DIG) s = s2 * kDigestMul + s1;
 	}
 	if (DIG) {
 #pragma unroll
