@@ -171,7 +171,10 @@ struct ric_batch {
 	void alone(bool on)
 	{
 		static const bool en = [] { const char* e = getenv("RIC_FQZ_ALONE"); return !e || atoi(e) != 0; }();
-		fq_ring = fq_pc1 = on && en ? 1 : 0;
+		// alone: the LDS-ring hand-off, levels 0-2 on one producer wave (level 2:
+		// 5.8-6.0 against 6.3-6.4 us per C3 frame, profiles/r05_level12_sweep.log)
+		fq_ring = on && en ? 1 : 0;
+		fq_pc1 = on && en ? 2 : 0;
 	}
 	ric_batch() { alone(true); }
 	// The host encoder's payload compacted on the GPU (compact.hip): the

@@ -2710,7 +2710,7 @@ void zargs_free(ZArgs& z)
 namespace {
 // segment rows of the ring forms over nz frames: about one round of resident
 // workgroups over the whole batch (tuning knobs RIC_FQZ_SL0..2)
-int pc_seg_rows_z(int W, int H, int nz, int level)
+int pc_seg_rows_z(int W, int H, int nz, int level, bool two_rounds = false)
 {
 	static const int sl[3] = {[] { const char* e = getenv("RIC_FQZ_SL0"); return e ? atoi(e) : 0; }(),
 	                          [] { const char* e = getenv("RIC_FQZ_SL1"); return e ? atoi(e) : 0; }(),
@@ -2722,7 +2722,9 @@ int pc_seg_rows_z(int W, int H, int nz, int level)
 	// levels 1-2 (latency-bound chains): one round over the whole batch
 	if (level == 0) return pc_seg_rows(W, H);
 	const int nstrip = (W + kFqStrip - 1) / kFqStrip;
-	const int want = std::max(1, kPcResident / (nstrip * nz));          // segments per strip per frame
+	// (two_rounds: level 1's one-producer form alone on the chip, measured
+	// 19.0-19.3 against 19.4-20.0 us per C3 frame, profiles/r05_level12_sweep.log)
+	const int want = std::max(1, kPcResident / (nstrip * nz)) * (two_rounds ? 2 : 1);   // segments per strip per frame
 	const int s = ((H + want - 1) / want + 7) / 8 * 8;
 	return s < 8 ? 8 : s;
 }
@@ -2732,7 +2734,11 @@ int launch_fwdq_level_z(const Pyramid& P, int l, const ZFrames& fr, int vec8, in
                         ZArgs& z, hipStream_t st, int in8)
 {
 	const Level& L = P.L[l];
-	const int S = pc_seg_rows_z(L.w, L.h, fr.nz, l);
+	// the one-producer form on level 0 (VALU-bound), two producers above (see
+	// fq_launch_pc); knob RIC_FQZ_PC1 = the last level on one producer
+	static const int pc1_env = [] { const char* e = getenv("RIC_FQZ_PC1"); return e ? atoi(e) : -1; }();
+	const int pc1 = pc1_env >= 0 ? pc1_env : fr.pc1;
+	const int S = pc_seg_rows_z(L.w, L.h, fr.nz, l, l == 1 && l <= pc1);
 	std::vector<FqArgs> v(fr.nz);
 	for (int f = 0; f < fr.nz; f++) {
 		v[f] = fq_args(P, l, (const char*)fr.src + f * fr.sstride, fr.sp, vec8, vec16, qp, fr.arena + f * fr.astride, false,
@@ -2742,10 +2748,6 @@ int launch_fwdq_level_z(const Pyramid& P, int l, const ZFrames& fr, int vec8, in
 	if (zargs_put(z, v.data(), v.size() * sizeof(FqArgs), st)) return -1;
 	const FqArgs* d = (const FqArgs*)z.dev;
 	const dim3 grid((L.w + kFqStrip - 1) / kFqStrip, v[0].nseg, fr.nz);
-	// the one-producer form on level 0 (VALU-bound), two producers above (see
-	// fq_launch_pc); knob RIC_FQZ_PC1 = the last level on one producer
-	static const int pc1_env = [] { const char* e = getenv("RIC_FQZ_PC1"); return e ? atoi(e) : -1; }();
-	const int pc1 = pc1_env >= 0 ? pc1_env : fr.pc1;
 	// the ring or the double-buffered hand-off (ZFrames::ring; knob
 	// RIC_FQZ_ASYNC=0/1 overrides)
 	static const int async_env = [] { const char* e = getenv("RIC_FQZ_ASYNC"); return e ? atoi(e) : -1; }();
