@@ -42,9 +42,12 @@ def _compile(src, hdr_mtime):
         # host sources (the serial coder): x86-64-v3 (AVX2/BMI2/LZCNT, present on the
         # GPU boxes' EPYC and this container's Xeon): encoder -7 %.  ROCm's clang
         # rather than g++ 11: the host coder 5-6 % faster on the box's EPYC 9575F
-        # (scripts/hostbench, one C3 frame: encode 102.8 -> 97.6 ms, decode 120.3 -> 112.9)
-        cmd = [HOSTCXX] + COMMON + ["-march=x86-64-v3", "-Wall", "-D__HIP_PLATFORM_AMD__", "-I" + os.path.join(ROCM, "include"),
-                                    "-c", path, "-o", obj]
+        # (scripts/hostbench, one C3 frame: encode 102.8 -> 97.6 ms, decode 120.3 -> 112.9).
+        # Scheduled for the box's Zen 5 (-mtune only: the code still runs here;
+        # decode -1 %).
+        tune = ["-mtune=znver5"] if "clang" in os.path.basename(HOSTCXX) else []
+        cmd = [HOSTCXX] + COMMON + ["-march=x86-64-v3", "-Wall"] + tune + [
+            "-D__HIP_PLATFORM_AMD__", "-I" + os.path.join(ROCM, "include"), "-c", path, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError("compile failed: %s\n%s" % (" ".join(cmd), r.stderr))

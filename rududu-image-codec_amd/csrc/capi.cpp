@@ -438,12 +438,18 @@ int decode_band(ric_wavelet* w, Mux& m)
 int decode_inverse_pipelined(ric_wavelet* w, Mux& m, int16_t* dimg, long stride, int trans, int quant)
 {
 	Pyramid& P = w->P;
-	auto issue = [&](int l) -> int {
-		// level l's D, H, V are contiguous in region A; the coarsest LL ends it
-		const Level& L = P.L[l];
-		const size_t lo = L.b[BD].off;
-		const size_t hi = l + 1 == P.nlev ? P.a_end : L.b[BV].off + L.b[BV].bytes();
+	auto put = [&](size_t lo, size_t hi) -> int {
 		HIPCHK(hipMemcpyAsync(w->d_arena + lo, w->h_arena + lo, hi - lo, hipMemcpyHostToDevice, w->st));
+		return RIC_OK;
+	};
+	auto issue = [&](int l) -> int {
+		// the coarsest level's D, H, V and the LL (contiguous in region A) go
+		// here; a finer level's bands went one by one as each became final
+		const Level& L = P.L[l];
+		if (l + 1 == P.nlev) {
+			int rc = put(L.b[BD].off, P.a_end);
+			if (rc) return rc;
+		}
 		void* out;
 		long po;
 		int out_int;
@@ -466,6 +472,15 @@ int decode_inverse_pipelined(ric_wavelet* w, Mux& m, int16_t* dimg, long stride,
 			BandView par;
 			if (l + 1 < P.nlev) par = view(w, P.L[l + 1].b[order[k]]);
 			tree_decode_fast(m, view(w, P.L[l].b[order[k]]), par, l == 0, l > 0);
+			// final now: the parent band (this scan cleared its markers) below
+			// the coarsest level, and a finest band (no children) itself --
+			// their copies overlap the next bands' decoding
+			const Band* done[2] = {l + 2 < P.nlev ? &P.L[l + 1].b[order[k]] : nullptr, l == 0 ? &P.L[0].b[order[k]] : nullptr};
+			for (const Band* B : done)
+				if (B) {
+					int rc = put(B->off, B->off + B->bytes());
+					if (rc) return rc;
+				}
 		}
 		if (l + 1 < P.nlev) {
 			int rc = issue(l + 1);

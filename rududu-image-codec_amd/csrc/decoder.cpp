@@ -104,7 +104,7 @@ struct DecCore {
 		if (__builtin_expect(p < limit, 1)) p++; else ovf = true;
 		return b;
 	}
-	__attribute__((noinline)) void norm()                      // normalize_dec, muxcodec.cpp:76-85
+	RIC_AI void norm()                                         // normalize_dec, muxcodec.cpp:76-85
 	{
 		do {
 			if (((code - low + range - 1) ^ (code - low)) >= 0x01000000u) range = (low - code) & 4095u;
@@ -118,10 +118,10 @@ struct DecCore {
 	{
 		if (__builtin_expect(range <= 4096u, 0)) norm();
 		const uint32_t t = (range * freq) >> 12;
-		const uint32_t tst = (uint32_t)(low < t) - 1u;
-		low -= t & tst;
-		range = t + ((range - 2 * t) & tst);
-		return tst & 1u;
+		const bool one = low >= t;                      // the same outcome, selects instead of masks
+		low = one ? low - t : low;
+		range = one ? range - t : t;
+		return one;
 	}
 	RIC_AI void fill(uint32_t len)                               // fillBuffer, muxcodec.cpp:572-579
 	{
@@ -273,26 +273,36 @@ struct GeoM {                                                   // CGeomCodec
 // not re-read from memory after every coefficient store (a band store may
 // alias the uint16_t model words for the compiler).
 struct GeoReg {
-	uint32_t freq, idx;
-	RIC_AI void load(const GeoM& g, int c) { freq = g.freq[c]; idx = g.idx[c]; }
+	// the context's idx-dependent parameters kept ready (k, the adaptation
+	// shift, its two thresholds), reloaded only when idx moves: the
+	// coefficient-to-coefficient recurrence is then the frequency update
+	// alone, not idx -> shift -> threshold loads (encoder.cpp GeoRegE)
+	uint32_t freq, idx, k, sh, th0, span;
+	RIC_AI void params()
+	{
+		const int s = kGeoShift[idx];
+		k = kGeoK[idx]; sh = 3 + s;
+		th0 = kGeoThres[s - 1]; span = (uint32_t)(kGeoThres[s] - kGeoThres[s - 1]);
+	}
+	RIC_AI void load(const GeoM& g, int c) { freq = g.freq[c]; idx = g.idx[c]; params(); }
 	RIC_AI void store(GeoM& g, int c) const { g.freq[c] = (uint16_t)freq; g.idx[c] = (uint8_t)idx; }
 	template <uint32_t LMAX>
 	RIC_AI int decode_signed(DecCore& d)                         // GeoM::decode_signed
 	{
-		const uint32_t k = kGeoK[idx], f = freq;
-		const int s = kGeoShift[idx];
+		const uint32_t f = freq;
 		uint32_t fr = freq, l = 0;
 		while (d.get_bit(f)) {
-			fr -= fr >> (3 + s);
+			fr -= fr >> sh;
 			if (++l > LMAX) break;                  // corrupt-stream guard
 		}
 		const uint32_t v = d.bits(k + 1);
 		const uint32_t sym = (l << k) | (v >> 1);
-		fr = (uint16_t)(fr + ((4096 - fr) >> (3 + s)));             // adapt
-		if ((uint16_t)(fr - kGeoThres[s - 1]) > kGeoThres[s] - kGeoThres[s - 1]) {
-			if (fr < kGeoThres[s - 1]) { if (idx < 24) idx++; }
+		fr = (uint16_t)(fr + ((4096 - fr) >> sh));                  // adapt
+		if (__builtin_expect((uint16_t)(fr - th0) > span, 0)) {
+			if (fr < th0) { if (idx < 24) idx++; }
 			else if (idx > 0) idx--;
 			if (idx >= 9) fr = 2048;
+			params();
 		}
 		freq = fr;
 		const int mag = (int)sym + 1;
@@ -357,8 +367,12 @@ RIC_AI int block_full_dec(DecCore& d, GeoM& g, C* blk, long st, int idx, CmpSink
 	return (int)k - (HIGH ? 1 : 0);
 }
 
+// The coder state goes in and comes back by value: a DecCore whose address
+// escapes into a call lives in memory, and tree_dec's loop would then load and
+// store range / low through the stack on every bit.
 template <typename C, bool HIGH, bool CMP = false>
-void block_edge_dec(DecCore& d, GeoM& g, C* blk, long st, int w, int h, CmpSink* cs = nullptr)
+__attribute__((noinline)) DecCore block_edge_dec(DecCore d, GeoM& g, C* blk, long st, int w, int h,
+                                                 CmpSink* cs = nullptr)
 {
 	constexpr bool SH = sizeof(C) == 2;
 	const uint32_t cnt = (uint32_t)(w * h);
@@ -379,6 +393,7 @@ void block_edge_dec(DecCore& d, GeoM& g, C* blk, long st, int w, int h, CmpSink*
 			}
 	}
 	if (CMP) cs->block(m);
+	return d;
 }
 
 // CBandCodec::tree<decode>, src/lib/bandcodec.cpp:484-589
@@ -399,17 +414,25 @@ void tree_dec(Mux& m, const BandView& b, const BandView& par, bool has_child, Cm
 	const int pdx = par.dx, pdy = par.dy;
 	const C mark = (C)tr<SH>(has_child ? kInsignif : 0);
 	C* band = (C*)b.p;
-	if (!CMP)
-		for (int j = 0; j < dy; j++) memset(band + j * st, 0, sizeof(C) * dx);   // Clear(), :503
+	// Clear() (:503) a stripe of rows at a time, just before its blocks are
+	// decoded: the zeroed lines are still in cache when the coefficients land
+	// (a whole-band clear first sends them to memory and reads them back)
+	auto clear = [&](int j, int h) {
+		if (!CMP)
+			for (int r = 0; r < h; r++) memset(band + (j + r) * st, 0, sizeof(C) * dx);
+	};
 
-	auto edge = [&](C* c1, int i, int w, int h, P* pp, bool chk_row, int j) {
+	// d passes through by value (a captured reference would put it in memory)
+	auto edge = [&](DecCore d, C* c1, int i, int w, int h, P* pp, bool chk_row, int j) {
 		if (pp && (i >> 1) < pdx && (!chk_row || (j >> 1) < pdy) && pp[i >> 1] == kInsignif) pp[i >> 1] = 0;
-		if (!bord.decode(d, 0)) block_edge_dec<C, HIGH, CMP>(d, g, c1 + i, st, w, h, cs);
+		if (!bord.decode(d, 0)) d = block_edge_dec<C, HIGH, CMP>(d, g, c1 + i, st, w, h, cs);
 		else if (CMP) cs->block(0);
+		return d;
 	};
 
 	int j = 0;
 	for (; j + 4 <= dy; j += 4) {
+		clear(j, 4);
 		C* c1 = band + j * st;
 		C* c2 = c1 + 2 * st;
 		P* pp = pbase ? pbase + (long)(j >> 1) * pst : nullptr;
@@ -417,7 +440,7 @@ void tree_dec(Mux& m, const BandView& b, const BandView& par, bool has_child, Cm
 		if (j & 4) {
 			bs = -4;
 			i = dx & ~3;
-			if (dx > i) edge(c1, i, dx - i, 4, pp, false, j);
+			if (dx > i) d = edge(d, c1, i, dx - i, 4, pp, false, j);
 			i += bs;
 		}
 		for (; i >= 0 && i + 4 <= dx; i += bs) {
@@ -441,9 +464,10 @@ void tree_dec(Mux& m, const BandView& b, const BandView& par, bool has_child, Cm
 				kmean[ctx] = (uint16_t)(kmean[ctx] + ((uint32_t)kk << 7) - (kmean[ctx] >> 3));
 			}
 		}
-		if (i > 0 && i < dx) edge(c1, i, dx - i, 4, pp, false, j);
+		if (i > 0 && i < dx) d = edge(d, c1, i, dx - i, 4, pp, false, j);
 	}
 	if (j < dy) {
+		clear(j, dy - j);
 		C* c1 = band + j * st;
 		P* pp = pbase ? pbase + (long)(j >> 1) * pst : nullptr;
 		const int h = dy - j;
@@ -451,15 +475,15 @@ void tree_dec(Mux& m, const BandView& b, const BandView& par, bool has_child, Cm
 		if (j & 4) {
 			bs = -4;
 			i = dx & ~3;
-			if (dx > i) edge(c1, i, dx - i, h, pp, true, j);
+			if (dx > i) d = edge(d, c1, i, dx - i, h, pp, true, j);
 			i += bs;
 		}
 		for (; i >= 0 && i + 4 <= dx; i += bs) {
 			if (pp && (j >> 1) < pdy && pp[i >> 1] == kInsignif) pp[i >> 1] = 0;
-			if (!bord.decode(d, 0)) block_edge_dec<C, HIGH, CMP>(d, g, c1 + i, st, 4, h, cs);
+			if (!bord.decode(d, 0)) d = block_edge_dec<C, HIGH, CMP>(d, g, c1 + i, st, 4, h, cs);
 			else if (CMP) cs->block(0);
 		}
-		if (i > 0 && i < dx) edge(c1, i, dx - i, h, pp, true, j);
+		if (i > 0 && i < dx) d = edge(d, c1, i, dx - i, h, pp, true, j);
 	}
 	m.set_dec_state(d.state());
 }

@@ -26,7 +26,9 @@ int main(int argc, char** argv)
 		double s1, s2, s3;
 		long len = hc_encode_rec(b.data(), n, 1, 7680, 4320, 5, 1, out.data(), cap, &s1, &s2);
 		hc_decode(out.data(), len, 1, 7680, 4320, 5, 1, dec.data(), &s3);
-		printf("len %ld enc %.2f dec %.2f\n", len, s1 * 1e3, s3 * 1e3);
+		uint64_t h = 1469598103934665603ull;              // FNV-1a of the decoded bands
+		for (long i = 0; i < n; i++) h = (h ^ (uint32_t)dec[i]) * 1099511628211ull;
+		printf("len %ld enc %.2f dec %.2f hash %016llx\n", len, s1 * 1e3, s3 * 1e3, (unsigned long long)h);
 	}
 	return 0;
 }
