@@ -38,7 +38,7 @@ struct EncCore {
 	explicit EncCore(const Mux::EncState& st) : s(st) {}
 
 	RIC_AI void put(uint8_t* slot, uint8_t v) { if (__builtin_expect(slot < s.limit, 1)) *slot = v; else s.ovf = true; }
-	__attribute__((noinline)) void norm()                 // normalize_enc, muxcodec.cpp:63-74
+	RIC_AI void norm()                                    // normalize_enc, muxcodec.cpp:63-74
 	{
 		// flushBuffer<false>: every complete raw byte first, then reserve the partial one
 		while (s.ebits >= 8) {
@@ -55,7 +55,7 @@ struct EncCore {
 			s.low <<= 8;
 		} while (s.range <= 4096u);
 	}
-	__attribute__((noinline)) void drain()                // emptyBuffer, muxcodec.cpp:536-548
+	RIC_AI void drain()                                   // emptyBuffer, muxcodec.cpp:536-548
 	{
 		while (s.ebits >= 8) {
 			s.ebits -= 8;
@@ -68,8 +68,8 @@ struct EncCore {
 		RIC_STAT(0, 1);
 		if (__builtin_expect(s.range <= 4096u, 0)) norm();
 		const uint32_t t = (s.range * freq) >> 12;
-		s.low += t & (0u - bit);
-		s.range = t + ((s.range - 2 * t) & (0u - bit));
+		s.low = bit ? s.low + t : s.low;
+		s.range = bit ? s.range - t : t;
 	}
 	RIC_AI void bits(uint32_t v, uint32_t len)             // bitsCode (64-bit FIFO, see entropy.h)
 	{
@@ -386,8 +386,8 @@ void replay_events(Mux& m, const uint64_t* ev, size_t n)
 		if (__builtin_expect((lo >> 14) & (e.s.range <= 4096u), 0)) e.norm();
 		const uint32_t freq = (lo >> 1) & 0x1FFFu, bit = lo & 1u;
 		const uint32_t t = (e.s.range * freq) >> 12;
-		e.s.low += t & (0u - bit);
-		e.s.range = t + ((e.s.range - 2 * t) & (0u - bit));
+		e.s.low = bit ? e.s.low + t : e.s.low;
+		e.s.range = bit ? e.s.range - t : t;
 		const uint32_t len = (lo >> 16) & 63u;
 		if (__builtin_expect(e.s.ebits + len > 64, 0)) e.drain();
 		e.s.ebuf = (e.s.ebuf << len) | (uint32_t)(x >> 32);
