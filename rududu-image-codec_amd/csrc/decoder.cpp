@@ -88,29 +88,40 @@ const HuffLutD kHuffLutD;
 
 #define RIC_AI __attribute__((always_inline)) inline
 
-struct DecCore {
-	uint32_t range, low, code, nbits, buffer;
-	const uint8_t* p;
-	const uint8_t* limit;
-	bool ovf;
+// The decoder's cold state -- the code register (read only by the carry
+// check of a normalisation), the stream limit and the overflow flag -- lives
+// outside the register state, so the hot loop keeps range, low, the raw-bit
+// buffer and the stream pointer in registers.  One decoder runs per thread at
+// a time.
+thread_local uint32_t t_code;
+thread_local const uint8_t* t_limit;
+thread_local bool t_ovf;
 
-	explicit DecCore(const Mux::DecState& s)
-		: range(s.range), low(s.low), code(s.code), nbits(s.nbits), buffer(s.buffer), p(s.p), limit(s.limit), ovf(s.ovf) {}
-	Mux::DecState state() const { return {range, low, code, nbits, buffer, p, limit, ovf}; }
+struct DecCore {
+	uint32_t range, low, nbits, buffer;
+	const uint8_t* p;
+
+	explicit DecCore(const Mux::DecState& s) : range(s.range), low(s.low), nbits(s.nbits), buffer(s.buffer), p(s.p)
+	{
+		t_code = s.code; t_limit = s.limit; t_ovf = s.ovf;
+	}
+	Mux::DecState state() const { return {range, low, t_code, nbits, buffer, p, t_limit, t_ovf}; }
 
 	RIC_AI uint8_t next()
 	{
 		const uint8_t b = *p;
-		if (__builtin_expect(p < limit, 1)) p++; else ovf = true;
+		if (__builtin_expect(p < t_limit, 1)) p++; else t_ovf = true;
 		return b;
 	}
 	RIC_AI void norm()                                         // normalize_dec, muxcodec.cpp:76-85
 	{
 		do {
-			if (((code - low + range - 1) ^ (code - low)) >= 0x01000000u) range = (low - code) & 4095u;
+			// the carry fix is rare: a predicted branch keeps t_code off the range chain
+			const uint32_t code = t_code;
+			if (__builtin_expect(((code - low + range - 1) ^ (code - low)) >= 0x01000000u, 0)) range = (low - code) & 4095u;
 			const uint32_t b = next();
 			low = (low << 8) | b;
-			code = (code << 8) | b;
+			t_code = (code << 8) | b;
 			range <<= 8;
 		} while (range <= 4096u);
 	}
@@ -150,7 +161,7 @@ struct DecCore {
 			}
 		}
 		p -= (int)(nbits - len) >> 3;
-		if (__builtin_expect(p > limit, 0)) { p = limit; ovf = true; }
+		if (__builtin_expect(p > t_limit, 0)) { p = t_limit; t_ovf = true; }
 		if (nbits < len) buffer = p[-1];
 		nbits = (nbits - len) & 7;
 		return sym;
