@@ -380,6 +380,12 @@ int ric_video_motion(ric_video* v, uint32_t* mv);
 #define RIC_COPY_D2H 2
 #define RIC_COPY_D2D 3
 int ric_device_alloc(int device, size_t bytes, void** out);   /* RIC_E_CAPACITY when HBM is exhausted */
+/* ric_device_free / ric_host_free never wait for a GPU stream coder launch:
+ * hipFree / hipHostFree synchronise the whole device, so while a call with a
+ * coder launch in flight runs (ric_batch_encode_gpu, _decode_gpu,
+ * _roundtrip_hybrid, on any thread) the pointer is parked and freed when the
+ * last such call returns; otherwise it is freed at once.  The same holds for
+ * the buffers of any ric_* object destroyed meanwhile. */
 int ric_device_free(void* p);
 int ric_device_copy(int device, void* dst, const void* src, size_t bytes, int kind);
 int ric_device_memset(int device, void* p, int value, size_t bytes);
@@ -450,6 +456,8 @@ int ric_diag_wgtrace(int device, uint64_t* out, int n);
  * (CodeBand, Quantize, TransformQuantize, the codec's encode) returns
  * RIC_E_HIP instead of a corrupt result. */
 int ric_diag_fault(int on);
+/* the number of frees parked so far (ric_device_free above) */
+long ric_diag_deferred_frees(void);
 /* SURVEY.md §8(d) synthetic image: channels planes of w*h bytes */
 void ric_synth_image(int w, int h, int channels, int frame, uint8_t* out);
 

@@ -943,34 +943,34 @@ void ric_batch_destroy(ric_batch* b)
 	for (int s = 0; s < 2; s++)
 		for (int l = 0; l < kMaxLevels; l++) { zargs_free(b->zf[s][l]); zargs_free(b->zi[s][l]); }
 	b->prof.destroy();
-	if (b->d_arena) (void)hipFree(b->d_arena);
-	if (b->h_arena) (void)hipHostFree(b->h_arena);
-	if (b->d_cmp) (void)hipFree(b->d_cmp);
-	if (b->d_cmp_cnt) (void)hipFree(b->d_cmp_cnt);
-	if (b->d_cmp_total) (void)hipFree(b->d_cmp_total);
-	if (b->h_cmp_total) (void)hipHostFree(b->h_cmp_total);
-	if (b->d_cmp_args) (void)hipFree(b->d_cmp_args);
-	if (b->d_planes) (void)hipFree(b->d_planes);
-	if (b->d_stage) (void)hipFree(b->d_stage);
-	if (b->d_genc) (void)hipFree(b->d_genc);
-	if (b->d_gdec) (void)hipFree(b->d_gdec);
-	if (b->d_res) (void)hipFree(b->d_res);
-	if (b->h_res) (void)hipHostFree(b->h_res);
+	if (b->d_arena) (void)dev_free(b->d_arena);
+	if (b->h_arena) (void)pinned_free(b->h_arena);
+	if (b->d_cmp) (void)dev_free(b->d_cmp);
+	if (b->d_cmp_cnt) (void)dev_free(b->d_cmp_cnt);
+	if (b->d_cmp_total) (void)dev_free(b->d_cmp_total);
+	if (b->h_cmp_total) (void)pinned_free(b->h_cmp_total);
+	if (b->d_cmp_args) (void)dev_free(b->d_cmp_args);
+	if (b->d_planes) (void)dev_free(b->d_planes);
+	if (b->d_stage) (void)dev_free(b->d_stage);
+	if (b->d_genc) (void)dev_free(b->d_genc);
+	if (b->d_gdec) (void)dev_free(b->d_gdec);
+	if (b->d_res) (void)dev_free(b->d_res);
+	if (b->h_res) (void)pinned_free(b->h_res);
 	{
 		auto& c = b->cp;
 		for (int h = 0; h < 2; h++)
 			if (c.st[h]) (void)hipStreamSynchronize(c.st[h]);
-		if (c.d_ab) (void)hipFree(c.d_ab);
-		if (c.d_out) (void)hipFree(c.d_out);
-		if (c.d_args) (void)hipFree(c.d_args);
-		if (c.d_dargs) (void)hipFree(c.d_dargs);
-		if (c.h_res) (void)hipHostFree(c.h_res);
-		if (c.d_ts) (void)hipFree(c.d_ts);
-		if (c.h_post) (void)hipHostFree(c.h_post);
-		if (c.d_yield) (void)hipFree(c.d_yield);
-		if (c.d_pcmp) (void)hipFree(c.d_pcmp);
-		if (c.d_pcnt) (void)hipFree(c.d_pcnt);
-		if (c.d_ptotal) (void)hipFree(c.d_ptotal);
+		if (c.d_ab) (void)dev_free(c.d_ab);
+		if (c.d_out) (void)dev_free(c.d_out);
+		if (c.d_args) (void)dev_free(c.d_args);
+		if (c.d_dargs) (void)dev_free(c.d_dargs);
+		if (c.h_res) (void)pinned_free(c.h_res);
+		if (c.d_ts) (void)dev_free(c.d_ts);
+		if (c.h_post) (void)pinned_free(c.h_post);
+		if (c.d_yield) (void)dev_free(c.d_yield);
+		if (c.d_pcmp) (void)dev_free(c.d_pcmp);
+		if (c.d_pcnt) (void)dev_free(c.d_pcnt);
+		if (c.d_ptotal) (void)dev_free(c.d_ptotal);
 		for (int h = 0; h < 2; h++) {
 			if (c.ev_fwd[h]) (void)hipEventDestroy(c.ev_fwd[h]);
 			if (c.ev_done[h]) (void)hipEventDestroy(c.ev_done[h]);
@@ -1156,6 +1156,7 @@ int ric_batch_roundtrip(ric_batch* b, const uint8_t* const* pix, int n, int q, i
 int ric_batch_encode_gpu(ric_batch* b, const uint8_t* const* pix, int n, int q, int trans, uint8_t* out, size_t ostride,
                          size_t cap, size_t* len)
 {
+	const CoderCall coder_call;   // frees from other threads park until this call ends (ric_kernels.h)
 	// the coder stores 16-byte chunks (gcoder.hip GEnc::flush_to): a capacity or
 	// stride off a multiple of 16 would drop the stream's last bytes unflagged
 	if (!b || !pix || !out || !len || n < 0 || n > b->slots || q < 0 || q > 31 || trans < 0 || trans > 2 || cap > ostride ||
@@ -1222,6 +1223,7 @@ extern "C" int ric_diag_gdec_dbg(void* dev_buf)
 // its end (the frames are still written), as ric_batch_decode.
 int ric_batch_decode_gpu(ric_batch* b, const uint8_t* in, size_t istride, const size_t* len, int n, uint8_t* const* pix_out)
 {
+	const CoderCall coder_call;   // frees from other threads park until this call ends (ric_kernels.h)
 	if (!b || !in || !len || !pix_out || n < 0 || n > b->slots || (istride & 15) || istride > 0xFFFFFFF0u) return RIC_E_ARG;
 	const int C = b->channels;
 	if (C == 3 && 3 * n > b->nslot()) return RIC_E_ARG;
@@ -1331,14 +1333,14 @@ int ric_batch_hybrid_config_ex(ric_batch* b, int pool_frames, size_t stream_cap,
 	auto& c = b->cp;
 	for (int h = 0; h < 2; h++)
 		if (c.st[h]) BCHK(hipStreamSynchronize(c.st[h]));
-	if (c.d_ab) { BCHK(hipFree(c.d_ab)); c.d_ab = nullptr; }
-	if (c.d_out) { BCHK(hipFree(c.d_out)); c.d_out = nullptr; }
-	if (c.h_res) { BCHK(hipHostFree(c.h_res)); c.h_res = c.d_res = nullptr; }
-	if (c.d_ts) { BCHK(hipFree(c.d_ts)); c.d_ts = nullptr; }
-	if (c.h_post) { BCHK(hipHostFree(c.h_post)); c.h_post = c.d_post = nullptr; }
-	if (c.d_pcmp) { BCHK(hipFree(c.d_pcmp)); c.d_pcmp = nullptr; }
-	if (c.d_pcnt) { BCHK(hipFree(c.d_pcnt)); c.d_pcnt = nullptr; }
-	if (c.d_ptotal) { BCHK(hipFree(c.d_ptotal)); c.d_ptotal = nullptr; }
+	if (c.d_ab) { BCHK(dev_free(c.d_ab)); c.d_ab = nullptr; }
+	if (c.d_out) { BCHK(dev_free(c.d_out)); c.d_out = nullptr; }
+	if (c.h_res) { BCHK(pinned_free(c.h_res)); c.h_res = c.d_res = nullptr; }
+	if (c.d_ts) { BCHK(dev_free(c.d_ts)); c.d_ts = nullptr; }
+	if (c.h_post) { BCHK(pinned_free(c.h_post)); c.h_post = c.d_post = nullptr; }
+	if (c.d_pcmp) { BCHK(dev_free(c.d_pcmp)); c.d_pcmp = nullptr; }
+	if (c.d_pcnt) { BCHK(dev_free(c.d_pcnt)); c.d_pcnt = nullptr; }
+	if (c.d_ptotal) { BCHK(dev_free(c.d_ptotal)); c.d_ptotal = nullptr; }
 	if (!c.d_yield) {
 		BCHK(hipMalloc(&c.d_yield, 256));
 		BCHK(hipMemset(c.d_yield, 0, 256));
@@ -1369,7 +1371,7 @@ int ric_batch_hybrid_config_ex(ric_batch* b, int pool_frames, size_t stream_cap,
 	// pending (a caller may retry with a smaller pool)
 	if (hipMalloc(&c.d_ab, 2 * c.fstride * c.n) != hipSuccess || hipMalloc(&c.d_out, 2 * c.ocap * c.n) != hipSuccess) {
 		const hipError_t e = hipGetLastError();
-		if (c.d_ab) (void)hipFree(c.d_ab);
+		if (c.d_ab) (void)dev_free(c.d_ab);
 		c.d_ab = nullptr;
 		c.d_out = nullptr;
 		set_last_error(std::string("ric_batch_hybrid_config: pool of ") + std::to_string(pool_frames) +
@@ -1439,15 +1441,15 @@ int ric_batch_hybrid_config_ex(ric_batch* b, int pool_frames, size_t stream_cap,
 	};
 	const int rc = rest();
 	if (rc) {
-		(void)hipFree(c.d_ab);
-		(void)hipFree(c.d_out);
+		(void)dev_free(c.d_ab);
+		(void)dev_free(c.d_out);
 		c.d_ab = nullptr;
 		c.d_out = nullptr;
-		if (c.h_res) (void)hipHostFree(c.h_res);
-		if (c.h_post) (void)hipHostFree(c.h_post);
-		if (c.d_pcmp) (void)hipFree(c.d_pcmp);
-		if (c.d_pcnt) (void)hipFree(c.d_pcnt);
-		if (c.d_ptotal) (void)hipFree(c.d_ptotal);
+		if (c.h_res) (void)pinned_free(c.h_res);
+		if (c.h_post) (void)pinned_free(c.h_post);
+		if (c.d_pcmp) (void)dev_free(c.d_pcmp);
+		if (c.d_pcnt) (void)dev_free(c.d_pcnt);
+		if (c.d_ptotal) (void)dev_free(c.d_ptotal);
 		c.h_res = c.d_res = c.h_post = c.d_post = nullptr;
 		c.d_pcmp = nullptr; c.d_pcnt = c.d_ptotal = nullptr;
 		c.n = 0;
@@ -1470,6 +1472,7 @@ struct HGroup {
 int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, int n_host, int gpu_decode, int q,
                                int trans, uint8_t* const* out, const size_t* cap, size_t* len, uint8_t* const* pix_out)
 {
+	const CoderCall coder_call;   // frees from other threads park until this call ends (ric_kernels.h)
 	if (!b || !pix || !out || !cap || !len || !pix_out || n < 0 || n_host < 0 || n_host > n || q < 0 || q > 31 ||
 	    trans < 0 || trans > 2)
 		return RIC_E_ARG;

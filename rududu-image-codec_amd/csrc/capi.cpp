@@ -642,11 +642,11 @@ void ric_wavelet_destroy(ric_wavelet* w)
 	(void)hipSetDevice(w->device);
 	if (w->st) (void)hipStreamSynchronize(w->st);
 	w->prof.destroy();
-	if (w->d_arena) (void)hipFree(w->d_arena);
-	if (w->d_img) (void)hipFree(w->d_img);
-	if (w->h_arena) (void)hipHostFree(w->h_arena);
-	if (w->d_small) (void)hipFree(w->d_small);
-	if (w->h_small) (void)hipHostFree(w->h_small);
+	if (w->d_arena) (void)dev_free(w->d_arena);
+	if (w->d_img) (void)dev_free(w->d_img);
+	if (w->h_arena) (void)pinned_free(w->h_arena);
+	if (w->d_small) (void)dev_free(w->d_small);
+	if (w->h_small) (void)pinned_free(w->h_small);
 	if (w->own_stream && w->st) (void)hipStreamDestroy(w->st);
 	delete w;
 }
@@ -1099,9 +1099,9 @@ void ric_codec_destroy(ric_codec* c)
 	if (!c) return;
 	(void)hipSetDevice(c->device);
 	if (c->wav) ric_wavelet_destroy(c->wav);
-	if (c->d_planes) (void)hipFree(c->d_planes);
-	if (c->d_pix) (void)hipFree(c->d_pix);
-	if (c->d_out) (void)hipFree(c->d_out);
+	if (c->d_planes) (void)dev_free(c->d_planes);
+	if (c->d_pix) (void)dev_free(c->d_pix);
+	if (c->d_out) (void)dev_free(c->d_out);
 	delete c;
 }
 
@@ -1284,6 +1284,8 @@ int ric_diag_wgtrace(int device, uint64_t* out, int n)
 	const int r = diag_wgtrace(device, out, n);
 	return r < 0 ? RIC_E_HIP : r;
 }
+
+long ric_diag_deferred_frees(void) { return deferred_frees(); }
 
 int ric_diag_fault(int on)
 {

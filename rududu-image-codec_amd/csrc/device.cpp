@@ -102,7 +102,7 @@ int aux_ready(Aux& a)
 int aux_stage(Aux& a, size_t bytes)
 {
 	if (a.stage_n >= bytes) return RIC_OK;
-	if (a.h_stage) DCHK(hipHostFree(a.h_stage));   // (growth only: once per size class)
+	if (a.h_stage) DCHK(pinned_free(a.h_stage));   // (growth only: once per size class)
 	a.h_stage = nullptr;
 	a.stage_n = 0;
 	const size_t n = std::max(kStageMin, (bytes + (16u << 20) - 1) / (16u << 20) * (16u << 20));
@@ -130,7 +130,58 @@ unsigned long long host_digest(const uint8_t* p, size_t n)
 	return s2 * kMul + s1;
 }
 
+// ------------------------------------------------ frees beside a coder launch
+// (codec_params.h CoderCall).  The lock is held across an immediate free, so a
+// CoderCall cannot begin (and launch) between the check and the free.
+std::mutex g_free_mu;
+int g_coder_calls = 0;
+long g_parked = 0;
+std::vector<std::pair<void*, bool>> g_deferred;   // (pointer, pinned)
+
+hipError_t free_now(void* p, bool pinned) { return pinned ? hipHostFree(p) : hipFree(p); }
+
+hipError_t free_or_park(void* p, bool pinned)
+{
+	if (!p) return hipSuccess;
+	// RIC_PARK_FREES=0: free at once (the A/B of tests/test_gpu_zz_concurrency.py)
+	static const bool park = [] { const char* e = getenv("RIC_PARK_FREES"); return !e || atoi(e) != 0; }();
+	std::lock_guard<std::mutex> g(g_free_mu);
+	if (park && g_coder_calls > 0) {
+		g_deferred.emplace_back(p, pinned);
+		g_parked++;
+		return hipSuccess;
+	}
+	return free_now(p, pinned);
+}
+
 }  // namespace
+
+namespace ric {
+
+CoderCall::CoderCall()
+{
+	std::lock_guard<std::mutex> g(g_free_mu);
+	g_coder_calls++;
+}
+
+CoderCall::~CoderCall()
+{
+	std::lock_guard<std::mutex> g(g_free_mu);
+	if (--g_coder_calls > 0) return;
+	for (auto& d : g_deferred) (void)free_now(d.first, d.second);
+	g_deferred.clear();
+}
+
+hipError_t dev_free(void* p) { return free_or_park(p, false); }
+hipError_t pinned_free(void* p) { return free_or_park(p, true); }
+
+long deferred_frees()
+{
+	std::lock_guard<std::mutex> g(g_free_mu);
+	return g_parked;
+}
+
+}  // namespace ric
 
 struct ric_comm {
 	ncclComm_t comm = nullptr;
@@ -161,7 +212,7 @@ int ric_device_alloc(int device, size_t bytes, void** out)
 
 int ric_device_free(void* p)
 {
-	if (p) DCHK(hipFree(p));
+	if (p) DCHK(dev_free(p));
 	return RIC_OK;
 }
 
@@ -175,7 +226,7 @@ int ric_host_alloc(size_t bytes, void** out)
 
 int ric_host_free(void* p)
 {
-	if (p) DCHK(hipHostFree(p));
+	if (p) DCHK(pinned_free(p));
 	return RIC_OK;
 }
 
@@ -309,7 +360,7 @@ void ric_comm_destroy(ric_comm* c)
 	(void)hipSetDevice(c->device);
 	if (c->st) (void)hipStreamSynchronize(c->st);
 	if (c->comm) (void)ncclCommDestroy(c->comm);
-	if (c->d_red) (void)hipFree(c->d_red);
+	if (c->d_red) (void)dev_free(c->d_red);
 	if (c->st) (void)hipStreamDestroy(c->st);
 	delete c;
 }
@@ -319,7 +370,7 @@ int ric_comm_allreduce_f64(ric_comm* c, double* vals, int n, int op)
 	if (!c || !vals || n < 1 || op < 0 || op > 2) return RIC_E_ARG;
 	DCHK(hipSetDevice(c->device));
 	if (c->red_n < n) {
-		if (c->d_red) DCHK(hipFree(c->d_red));
+		if (c->d_red) DCHK(dev_free(c->d_red));
 		c->d_red = nullptr;
 		DCHK(hipMalloc(&c->d_red, sizeof(double) * (size_t)n));
 		c->red_n = n;

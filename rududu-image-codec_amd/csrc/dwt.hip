@@ -2689,7 +2689,7 @@ int zargs_put(ZArgs& z, const void* data, size_t bytes, hipStream_t st)
 	// the previous image may still be read by queued launches or copied from
 	if (hipStreamSynchronize(st) != hipSuccess) return -1;
 	if (z.cap < bytes) {
-		if (z.dev && hipFree(z.dev) != hipSuccess) return -1;
+		if (z.dev && dev_free(z.dev) != hipSuccess) return -1;
 		z.dev = nullptr;
 		z.cap = 0;
 		if (hipMalloc(&z.dev, bytes) != hipSuccess) return -1;
@@ -2701,7 +2701,7 @@ int zargs_put(ZArgs& z, const void* data, size_t bytes, hipStream_t st)
 
 void zargs_free(ZArgs& z)
 {
-	if (z.dev) (void)hipFree(z.dev);
+	if (z.dev) (void)dev_free(z.dev);
 	z.dev = nullptr;
 	z.cap = 0;
 	z.img.clear();

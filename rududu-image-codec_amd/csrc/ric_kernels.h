@@ -6,6 +6,24 @@
 
 namespace ric {
 
+// Frees that never wait for a stream coder launch (device.cpp).  hipFree and
+// hipHostFree synchronise every stream of the device, so a free issued while a
+// k_gc_* launch runs (seconds) -- a caller's buffer released by its garbage
+// collector, another batch destroyed -- would wait for the whole launch.
+// CoderCall marks a library call that may have such a launch in flight; while
+// any is active, dev_free / pinned_free park the pointer and the last
+// CoderCall to end frees it.  With none active they free at once.
+struct CoderCall {
+	CoderCall();
+	~CoderCall();
+	CoderCall(const CoderCall&) = delete;
+	CoderCall& operator=(const CoderCall&) = delete;
+};
+hipError_t dev_free(void* p);       // hipFree, deferred while a CoderCall is active
+hipError_t pinned_free(void* p);    // hipHostFree, the same
+long deferred_frees();              // frees parked so far (ric_diag_deferred_frees)
+
+
 // Forward level: src (level input, in_is_int ? int32 : int16, pitch sp) -> the
 // level's D/H/V/L bands in the arena.  vec: src rows are 8/16-byte aligned.
 void launch_fwd_level(const Level& L, const void* src, long sp, char* arena, int trans, int vec,

@@ -106,7 +106,7 @@ struct ric_video {
 		VCHK(hipMemsetAsync(raw, 0, bytes, st));      // a fresh CImage reads as zeros (see oracle/ref_video.cpp)
 		return RIC_OK;
 	}
-	static void free_image(int16_t* p) { if (p) (void)hipFree(p - kImgSlack); }
+	static void free_image(int16_t* p) { if (p) (void)dev_free(p - kImgSlack); }
 	// CImageBuffer::getFree (imagebuffer.cpp:44-61)
 	int get_free(int* id)
 	{
@@ -265,11 +265,11 @@ void ric_video_destroy(ric_video* v)
 	if (v->st) (void)hipStreamSynchronize(v->st);
 	for (int16_t* p : v->bufs) ric_video::free_image(p);
 	ric_video::free_image(v->pred);
-	if (v->d_mv) (void)hipFree(v->d_mv);
-	if (v->d_dist) (void)hipFree(v->d_dist);
-	if (v->d_gran) (void)hipFree(v->d_gran);
-	if (v->d_status) (void)hipFree(v->d_status);
-	if (v->d_rgb) (void)hipFree(v->d_rgb);
+	if (v->d_mv) (void)dev_free(v->d_mv);
+	if (v->d_dist) (void)dev_free(v->d_dist);
+	if (v->d_gran) (void)dev_free(v->d_gran);
+	if (v->d_status) (void)dev_free(v->d_status);
+	if (v->d_rgb) (void)dev_free(v->d_rgb);
 	if (v->wav) ric_wavelet_destroy(v->wav);
 	delete v;
 }
@@ -299,7 +299,7 @@ int ric_video_encode(ric_video* v, const uint8_t* pix, int stride, int pix_on_de
 	if (!pix_on_device) {
 		const size_t n = (size_t)stride * g.h * 3;
 		if (v->rgb_cap < n) {
-			if (v->d_rgb) VCHK(hipFree(v->d_rgb));
+			if (v->d_rgb) VCHK(dev_free(v->d_rgb));
 			VCHK(hipMalloc(&v->d_rgb, n));
 			v->rgb_cap = n;
 		}

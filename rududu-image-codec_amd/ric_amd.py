@@ -96,6 +96,7 @@ def lib():
         "ric_synth_image": (None, [_I, _I, _I, _I, _P]),
         "ric_diag_wgtrace": (_I, [_I, _P, _I]),
         "ric_diag_fault": (_I, [_I]),
+        "ric_diag_deferred_frees": (ctypes.c_long, []),
         "ric_batch_create": (_I, [ctypes.POINTER(_P), _I, _I, _I, _I, _I, _I]),
         "ric_batch_destroy": (None, [_P]),
         "ric_batch_encode": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _P]),

@@ -345,98 +345,3 @@ def test_hybrid_colour_small_slots(ric, port, slots):
         r = b.stream(i)
         assert r == port.encode_ric(host[i], 9, 0), i
         assert np.array_equal(outs[i].numpy().reshape(-1), port.decode_ric(r)[0].reshape(-1)), i
-
-
-def test_gather_ops_during_coder_launch(ric, port):
-    """The stream gather's device operations complete while a stream coder
-    launch is in flight: once the launch has posted its first
-    streams (ready words) and while its waves still decode -- three coder waves
-    on every SIMD, as in the serving step -- device digests, H2D / D2H copies,
-    a chunk pack and a one-rank RCCL send / receive all finish, and the launch
-    is still running when they have.  Also the rank-0 receive-side cost of one
-    64 MiB chunk of 64 streams (digests + D2H into pinned memory), during the
-    launch and on the idle device (printed)."""
-    import threading
-    import time
-    import shard
-    w, h, n, pool = 2048, 1088, 3072, 1536
-    distinct = 8
-    host = [ric.synth(w, h, 1, 700 + i) for i in range(distinct)]
-    dev = [ric.DeviceArray.from_numpy(x) for x in host]
-    frames = [dev[i % distinct] for i in range(n)]
-    pouts = [ric.DeviceArray((1, h, w), np.uint8) for _ in range(distinct)]
-    outs = [pouts[i % distinct] for i in range(n)]
-    scap = (w * h * 3 // 8 + 65536) // 16 * 16
-    b = ric.Batch(w, h, 1, slots=16, threads=2)
-    b.hybrid_config(pool, scap)
-    words = np.zeros(n, np.uint32)
-    b.set_ready(words, n)
-    sbufs = [np.empty(scap, np.uint8) for _ in range(n)]
-    comm = ric.Comm(ric.Comm.unique_id(), 1, 0, 0)
-    t = shard.RcclTransport(comm, 0)
-    rng = np.random.default_rng(9)
-    chunk = rng.integers(0, 256, 64 << 20, dtype=np.uint8)
-    dchunk = ric.DeviceArray.from_numpy(chunk)
-    back = ric.DeviceArray(1 << 20, np.uint8, zero=True)
-    offs = [i << 20 for i in range(64)]
-    lens = [(1 << 20) - 16 * i for i in range(64)]
-    want = [shard.digest_bytes(chunk[o:o + L]) for o, L in zip(offs, lens)]
-
-    def rank0_chunk():
-        t0 = time.perf_counter()
-        dg = t.digests(dchunk, offs, lens)
-        t1 = time.perf_counter()
-        sink = t.get(dchunk, 0, 64 << 20)
-        t2 = time.perf_counter()
-        assert [int(x) for x in dg] == [int(x) for x in want]
-        assert sink[12345] == chunk[12345]
-        return (t1 - t0) * 1e3, (t2 - t1) * 1e3
-
-    rank0_chunk()                                   # warm (pinned sink, scratch)
-    err = []
-
-    def run():
-        try:
-            b.roundtrip_hybrid(frames, outs, 0, 9, 0, gpu_decode=1, streams=sbufs)
-        except Exception as e:                      # pragma: no cover
-            err.append(e)
-    th = threading.Thread(target=run)
-    t_start = time.perf_counter()
-    th.start()
-    while not words.any():
-        assert th.is_alive(), err
-        time.sleep(0.001)
-    t_first = time.perf_counter() - t_start
-    t0 = time.perf_counter()
-    dg = ric.device_digests(0, dchunk, offs[:4], lens[:4])
-    assert [int(x) for x in dg] == [int(x) for x in want[:4]]
-    t.put(back, 0, chunk[:1 << 20])
-    assert np.array_equal(back.numpy(), chunk[:1 << 20])
-    pk = t.put_many(back, [chunk[:1000], chunk[5000:7000]], [0, 1008])
-    assert [int(x) for x in pk] == [int(shard.digest_bytes(chunk[:1000])), int(shard.digest_bytes(chunk[5000:7000]))]
-    ops_ms = (time.perf_counter() - t0) * 1e3
-    # RCCL: the first send/receive of a launch waits until the launch's first
-    # waves retire (DESIGN §11); the next ones go straight through
-    rccl_ms = []
-    for k in range(2):
-        t1 = time.perf_counter()
-        comm.sendrecv([(0, True, dchunk.data_ptr() + ((k + 1) << 20), 1 << 20), (0, False, back, 1 << 20)])
-        rccl_ms.append((time.perf_counter() - t1) * 1e3)
-        assert np.array_equal(back.numpy(), chunk[(k + 1) << 20:(k + 2) << 20])
-    busy = rank0_chunk()
-    alive = th.is_alive()
-    n_ready = int((words != 0).sum())
-    th.join()
-    assert not err, err
-    total = time.perf_counter() - t_start
-    idle = rank0_chunk()
-    print("\n[gather-ops] launch %.0f ms, first stream ready at %.0f ms, %d of %d ready after the ops; "
-          "digests + copies + pack %.1f ms; RCCL send/receive %.1f ms (first) / %.1f ms (next); "
-          "rank-0 64 MiB chunk (digests ms, D2H ms): in flight %.1f / %.1f, idle %.1f / %.1f"
-          % (total * 1e3, t_first * 1e3, n_ready, n, ops_ms, rccl_ms[0], rccl_ms[1], busy[0], busy[1], idle[0], idle[1]))
-    assert alive, "the coder launch ended before the gather's operations did (ops %.1f ms, RCCL %s)" % (ops_ms, rccl_ms)
-    # none of the side stream's operations waits for the launch
-    assert ops_ms < 100, ops_ms
-    assert rccl_ms[1] < 50, rccl_ms
-    r = b.stream(0)
-    assert r == port.encode_ric(host[0], 9, 0)
