@@ -12,6 +12,7 @@
 // positions are visited by scanning set bits, and a geometric remainder and
 // the sign bit that follows it are read as one (k + 1)-bit chunk (no range
 // decoding happens between them, so the same bytes are read).
+#include <cstdlib>
 #include "entropy.h"
 #include "coder_tables.h"
 
@@ -91,11 +92,15 @@ const HuffLutD kHuffLutD;
 // The decoder's cold state -- the code register (read only by the carry
 // check of a normalisation), the stream limit and the overflow flag -- lives
 // outside the register state, so the hot loop keeps range, low, the raw-bit
-// buffer and the stream pointer in registers.  One decoder runs per thread at
-// a time.
+// buffer and the stream pointer in registers.  The rule this imposes: at most
+// one DecCore per thread between its construction (from Mux::dec_state) and
+// Mux::set_dec_state(d.state()) -- no nested or interleaved decodes on one
+// thread (tree_dec is the only constructor and does not nest).  t_live
+// enforces it: a second construction before state() aborts.
 thread_local uint32_t t_code;
 thread_local const uint8_t* t_limit;
 thread_local bool t_ovf;
+thread_local bool t_live;
 
 struct DecCore {
 	uint32_t range, low, nbits, buffer;
@@ -103,9 +108,11 @@ struct DecCore {
 
 	explicit DecCore(const Mux::DecState& s) : range(s.range), low(s.low), nbits(s.nbits), buffer(s.buffer), p(s.p)
 	{
+		if (t_live) abort();                                    // a nested decode on this thread (above)
+		t_live = true;
 		t_code = s.code; t_limit = s.limit; t_ovf = s.ovf;
 	}
-	Mux::DecState state() const { return {range, low, t_code, nbits, buffer, p, t_limit, t_ovf}; }
+	Mux::DecState state() const { t_live = false; return {range, low, t_code, nbits, buffer, p, t_limit, t_ovf}; }
 
 	RIC_AI uint8_t next()
 	{

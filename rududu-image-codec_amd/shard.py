@@ -197,7 +197,7 @@ class StreamGather:
     A round: every sender still active sends one chunk -- a header (round,
     count, done, payload bytes, then per stream: its index, length and
     digest) and the payload (whole streams back to back at 16-byte offsets,
-    at most `chunk_bytes`, at most MAX_PER_CHUNK streams), as one group -- and
+    at most `chunk_bytes`, at most MAX_PER_CHUNK streams), as two point-to-point operations -- and
     rank 0 receives the headers, then the payloads, checks each stream's
     digest against the sender's, and hands each stream to
     `on_stream(rank, index, bytes)` from its sink buffer.  A sender takes into
@@ -207,10 +207,13 @@ class StreamGather:
     is larger (its header announces the payload's size) grows that buffer.
     """
 
-    def __init__(self, transport, rank, world, chunk_bytes=64 << 20):
+    def __init__(self, transport, rank, world, chunk_bytes=64 << 20, max_chunk=1 << 30):
         self.t = transport
         self.rank, self.world = rank, world
         self.chunk = int(chunk_bytes)
+        # the largest chunk a peer's header may announce (rank 0 grows that
+        # peer's buffer to it; a corrupt header cannot ask for more)
+        self.max_chunk = max(int(max_chunk), self.chunk)
         self.hdr = [self.t.alloc(HDR_WORDS * 8) for _ in range(max(world - 1, 1))]
         if rank == 0:
             self.bufs = [self.t.alloc(self.chunk) for _ in range(world - 1)]
@@ -261,7 +264,11 @@ class StreamGather:
                 hdr[4 + 3 * k], hdr[5 + 3 * k] = i, ln
             hdr[6:6 + 3 * len(take):3] = dg.view(np.int64)
             self.t.put(self.hdr[0], 0, hdr.view(np.uint8))
-            self.t.sendrecv([(0, True, self.hdr[0], HDR_WORDS * 8), (0, True, self.bufs[0], off)])
+            # header and payload as two operations, as rank 0 receives them (it
+            # reads the header on the host in between): the same grouping on
+            # both sides of every RCCL transfer
+            self.t.sendrecv([(0, True, self.hdr[0], HDR_WORDS * 8)])
+            self.t.sendrecv([(0, True, self.bufs[0], off)])
             sent += len(take)
             nbytes += off
             rnd += 1
@@ -288,7 +295,7 @@ class StreamGather:
             heads = {}
             for r in active:
                 h = np.frombuffer(bytes(self.t.get(self.hdr[r - 1], 0, HDR_WORDS * 8)), np.int64).copy()
-                if h[0] != rnd or h[1] > MAX_PER_CHUNK or h[3] < 0:
+                if h[0] != rnd or h[1] > MAX_PER_CHUNK or h[3] < 0 or h[3] > self.max_chunk:
                     raise RuntimeError("gather: bad chunk header from rank %d (round %d): %s" % (r, rnd, h[:4]))
                 if h[3] > self.cap[r - 1]:
                     # a peer with a larger chunk (e.g. gather_streams' per-rank sizes)
@@ -358,7 +365,10 @@ def scatter_streams(per_rank, transport, rank, world):
             transport.put(lb, 0, lens.view(np.uint8))
             pb = transport.alloc(len(payload))
             transport.put(pb, 0, payload)
-            transport.sendrecv([(r, True, cb, 8), (r, True, lb, 8 * len(lst)), (r, True, pb, len(payload))])
+            # one operation per message, as the peer receives them
+            transport.sendrecv([(r, True, cb, 8)])
+            transport.sendrecv([(r, True, lb, 8 * len(lst))])
+            transport.sendrecv([(r, True, pb, len(payload))])
         return list(per_rank[0])
     cb = transport.alloc(8)
     transport.sendrecv([(0, False, cb, 8)])

@@ -255,3 +255,36 @@ def test_gather_big_and_empty_streams_scatter_many_gloo():
     assert [g for g in got] == [out[r][0] for r in range(3)]
     for r in range(3):
         assert out[r][2] == [bytes([r, i % 256]) * (i % 5) for i in range(70 + r)]
+
+
+def test_gather_rejects_oversized_chunk_header():
+    """Rank 0 grows a peer's buffer to the payload size its header announces,
+    up to StreamGather.max_chunk: a corrupt header asking for more is refused
+    before any allocation."""
+    class OneHeader(shard.GlooTransport):
+        def __init__(self, size):
+            super().__init__(None)
+            self.size = size
+            self.allocs = []
+
+        def alloc(self, nbytes):
+            self.allocs.append(int(nbytes))
+            return super().alloc(nbytes)
+
+        def sendrecv(self, ops):
+            for peer, is_send, buf, n in ops:
+                assert not is_send
+                if n == shard.HDR_WORDS * 8:
+                    h = np.zeros(shard.HDR_WORDS, np.int64)
+                    h[1], h[2], h[3] = 0, 1, self.size
+                    buf[:n] = h.view(np.uint8)
+
+    t = OneHeader(3 << 30)
+    g = shard.StreamGather(t, 0, 2, chunk_bytes=1 << 20, max_chunk=1 << 24)
+    with pytest.raises(RuntimeError, match="bad chunk header"):
+        g.receive()
+    assert max(t.allocs) <= 1 << 20
+    ok = OneHeader(1 << 22)                    # within the bound: grown and accepted
+    g = shard.StreamGather(ok, 0, 2, chunk_bytes=1 << 20, max_chunk=1 << 24)
+    g.receive()
+    assert g.cap[0] == 1 << 22
