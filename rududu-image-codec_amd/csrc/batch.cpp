@@ -201,6 +201,8 @@ struct ric_batch {
 	// ric_batch_set_digests: per frame of a call, the digest of its decoded pixels
 	unsigned long long* digest = nullptr;
 	long ndigest = 0;
+	// the fused pixel output's partial digest words (16 per frame of a group)
+	unsigned long long* d_dpart = nullptr;
 	// ric_batch_set_ready: per frame of a call, its .ric file's length once the
 	// file is complete in out[i] (host words the caller polls)
 	uint32_t* ready = nullptr;
@@ -302,12 +304,16 @@ struct ric_batch {
 
 namespace {
 
-// RIC_GC_PRIO: the stream coder waves' issue priority by progress (prio_band, gcoder.hip):
-// 0 one priority, 1 steps at the finest H band of each phase, 2 (default) steps through the decode's finest
-// bands, 3 steps at the decode's finest H and D bands and half-way through D
+// RIC_GC_PRIO: the stream coder waves' issue priority by progress (prio_band, level_step, gcoder.hip):
+// 0 one priority, 1 steps at the finest H band of each phase, 2 steps through the decode's finest
+// bands, 3 steps at the decode's finest H and D bands and half-way through D, 4 (default; the round-trip
+// kernel, else 2's schedule is not applied) by rank among the coder waves of the same SIMD at every chunk,
+// 5 the same ranks one priority lower.
+// Measured (one C3 serving step, 3072 streams): mode 2 11011 ms per launch, the waves ending in three
+// tiers (9.25 / 10.0 / 10.9 s); mode 4 10327 ms, every wave ending within 10.2-10.3 s
 int gc_prio()
 {
-	static const int mode = [] { const char* e = getenv("RIC_GC_PRIO"); return e ? atoi(e) : 2; }();
+	static const int mode = [] { const char* e = getenv("RIC_GC_PRIO"); return e ? atoi(e) : 4; }();
 	return mode;
 }
 
@@ -579,8 +585,27 @@ int h2d_slots(ric_batch* b, int set, int n)
 // (region C) stay in the frame's arena -- no copy of the bands.
 // lo (a compacted pool): level 0's bands are read from the arenas (expanded
 // there from the pool's compact blocks)
+// The pixel output fused into level 0's inverse (a gray 9/7 frame: ZFrames::pix):
+// frames' device pixel buffers, their quantisers, and frames idx0.. of the
+// call for the digests (ric_batch_set_digests)
+struct PixFuse {
+	uint8_t* const* pix;
+	const int* q;
+	long idx0;
+};
+// RIC_PIX_FUSE=0: the separate pixel output kernel after the inverse
+bool pix_fuse_ok(const ric_batch* b, int trans, uint8_t* const* pix, int n)
+{
+	static const bool on = [] { const char* e = getenv("RIC_PIX_FUSE"); return !e || atoi(e) != 0; }();
+	if (!on || b->channels != 1 || trans != CDF97 || (b->w & 3) || b->P.L[0].is_int) return false;
+	for (int i = 0; i < n; i++)
+		if (!pix[i] || ((uintptr_t)pix[i] & 3)) return false;
+	return true;
+}
+
 int gpu_decode_plane(ric_batch* b, int set, int n, int p, const int* qs, int trans, bool h2d = true, int abase = -1,
-                     int amul = 1, uint32_t* yflag = nullptr, char* pool = nullptr, size_t pstr = 0, size_t lo = 0)
+                     int amul = 1, uint32_t* yflag = nullptr, char* pool = nullptr, size_t pstr = 0, size_t lo = 0,
+                     const PixFuse* pf = nullptr)
 {
 	Pyramid& P = b->P;
 	const int s0 = set * b->slots;
@@ -604,8 +629,19 @@ int gpu_decode_plane(ric_batch* b, int set, int n, int p, const int* qs, int tra
 			fr.scratch = b->arena(abase); fr.scstride = ast; fr.split = P.b_end; fr.lo = lo;
 		}
 		int out_int;
+		long ndig = 0;
 		if (l == 0) {
 			fr.out = b->plane(s0, p); fr.ostride = b->pstride; fr.po = b->pitch; out_int = 0;
+			if (pf) {
+				fr.pix = pf->pix; fr.pix_q = pf->q;
+				ndig = b->digest && pf->idx0 >= 0 ? std::max(0L, std::min((long)n, b->ndigest - pf->idx0)) : 0;
+				if (ndig) {
+					if (!b->d_dpart) BCHK(hipMalloc(&b->d_dpart, sizeof(unsigned long long) * 16 * 2 * (size_t)b->slots));
+					if (n > 2 * b->slots) return RIC_E_ARG;
+					BCHK(hipMemsetAsync(b->d_dpart, 0, sizeof(unsigned long long) * 16 * (size_t)n, b->st));
+					fr.dig_part = b->d_dpart;
+				}
+			}
 		} else {
 			const Band& LL = P.L[l - 1].b[BL];
 			fr.out = b->arena(abase) + LL.off; fr.ostride = ast; fr.po = LL.pitch; out_int = LL.is_int;
@@ -623,6 +659,7 @@ int gpu_decode_plane(ric_batch* b, int set, int n, int p, const int* qs, int tra
 		auto si = b->prof.begin(B_INV + std::min(l, 7), n, b->st);
 		if (launch_inv_level_z(L, L.b[BL], fr, out_int, trans, qf.data(), b->zi[set][l], b->st)) return RIC_E_HIP;
 		b->prof.end(si);
+		if (ndig) launch_digest_fold(b->d_dpart, b->digest + pf->idx0, (int)ndig, b->st);
 	}
 	if (yf.lower()) return RIC_E_HIP;
 	BCHK(hipGetLastError());
@@ -968,6 +1005,7 @@ void ric_batch_destroy(ric_batch* b)
 		if (c.d_ts) (void)dev_free(c.d_ts);
 		if (c.h_post) (void)pinned_free(c.h_post);
 		if (c.d_yield) (void)dev_free(c.d_yield);
+		if (b->d_dpart) (void)dev_free(b->d_dpart);
 		if (c.d_pcmp) (void)dev_free(c.d_pcmp);
 		if (c.d_pcnt) (void)dev_free(c.d_pcnt);
 		if (c.d_ptotal) (void)dev_free(c.d_ptotal);
@@ -1132,8 +1170,13 @@ int ric_batch_roundtrip(ric_batch* b, const uint8_t* const* pix, int n, int q, i
 		if (r && r != RIC_E_STREAM) { rc = r; break; }
 		stream_err |= r == RIC_E_STREAM;
 		const int f0 = g * S, m = std::min(S, n - f0), set = g & 1;
-		rc = gpu_decode_plane(b, set, m, 0, qs.data(), trans);
-		if (!rc) rc = gpu_pix_out(b, set, m, qs.data(), pix_out + f0, 1, f0);
+		if (pix_fuse_ok(b, trans, pix_out + f0, m)) {
+			const PixFuse pf{pix_out + f0, qs.data(), f0};
+			rc = gpu_decode_plane(b, set, m, 0, qs.data(), trans, true, -1, 1, nullptr, nullptr, 0, 0, &pf);
+		} else {
+			rc = gpu_decode_plane(b, set, m, 0, qs.data(), trans);
+			if (!rc) rc = gpu_pix_out(b, set, m, qs.data(), pix_out + f0, 1, f0);
+		}
 		if (!rc && launched < G) rc = launch_enc(launched++);
 	}
 	// on an error, the tasks already queued still run: wait for them
@@ -1791,9 +1834,15 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 				if (launch_dcmp_expand(x, gm, b->st)) return bfail(hipGetLastError(), "k_dcmp_expand") ? RIC_E_HIP : RIC_E_HIP;
 				b->prof.end(sx);
 			}
+			const bool fuse = pix_fuse_ok(b, trans, pix_out + f0 + g0, gm);
+			const PixFuse pf{pix_out + f0 + g0, qs.data(), f0 + g0};
 			int r = gpu_decode_plane(b, 0, gm, p, qs.data(), trans, false, -1, 1, nullptr,
-			                         kbase(h, g0) + (size_t)p * c.abstride, c.fstride, c.lo);
+			                         kbase(h, g0) + (size_t)p * c.abstride, c.fstride, c.lo, fuse ? &pf : nullptr);
 			if (r) return r;
+			if (fuse) {
+				hv_done[j][g0 / S] = 1;
+				return RIC_OK;
+			}
 		}
 		const int r = gpu_pix_out(b, 0, gm, qs.data(), pix_out + f0 + g0, 1, f0 + g0);
 		if (r == RIC_OK) hv_done[j][g0 / S] = 1;          // a failed group is not taken for harvested
@@ -2045,14 +2094,17 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 		} else if (trace > 1) {
 			tr("decode group done", F.g.f0);
 		}
-		if (!r2 && C == 1) r2 = gpu_decode_plane(b, F.set, F.g.m, 0, qs.data(), trans, true, -1, 1, yflag);
+		const bool fuse = C == 1 && pix_fuse_ok(b, trans, pix_out + F.g.f0, F.g.m);
+		const PixFuse pf{pix_out + F.g.f0, qs.data(), F.g.f0};
+		if (!r2 && C == 1) r2 = gpu_decode_plane(b, F.set, F.g.m, 0, qs.data(), trans, true, -1, 1, yflag, nullptr, 0, 0,
+		                                         fuse ? &pf : nullptr);
 		if (!r2 && C > 1) {
 			r2 = h2d_slots(b, F.set, C * F.g.m);
 			for (int p = 0; p < C && !r2; p++)
 				r2 = gpu_decode_plane(b, F.set, F.g.m, p, qs.data(), trans, false, F.set * S + p, C, yflag);
 		}
 		if (trace > 2) tr("  inverse issued", F.g.f0);
-		if (!r2) r2 = gpu_pix_out(b, F.set, F.g.m, qs.data(), pix_out + F.g.f0, 1, F.g.f0);
+		if (!r2 && !fuse) r2 = gpu_pix_out(b, F.set, F.g.m, qs.data(), pix_out + F.g.f0, 1, F.g.f0);
 		if (trace > 2) tr("  pix out issued", F.g.f0);
 		if (!r2) BCHK(hipEventRecord(F.ev, b->st));   // the set's mirrors are free once this passes
 		set_busy[F.set] = false;

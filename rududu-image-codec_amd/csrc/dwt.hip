@@ -2035,6 +2035,12 @@ struct InvArgs {
 	int W, H, nseg, ovec, nofast;
 	int quirk_dalign, quirk_halign;   // reference DimXAlign of D and H (5/3 only)
 	int q[4];                   // fused TSUQi multipliers of D, H, V, LL (1 = none)
+	// pixel output fused into a gray frame's level 0 (k_inv_z PIX): instead of
+	// the int16 plane, the u8 pixels (W bytes per row) with ric's unshift +
+	// clip (src/ric/ric.cpp:237-240; q: the frame's quantiser, 0 = lossless),
+	// and the pixels' digest (launch_digest's formula) added into one of the
+	// frame's 16 partial words dig[0..15] (folded by launch_digest_fold)
+	uint8_t* pix; unsigned long long* dig; int pq;
 };
 
 // CBand::TSUQi (src/lib/band.h:94-107) on a loaded band value: v *= (C)q
@@ -2250,9 +2256,34 @@ __device__ __forceinline__ void inv_seg(const InvArgs<TB, TL, TO>& a, int x, int
 	}
 }
 
+// The fused pixel epilogue (InvArgs::pix): row y's 4 values at columns x..x+3
+// -> u8 pixels (k_gray_out8's conversion), and their digest terms
+struct PixAcc { unsigned long long s2; uint32_t s1; };
+__device__ __forceinline__ void pix_put(const InvArgs<int16_t, int16_t, int16_t>& a, int y, int x, uint2 u, PixAcc& acc)
+{
+	const int W = a.W;
+	const int v[4] = {(int16_t)(u.x & 0xffff), (int)u.x >> 16, (int16_t)(u.y & 0xffff), (int)u.y >> 16};
+	uint32_t pk = 0, s = 0, t = 0;
+	FOR4 {
+		int c = a.pq ? (int16_t)(128 + ((v[j] + 8) >> 4)) : (int16_t)(v[j] + 128);
+		c = c < 0 ? 0 : c > 255 ? 255 : c;
+		if (x + j >= W) c = 0;
+		pk |= (uint32_t)c << (8 * j);
+		s += (uint32_t)c;
+		t += (uint32_t)c * (uint32_t)j;
+	}
+	uint8_t* row = a.pix + (long)y * W;
+	if (x + 3 < W) *reinterpret_cast<uint32_t*>(row + x) = pk;
+	else FOR4 if (x + j < W) row[x + j] = (uint8_t)(pk >> (8 * j));
+	acc.s2 += (unsigned long long)((long)y * W + x) * s + t;
+	acc.s1 += s;
+}
+
 // Inverse 9/7 level, short bands -> short plane, packed (same schedule as inv_seg).
-template <int S, bool FAST>
-__device__ __forceinline__ void inv97p_seg(const InvArgs<int16_t, int16_t, int16_t>& a, int x, int lane, int y0)
+// PIX: a gray frame's level 0 with the pixel output fused (InvArgs::pix)
+template <int S, bool FAST, bool PIX = false>
+__device__ __forceinline__ void inv97p_seg(const InvArgs<int16_t, int16_t, int16_t>& a, int x, int lane, int y0,
+                                           PixAcc* acc = nullptr)
 {
 	constexpr bool EDGE = !FAST;
 	const int W = a.W, H = a.H;
@@ -2265,6 +2296,10 @@ __device__ __forceinline__ void inv97p_seg(const InvArgs<int16_t, int16_t, int16
 		PRow r = rw;
 		row_inv97p<EDGE>(r, m);
 		if (!out_lane) return;
+		if constexpr (PIX) {
+			pix_put(a, y, x, prow_to_u2(r), *acc);
+			return;
+		}
 		int16_t* row = a.out + (long)y * a.po;
 		const uint2 u = prow_to_u2(r);
 		if (FAST || (a.ovec && x + 3 < W)) {
@@ -2276,9 +2311,18 @@ __device__ __forceinline__ void inv97p_seg(const InvArgs<int16_t, int16_t, int16
 	};
 	// FAST: rows y, y+1 inverse-lifted together, written through a running pointer
 	int16_t* po = a.out + (long)y0 * a.po + x;
+	int ypo = y0;                                        // (PIX: the row po points at)
 	auto emit_pair = [&](const PRow& rw0, const PRow& rw1) {
 		PRow r0 = rw0, r1 = rw1;
 		row_inv97p2<EDGE>(r0, r1, m);
+		if constexpr (PIX) {
+			if (out_lane) {
+				pix_put(a, ypo, x, prow_to_u2(r0), *acc);
+				pix_put(a, ypo + 1, x, prow_to_u2(r1), *acc);
+			}
+			ypo += 2;
+			return;
+		}
 		if (out_lane) {
 			*reinterpret_cast<uint2*>(po) = prow_to_u2(r0);
 			*reinterpret_cast<uint2*>(po + a.po) = prow_to_u2(r1);
@@ -2428,7 +2472,7 @@ __device__ __forceinline__ void inv97p_seg(const InvArgs<int16_t, int16_t, int16
 	}
 }
 
-template <int TRANS, typename TB, typename TL, typename TO, int S>
+template <int TRANS, typename TB, typename TL, typename TO, int S, bool PIX = false>
 __device__ __forceinline__ void inv_body(const InvArgs<TB, TL, TO>& a)
 {
 	const int lane = threadIdx.x & 63;
@@ -2439,6 +2483,19 @@ __device__ __forceinline__ void inv_body(const InvArgs<TB, TL, TO>& a)
 	const int y0 = seg * S;
 	const bool edge = X0 < 0 || X0 + kLanes * kCols >= a.W;
 	const bool fast = !edge && a.ovec && !a.nofast && y0 >= 16 && y0 + S + 4 < a.H;
+	if constexpr (PIX) {
+		static_assert(TRANS == CDF97 && sizeof(TB) == 2 && sizeof(TO) == 2, "the fused pixel output: 9/7 short levels");
+		PixAcc acc = {0, 0};
+		if (fast) inv97p_seg<S, true, true>(a, x, lane, y0, &acc);
+		else inv97p_seg<S, false, true>(a, x, lane, y0, &acc);
+		// the wave's digest terms: one atomic per wave into one of the frame's
+		// 16 partial words (a single word per frame would take ~8000 atomics)
+		unsigned long long d = acc.s2 * 0x9E3779B97F4A7C15ull + acc.s1;
+#pragma unroll
+		for (int o = 32; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
+		if (lane == 0 && a.dig) atomicAdd(a.dig + ((seg + blockIdx.x) & 15), d);
+		return;
+	}
 	if constexpr (TRANS == CDF97 && sizeof(TB) == 2 && sizeof(TO) == 2) {
 		if (fast) inv97p_seg<S, true>(a, x, lane, y0);
 		else inv97p_seg<S, false>(a, x, lane, y0);
@@ -2450,10 +2507,10 @@ __device__ __forceinline__ void inv_body(const InvArgs<TB, TL, TO>& a)
 
 template <int TRANS, typename TB, typename TL, typename TO, int S>
 __global__ void __launch_bounds__(256) k_inv(InvArgs<TB, TL, TO> a) { inv_body<TRANS, TB, TL, TO, S>(a); }
-template <int TRANS, typename TB, typename TL, typename TO, int S>
+template <int TRANS, typename TB, typename TL, typename TO, int S, bool PIX = false>
 __global__ void __launch_bounds__(256) k_inv_z(const InvArgs<TB, TL, TO>* __restrict__ az)
 {
-	inv_body<TRANS, TB, TL, TO, S>(az[blockIdx.z]);
+	inv_body<TRANS, TB, TL, TO, S, PIX>(az[blockIdx.z]);
 }
 
 // S rows per wave: enough waves to fill the chip on every level, short
@@ -2819,11 +2876,24 @@ template <int TRANS, typename TB, typename TO, int S>
 int inv_launch_z(const Level& L, const Band& lls, const ZFrames& fr, int nz, const int* q, ZArgs& z, hipStream_t st)
 {
 	std::vector<InvArgs<TB, TB, TO>> v(nz);
-	for (int f = 0; f < nz; f++)
+	for (int f = 0; f < nz; f++) {
 		v[f] = inv_args<TB, TO>(L, lls, fr.arena + f * fr.astride, (char*)fr.out + f * fr.ostride, fr.po,
 		                        q ? q + 4 * f : nullptr, S, fr.scratch ? fr.c_base(f) : nullptr, fr.split, fr.lo);
+		if (fr.pix) {
+			v[f].pix = fr.pix[f];
+			v[f].dig = fr.dig_part ? fr.dig_part + 16 * (size_t)f : nullptr;
+			v[f].pq = fr.pix_q[f];
+		}
+	}
 	if (zargs_put(z, v.data(), v.size() * sizeof(v[0]), st)) return -1;
 	const dim3 grid((L.w + kStripValid - 1) / kStripValid, (v[0].nseg + kWavesPerBlock - 1) / kWavesPerBlock, nz);
+	if constexpr (TRANS == CDF97 && sizeof(TB) == 2 && sizeof(TO) == 2) {
+		if (fr.pix) {
+			hipLaunchKernelGGL((k_inv_z<TRANS, TB, TB, TO, S, true>), grid, dim3(256), 0, st, (const InvArgs<TB, TB, TO>*)z.dev);
+			return 0;
+		}
+	}
+	if (fr.pix) return -1;                               // (pix_fusable() refuses these)
 	hipLaunchKernelGGL((k_inv_z<TRANS, TB, TB, TO, S>), grid, dim3(256), 0, st, (const InvArgs<TB, TB, TO>*)z.dev);
 	return 0;
 }

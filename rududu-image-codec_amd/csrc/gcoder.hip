@@ -223,6 +223,52 @@ GC_DI void prio_band(int mode, bool dec, int b, int nb)
 	}
 }
 
+// prio 4: by rank among the coder waves of the same SIMD.  Waves record
+// their progress (chunks of 64 blocks coded, encode then decode) in a device
+// table with one row per SIMD, one word per wave slot; at every chunk a wave
+// reads its SIMD's row and takes priority 3 if no other coder wave of this
+// launch on its SIMD is behind it, 2 if one is, 1 if two are, 0 beyond.  The
+// wave furthest behind always issues first, so the waves of a SIMD finish
+// together instead of one after another by age (modes 1-3 level them only at
+// band steps: a C3 step's 3072 waves ended in three tiers, 9.25 / 10.0 /
+// 10.9 s, the SIMDs holding two, then one wave for the last 1.7 s).
+// Row = XCC_ID, SE, SH, CU, SIMD (13 bits), word = wave slot (4 bits); a word
+// is tag << 20 | progress, the tag being the launch's (12 bits, top bit set),
+// so words left by other launches are ignored and no reset is needed.
+constexpr uint32_t kLevelRows = 1u << 13;
+__device__ uint32_t g_level[kLevelRows * 16];
+// mode 5: the same ranks one priority lower (2, 1, 0), below the level
+// kernels' producer waves (priority 2) that run beside the coder
+__shared__ uint32_t g_lv[3];          // progress, table word, tag << 20 | top priority (0: mode off)
+GC_DI void level_init(int mode, uint32_t tag)
+{
+	if (mode != 4 && mode != 5) { g_lv[2] = 0; return; }
+	const uint32_t hw = __builtin_amdgcn_s_getreg(0xF804), xcc = __builtin_amdgcn_s_getreg(0xF814);
+	const uint32_t row = (xcc & 7u) << 10 | ((hw >> 13) & 7u) << 7 | ((hw >> 12) & 1u) << 6 | ((hw >> 8) & 15u) << 2 |
+	                     ((hw >> 4) & 3u);
+	g_lv[0] = 0;
+	g_lv[1] = row << 4 | (hw & 15u);
+	g_lv[2] = ((tag & 0x7FFu) | 0x800u) << 20 | (mode == 4 ? 3u : 2u);
+}
+GC_DI void level_step(bool last = false)
+{
+	const uint32_t tw = g_lv[2], tg = tw & 0xFFF00000u;
+	if (!tw) return;
+	const uint32_t p = last ? 0xFFFFFu : (g_lv[0] + 1) & 0xFFFFFu;
+	const uint32_t me = g_lv[1], l = lane_id();
+	g_lv[0] = p;
+	if (l == 0) __hip_atomic_store(g_level + me, tg | p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+	if (last) return;
+	uint32_t v = 0;
+	if (l < 16 && l != (me & 15u)) v = __hip_atomic_load(g_level + (me & ~15u) + l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+	const uint32_t behind = (uint32_t)__builtin_popcountll(__ballot((v & 0xFFF00000u) == tg && (v & 0xFFFFFu) < p));
+	const int pr = (int)(tw & 3u) - (int)behind;
+	if (pr >= 3) __builtin_amdgcn_s_setprio(3);
+	else if (pr == 2) __builtin_amdgcn_s_setprio(2);
+	else if (pr == 1) __builtin_amdgcn_s_setprio(1);
+	else __builtin_amdgcn_s_setprio(0);
+}
+
 // Yielding to the level kernels (GEncArgs::yield): while the batch stream
 // runs the host-coded frames' level kernels it raises a flag in device memory;
 // a coder wave that finds it raised at a chunk boundary sleeps (at most ~0.25
@@ -724,6 +770,7 @@ GC_DI void tree_enc(E& e, const GTabs& T, const GBandDesc& B, const char* arena,
 	}
 	for (int s0 = 0; s0 < nblk; s0 += 64) {
 		coder_yield(yield);
+		level_step();
 		const RecChunk rc = rn;
 		RIC_UNROLL
 		for (int g = 0; g < 16; g++) g_coef[g * 64 + l] = cmp ? cn[g] : unpack_coef(cn[g], is_int, half, g);
@@ -858,9 +905,11 @@ __global__ void __launch_bounds__(64) GC_KATTR k_gc_encode(const GEncArgs* __res
 	const int f = blockIdx.x;
 	const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
 	set_prio<3>(a.prio);
+	level_init(a.prio, tag);
 	load_huff();
 	uint32_t end;
 	const uint32_t rc = enc_frame<RING>(a, f, end);
+	level_step(true);
 	if (lane_id() == 0) {
 		gst(a.res)[2 * f] = rc ? 0u : end;               // file length = 9 + (end - 7) - 2
 		gst(a.res)[2 * f + 1] = rc;
@@ -1396,6 +1445,7 @@ GC_DI void tree_dec(GDec& d, const GTabs& T, const GBandDesc& B, const GBandDesc
 	uint32_t cnt_band = 0;                              // (compacted) the band's values so far
 	for (int s0 = 0; s0 < nblk; s0 += 64) {
 		coder_yield(yield);
+		level_step();
 		if (s0 == s_half) set_prio<0>(1);
 		int bx, by;
 		const uint32_t info = block_info(B, P, arena, nblk, s0 + (int)l, bx, by);
@@ -1589,8 +1639,10 @@ __global__ void __launch_bounds__(64) GC_KATTR k_gc_decode(const GDecArgs* __res
 	const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
 	if (a.prio == 1) set_prio<1>(1);
 	else set_prio<3>(a.prio);
+	level_init(a.prio, 0x7FFu);                      // (a finished wave's word reads as ahead of every wave)
 	load_huff();
 	const uint32_t r = dec_frame<ETAB>(a, f, gld(a.lens)[(size_t)f * a.lens_stride]);
+	level_step(true);
 	if (lane_id() == 0) {
 		gst(a.res)[f] = r;
 		if (a.ts) ts_put(a.ts, f, t_start);
@@ -1612,6 +1664,7 @@ __global__ void __launch_bounds__(64) GC_KATTR k_gc_roundtrip(const GEncArgs* __
 	const int f = blockIdx.x;
 	const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
 	set_prio<3>(ea.prio);
+	level_init(ea.prio, tag);
 	load_huff();
 	uint32_t end;
 	const uint32_t rc = enc_frame<4096>(ea, f, end);
@@ -1640,6 +1693,7 @@ __global__ void __launch_bounds__(64) GC_KATTR k_gc_roundtrip(const GEncArgs* __
 		if (lane_id() == 0)
 			__hip_atomic_store(posted_dec + f, (rc ? 0x80u : (r & 0x7Fu)) | 0x100u | tag << 12, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 	}
+	level_step(true);                                     // (done: behind no one)
 }
 }  // namespace
 

@@ -327,6 +327,22 @@ void launch_digests(const uint8_t* base, const size_t* off, const size_t* len, i
 	hipLaunchKernelGGL(k_digests, dim3((unsigned)gx, (unsigned)n), dim3(256), 0, st, r, out);
 }
 
+__global__ void k_digest_fold(const unsigned long long* __restrict__ part, unsigned long long* __restrict__ out, int n)
+{
+	const int i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= n) return;
+	unsigned long long s = 0;
+#pragma unroll
+	for (int k = 0; k < 16; k++) s += part[16 * (size_t)i + k];
+	out[i] = s;
+}
+
+void launch_digest_fold(const unsigned long long* part, unsigned long long* out, int n, hipStream_t st)
+{
+	if (n <= 0) return;
+	hipLaunchKernelGGL(k_digest_fold, dim3((n + 63) / 64), dim3(64), 0, st, part, out, n);
+}
+
 void launch_digest(const uint8_t* p, size_t n, unsigned long long* out, hipStream_t st)
 {
 	if (!n) return;

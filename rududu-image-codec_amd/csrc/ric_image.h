@@ -19,4 +19,7 @@ void launch_digest(const uint8_t* p, size_t n, unsigned long long* out, hipStrea
 // launch, run i's digest to out[i] (written, not added)
 constexpr int kDigestRuns = 64;
 void launch_digests(const uint8_t* base, const size_t* off, const size_t* len, int n, unsigned long long* out, hipStream_t st);
+// out[i] = the sum of part[16 i .. 16 i + 15] for i < n (the fused pixel
+// output's 16 partial digest words per frame: launch_inv_level_z)
+void launch_digest_fold(const unsigned long long* part, unsigned long long* out, int n, hipStream_t st);
 }  // namespace ric

@@ -115,6 +115,14 @@ struct ZFrames {
 	// holds them compacted, not at their pyramid offsets
 	size_t lo = 0;
 	char* c_base(int f) const { return scratch ? scratch + (size_t)f * scstride : arena + (size_t)f * astride; }
+	// level 0 of a gray 9/7 decode (launch_inv_level_z): the pixel output
+	// fused -- frame f's u8 pixels to pix[f] (w bytes per row, 4-byte aligned,
+	// w a multiple of 4), unshifted with quantiser pix_q[f]; dig_part (or
+	// null): 16 partial digest words per frame (zeroed first), folded by
+	// launch_digest_fold.  The int16 plane (out) is not written.
+	uint8_t* const* pix = nullptr;
+	const int* pix_q = nullptr;
+	unsigned long long* dig_part = nullptr;
 };
 // Per-frame argument array of one batched launch, on the device; re-uploaded
 // (after a stream sync) only when it changes.
