@@ -553,10 +553,35 @@ def main():
     # the warmup steps' gather statistics are not the timed ones
     gstats.update(rounds=0, streams=0, bytes=0, digest_mismatches=0, tail_ms=[])
     barrier()
+    # the host share follows each step's own timeline (auto split): the next
+    # step's host round trips are set so that the host side ends RIC_BENCH_MARGIN
+    # ms (default 60) before the GPU side did in this step.  The warmup's
+    # estimate alone left the two sides +-1 % apart from step to step.
+    margin = float(os.environ.get("RIC_BENCH_MARGIN", "60"))
+    per_step = []
+
+    def rebalance():
+        nonlocal n_host, nstep
+        th, tg = b.hybrid_times()
+        nh = n_host
+        if th > 0 and tg > 0 and n_host > 0:
+            t_eff = th / (n_host / threads)           # host wall ms per round trip per thread, this step
+            want = threads * (tg - margin) / t_eff
+            nh = int(round(0.5 * n_host + 0.5 * want))
+            nh = max(threads, min(nh, host_frames_room(a, threads), nfr - n_gpu))
+        nh = int(allreduce(nh, "min"))
+        n_host = nh
+        nstep = n_host + n_gpu
+
     dsync()
     t0 = time.perf_counter()
+    frames_timed = 0
     for i in range(a.steps):
         step()
+        frames_timed += nstep
+        per_step.append(nstep)
+        if auto and i + 1 < a.steps:
+            rebalance()
         progress("step %d/%d" % (i + 1, a.steps))
     dsync()
     dt = time.perf_counter() - t0
@@ -773,9 +798,9 @@ def main():
         split = {"encode_mpix_s": round(mpx / te, 2), "decode_mpix_s": round(mpx / td, 2),
                  "note": "rank 0, %d frames in groups of %d, groups not pipelined" % (nfr, slots)}
 
-    total_px = nstep * W * H
+    total_px = frames_timed * W * H                 # every timed step's frames (the auto split varies them)
     sum_px = allreduce(total_px, "sum")
-    value = sum_px * a.steps / 1e6 / dt
+    value = sum_px / 1e6 / dt
     wl = {"C3": "C3: 7680x4320 gray, 5-level cdf97, q=%d, .ric encode+decode round trip, bit-exact" % a.q,
           "C5": "C5: %d x 4096x4096 gray frames per step, 5-level cdf97, q=%d, encode+decode, frame f on rank f mod N"
                 % (a.frames or a.batch or 64, a.q),
@@ -802,7 +827,8 @@ def main():
         "vs_baseline": None,
         "dtype": "int16",
         "data": "synthetic (SURVEY.md §8(d) generator), resident in HBM",
-        "config": {"workload": wl, "frames_per_gpu_per_step": nstep, "frames_per_launch": slots,
+        "config": {"workload": wl, "frames_per_gpu_per_step": (nstep if len(set(per_step)) <= 1 else round(frames_timed / a.steps, 2)),
+                   "frames_per_step_timed": per_step, "frames_per_launch": slots,
                    "host_coder_threads_per_gpu": threads, "parallelism": "frames sharded over %d GPU(s)" % world,
                    "coder": ("GPU stream coder (one wave per stream, %d streams per launch): encode%s of %d of %d "
                              "frames; host threads: %s" % (b.cp_pool, {0: "", 1: " and decode", 2: " (and decode of the "

@@ -2742,26 +2742,58 @@ void launch_inv_level(const Level& L, const Band& lls, char* arena, void* out, l
 // in a device array (ZArgs) that is only re-uploaded when it changes.
 int zargs_put(ZArgs& z, const void* data, size_t bytes, hipStream_t st)
 {
-	if (z.img.size() == bytes && memcmp(z.img.data(), data, bytes) == 0) return 0;
-	// the previous image may still be read by queued launches or copied from
-	if (hipStreamSynchronize(st) != hipSuccess) return -1;
-	if (z.cap < bytes) {
-		if (z.dev && dev_free(z.dev) != hipSuccess) return -1;
-		z.dev = nullptr;
-		z.cap = 0;
-		if (hipMalloc(&z.dev, bytes) != hipSuccess) return -1;
-		z.cap = bytes;
+	if (z.cur >= 0 && z.img.size() == bytes && memcmp(z.img.data(), data, bytes) == 0) {
+		if (z.st != st) {                            // (launches on another stream from here on: stream order)
+			if (hipEventRecord(z.ev[z.cur], z.st) != hipSuccess || hipStreamWaitEvent(st, z.ev[z.cur], 0) != hipSuccess) return -1;
+			z.st = st;
+		}
+		return 0;
 	}
+	if (z.cap < bytes) {
+		// growth (rare: a larger group): every slot idle first
+		if (z.st && hipStreamSynchronize(z.st) != hipSuccess) return -1;
+		if (st && hipStreamSynchronize(st) != hipSuccess) return -1;
+		if (z.dbase && dev_free(z.dbase) != hipSuccess) return -1;
+		if (z.hbase && pinned_free(z.hbase) != hipSuccess) return -1;
+		z.dbase = z.hbase = nullptr;
+		z.cap = 0;
+		z.cur = -1;
+		const size_t c = (bytes + 255) & ~(size_t)255;
+		if (hipMalloc(&z.dbase, c * ZArgs::kRing) != hipSuccess) return -1;
+		if (hipHostMalloc(&z.hbase, c * ZArgs::kRing, 0) != hipSuccess) return -1;
+		for (int k = 0; k < ZArgs::kRing; k++) {
+			if (!z.ev[k] && hipEventCreateWithFlags(&z.ev[k], hipEventDisableTiming) != hipSuccess) return -1;
+			z.evset[k] = false;
+		}
+		z.cap = c;
+	}
+	// the current slot's launches are all queued: its event follows them
+	if (z.cur >= 0) {
+		if (hipEventRecord(z.ev[z.cur], z.st) != hipSuccess) return -1;
+		z.evset[z.cur] = true;
+	}
+	const int k = (z.cur + 1) % ZArgs::kRing;
+	if (z.evset[k] && hipEventSynchronize(z.ev[k]) != hipSuccess) return -1;
+	z.evset[k] = false;
+	char* h = z.hbase + (size_t)k * z.cap;
+	char* d = z.dbase + (size_t)k * z.cap;
+	memcpy(h, data, bytes);
+	if (hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, st) != hipSuccess) return -1;
 	z.img.assign((const char*)data, (const char*)data + bytes);
-	return hipMemcpyAsync(z.dev, z.img.data(), bytes, hipMemcpyHostToDevice, st) == hipSuccess ? 0 : -1;
+	z.cur = k;
+	z.st = st;
+	z.dev = d;
+	return 0;
 }
 
 void zargs_free(ZArgs& z)
 {
-	if (z.dev) (void)dev_free(z.dev);
-	z.dev = nullptr;
-	z.cap = 0;
-	z.img.clear();
+	if (z.st) (void)hipStreamSynchronize(z.st);
+	if (z.dbase) (void)dev_free(z.dbase);
+	if (z.hbase) (void)pinned_free(z.hbase);
+	for (int k = 0; k < ZArgs::kRing; k++)
+		if (z.ev[k]) (void)hipEventDestroy(z.ev[k]);
+	z = ZArgs();
 }
 
 namespace {

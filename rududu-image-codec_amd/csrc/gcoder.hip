@@ -250,6 +250,35 @@ GC_DI void level_init(int mode, uint32_t tag)
 	g_lv[1] = row << 4 | (hw & 15u);
 	g_lv[2] = ((tag & 0x7FFu) | 0x800u) << 20 | (mode == 4 ? 3u : 2u);
 }
+// the table word of this wave posted (its progress advanced by a chunk) and
+// its SIMD's row loaded: the row is used at the next chunk (level_apply), so
+// the load's round trip overlaps the chunk's coding
+GC_DI uint32_t level_post()
+{
+	const uint32_t tw = g_lv[2], tg = tw & 0xFFF00000u;
+	if (!tw) return 0u;
+	const uint32_t p = (g_lv[0] + 1) & 0xFFFFFu;
+	const uint32_t me = g_lv[1], l = lane_id();
+	g_lv[0] = p;
+	if (l == 0) __hip_atomic_store(g_level + me, tg | p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+	uint32_t v = 0;
+	if (l < 16 && l != (me & 15u)) v = __hip_atomic_load(g_level + (me & ~15u) + l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+	return v;
+}
+// the priority from the row loaded at the last level_post, against the
+// progress posted with it
+GC_DI void level_apply(uint32_t v)
+{
+	const uint32_t tw = g_lv[2], tg = tw & 0xFFF00000u;
+	if (!tw) return;
+	const uint32_t p = g_lv[0];
+	const uint32_t behind = (uint32_t)__builtin_popcountll(__ballot((v & 0xFFF00000u) == tg && (v & 0xFFFFFu) < p));
+	const int pr = (int)(tw & 3u) - (int)behind;
+	if (pr >= 3) __builtin_amdgcn_s_setprio(3);
+	else if (pr == 2) __builtin_amdgcn_s_setprio(2);
+	else if (pr == 1) __builtin_amdgcn_s_setprio(1);
+	else __builtin_amdgcn_s_setprio(0);
+}
 GC_DI void level_step(bool last = false)
 {
 	const uint32_t tw = g_lv[2], tg = tw & 0xFFF00000u;
@@ -285,6 +314,34 @@ GC_DI void coder_yield(const uint32_t* flag)
 	for (int n = 0; n < 64 && __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); n++)
 		__builtin_amdgcn_s_sleep(127);
 }
+
+// A band walk's per-chunk synchronisation -- the yield flag and the level
+// table -- loaded one chunk ahead (RIC_GC_SYNC_AHEAD, default on): the loads
+// issued at chunk c are consumed at chunk c + 1, so their round trip overlaps
+// the chunk's coding instead of stalling the wave at every chunk start.  A
+// flag seen raised is then polled until it falls (coder_yield).
+#ifndef RIC_GC_SYNC_AHEAD
+#define RIC_GC_SYNC_AHEAD 1
+#endif
+struct ChunkSync {
+	uint32_t yv = 0, lv = 0;
+	bool have = false;
+	GC_DI void step(const uint32_t* yield)
+	{
+#if RIC_GC_SYNC_AHEAD
+		if (have) {
+			if (yv) coder_yield(yield);
+			level_apply(lv);
+		}
+		yv = yield ? __hip_atomic_load(yield, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+		lv = level_post();
+		have = true;
+#else
+		coder_yield(yield);
+		level_step();
+#endif
+	}
+};
 
 // diagnostics (GEncArgs::ts): the wave's start and end (s_memrealtime, 100
 // MHz), and where it ran: HW_ID (wave, SIMD, CU, SE) | XCC_ID << 32
@@ -768,9 +825,9 @@ GC_DI void tree_enc(E& e, const GTabs& T, const GBandDesc& B, const char* arena,
 		RIC_UNROLL
 		for (int g = 0; g < 16; g++) cn[g] = fetch_group(band, is_int, st, dx, dy, nblk, 4 * g, g, half);
 	}
+	ChunkSync cs;
 	for (int s0 = 0; s0 < nblk; s0 += 64) {
-		coder_yield(yield);
-		level_step();
+		cs.step(yield);
 		const RecChunk rc = rn;
 		RIC_UNROLL
 		for (int g = 0; g < 16; g++) g_coef[g * 64 + l] = cmp ? cn[g] : unpack_coef(cn[g], is_int, half, g);
@@ -1443,9 +1500,9 @@ GC_DI void tree_dec(GDec& d, const GTabs& T, const GBandDesc& B, const GBandDesc
 	const uint32_t lmax = is_int ? (1u << 20) : (1u << 15);
 	const int s_half = prio_half ? (nblk / 2) & ~63 : -1;
 	uint32_t cnt_band = 0;                              // (compacted) the band's values so far
+	ChunkSync csy;
 	for (int s0 = 0; s0 < nblk; s0 += 64) {
-		coder_yield(yield);
-		level_step();
+		csy.step(yield);
 		if (s0 == s_half) set_prio<0>(1);
 		int bx, by;
 		const uint32_t info = block_info(B, P, arena, nblk, s0 + (int)l, bx, by);

@@ -124,11 +124,24 @@ struct ZFrames {
 	const int* pix_q = nullptr;
 	unsigned long long* dig_part = nullptr;
 };
-// Per-frame argument array of one batched launch, on the device; re-uploaded
-// (after a stream sync) only when it changes.
+// Per-frame argument array of one batched launch, on the device; uploaded
+// only when it changes.  A ring of kRing device / pinned host slots: a new
+// image goes to the next slot by an async copy in stream order, so an upload
+// never waits for the kernels still reading the previous images (round 5
+// synchronised the stream before every upload: the batch stream's host thread
+// then waited out each level launch of the step's front, ~1000 per step, with
+// the GPU idle while it issued the next).  A slot is reused once the event
+// recorded after its last launch has passed (kRing uploads later: at once).
 struct ZArgs {
-	void* dev = nullptr;
+	static constexpr int kRing = 8;
+	void* dev = nullptr;             // the current image's slot (the launches' argument)
+	char* dbase = nullptr;           // kRing slots of cap bytes
+	char* hbase = nullptr;           // pinned staging, the same
 	size_t cap = 0;
+	int cur = -1;
+	hipStream_t st = nullptr;        // the stream of the current slot's launches
+	hipEvent_t ev[kRing] = {};
+	bool evset[kRing] = {};
 	std::vector<char> img;
 };
 int zargs_put(ZArgs& z, const void* data, size_t bytes, hipStream_t st);
