@@ -1605,6 +1605,18 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 	};
 	int host_groups_done = 0;
 	b->hyb_host_ms = b->hyb_gpu_ms = 0;
+	// the GPU side's end: the coder frames' last harvest kernel, timed on the
+	// batch stream from the call's start (the host side's end is host time)
+	struct EvPair {
+		hipEvent_t a = nullptr, b = nullptr;
+		~EvPair() { if (a) (void)hipEventDestroy(a); if (b) (void)hipEventDestroy(b); }
+	} evt;
+	hipEvent_t& ev_t0 = evt.a;
+	hipEvent_t& ev_t1 = evt.b;
+	bool t1_set = false;
+	BCHK(hipEventCreate(&ev_t0));
+	BCHK(hipEventCreate(&ev_t1));
+	BCHK(hipEventRecord(ev_t0, b->st));
 	b->hyb_fallback = 0;
 	std::deque<HGroup> ready_host, ready_dec;
 	for (int f0 = 0; f0 < n_host; f0 += SG) ready_host.push_back({f0, std::min(SG, n_host - f0), false, 0, 0});
@@ -2136,6 +2148,7 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 				tr("decoded", finished);
 				rc = harvest(finished);
 				finished++;
+				if (rc == RIC_OK && finished == nbatch) t1_set = hipEventRecord(ev_t1, b->st) == hipSuccess;
 				if (rc) break;
 			} else if (e != hipErrorNotReady) {
 				rc = bfail(e, "coder stream") ? RIC_E_HIP : RIC_E_HIP;
@@ -2204,6 +2217,10 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 	for (int h = 0; h < 2; h++)
 		if (c.st[h]) (void)hipStreamSynchronize(c.st[h]);
 	const bool ok = !bfail(hipStreamSynchronize(b->st), "hipStreamSynchronize");
+	if (ok && t1_set) {
+		float ms = 0;
+		if (hipEventElapsedTime(&ms, ev_t0, ev_t1) == hipSuccess) b->hyb_gpu_ms = ms;
+	}
 	b->hyb_fallback = n_fallback;
 	if (trace)
 		fprintf(stderr, "[hybrid] %d coder-frame groups harvested while the launch ran; %d frames left to the host "

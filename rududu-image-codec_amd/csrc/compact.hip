@@ -278,13 +278,20 @@ __global__ __launch_bounds__(64 * kCmpWaves) __attribute__((amdgpu_waves_per_eu(
 // the decode side: one wave per chunk of 64 blocks (flattened over the three
 // bands), every position of each block written, a value where its mask bit is
 // set.  The chunk's values are contiguous (its offset to the next chunk's, or
-// the band's count): the wave loads them into LDS with consecutive lanes on
-// consecutive values while its masks arrive, then each lane assembles its
-// block's rows and writes each as one 8-byte word (a narrow edge block value
-// by value).  The next chunk's masks and offsets are loaded ahead.
+// the band's count).  A wave loads the next chunk's masks, offsets and values
+// while it writes the current one: the values as 16-byte words (the chunk's
+// run rounded out to 16-byte boundaries, at most 3 words a lane), staged in
+// LDS at the chunk's start; then each lane assembles its block's rows and
+// writes each as one 8-byte word (a narrow edge block value by value).
+// (Round 5 loaded a chunk's values 2 bytes a lane once the chunk started:
+// 23 us per C3 frame alone, 0.44 of HBM peak.)
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+constexpr int kDcmpW = 3;                 // 16-byte value words per lane: 3 x 64 x 8 >= 1024 + 14 values
 struct DcmpChunk {
 	uint32_t m;                      // the lane's block mask (loaded)
 	uint32_t o0, tot;                // the chunk's first value and count
+	uint32_t a0;                     // o0 rounded down to 8 values (16 bytes)
+	u32x4 w[kDcmpW];                 // values a0 + 8 (lane + 64 i) .. + 7
 	int b, s;
 };
 
@@ -301,32 +308,47 @@ __device__ __forceinline__ void dcmp_load(const DcmpArgs& a, const char* in, int
 	L.o0 = vbase + coff[ch];
 	L.tot = (ch + 1 < a.chunk0[b + 1] - a.chunk0[b] ? coff[ch + 1] : nval[b]) - coff[ch];
 	L.m = s < a.nblk[b] ? gp((const uint16_t*)(in + a.mask_off[b]))[s] : 0u;
+	// the value words: none past the pool's capacity (a frame the coder left
+	// to the host holds no valid offsets; the capacity's block is rounded up
+	// to 256 bytes, so a word ending past vcap but below vcap rounded to 8 is
+	// inside it)
+	L.a0 = L.o0 & ~7u;
+	const uint32_t tot = L.tot < 1024u ? L.tot : 1024u;
+	const uint32_t nw = (L.o0 + tot - L.a0 + 7u) >> 3;
+	const uint32_t lim = a.vcap ? ((a.vcap + 7u) >> 3) : 0xFFFFFFFFu;
+	const u32x4* vw = (const u32x4*)(in + a.vals_off);
+#pragma unroll
+	for (int i = 0; i < kDcmpW; i++) {
+		const uint32_t j = (uint32_t)lane64() + 64u * (uint32_t)i;
+		const uint32_t wi = (L.a0 >> 3) + j;
+		u32x4 v = {0, 0, 0, 0};
+		if (j < nw && wi < lim) v = *gp(vw + wi);
+		L.w[i] = v;
+	}
 }
 
 __global__ __launch_bounds__(64 * kCmpWaves) void k_dcmp_expand(DcmpArgs a)
 {
 	const int f = blockIdx.z;
 	const char* in = a.in + (size_t)f * a.istride;
-	const int16_t* vals = (const int16_t*)(in + a.vals_off);
-	__shared__ int16_t stage[kCmpWaves][64 * 16];
-	int16_t* sv = stage[threadIdx.x >> 6];
+	__shared__ u32x4 stage[kCmpWaves][64 * kDcmpW];
+	int16_t* sv = (int16_t*)stage[threadIdx.x >> 6];
 	const int l = lane64();
 	int c = wave_gid();
 	DcmpChunk cur, nxt;
 	if (c < a.chunk0[3]) dcmp_load(a, in, c, cur);
 	for (; c < a.chunk0[3]; c += wave_count()) {
-		// the chunk's values into LDS (at most 1024; a value past the pool's
-		// capacity reads as 0 -- a frame the coder left to the host)
-		const uint32_t tot = cur.tot < 1024u ? cur.tot : 1024u;
-		for (uint32_t i = (uint32_t)l; i < tot; i += 64) {
-			const uint32_t o = cur.o0 + i;
-			sv[i] = (!a.vcap || o < a.vcap) ? gp(vals)[o] : (int16_t)0;
-		}
+		// the chunk's value words into LDS
+#pragma unroll
+		for (int i = 0; i < kDcmpW; i++) ((u32x4*)sv)[l + 64 * i] = cur.w[i];
 		const int cn = c + wave_count();
 		if (cn < a.chunk0[3]) dcmp_load(a, in, cn, nxt);
 		const uint32_t m = cur.m;
 		uint32_t ptot;
+		// value k of the chunk is sv[sh + k]; past the capacity it reads as 0
+		const uint32_t sh = cur.o0 - cur.a0;
 		uint32_t k = wave_prefix5((uint32_t)__popc(m), ptot);
+		const uint32_t kcap = a.vcap ? (a.vcap > cur.o0 ? a.vcap - cur.o0 : 0u) : 0xFFFFFFFFu;
 		__builtin_amdgcn_wave_barrier();
 		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 		const int b = cur.b, s = cur.s;
@@ -335,6 +357,7 @@ __global__ __launch_bounds__(64 * kCmpWaves) void k_dcmp_expand(DcmpArgs a)
 		if (s < a.nblk[b]) {
 			const int w = a.dx[b] - bx * 4 < 4 ? a.dx[b] - bx * 4 : 4, h = a.dy[b] - by * 4 < 4 ? a.dy[b] - by * 4 : 4;
 			int16_t* band = (int16_t*)(a.arena + (size_t)f * a.astride + a.off[b]) + (long)by * 4 * a.pitch[b] + bx * 4;
+			auto val = [&](uint32_t kk) -> uint32_t { return kk < kcap && kk < 1024u ? (uint16_t)sv[sh + kk] : 0u; };
 			if (w == 4 && h == 4) {
 				// straight through the 16 positions: a kept position takes the
 				// lane's next value, the others read a slot and drop it
@@ -344,7 +367,7 @@ __global__ __launch_bounds__(64 * kCmpWaves) void k_dcmp_expand(DcmpArgs a)
 #pragma unroll
 					for (int q = 0; q < 4; q++) {
 						const uint32_t bit = (m >> (4 * r + q)) & 1u;
-						const uint32_t v = (uint16_t)sv[bit ? k : 0u];
+						const uint32_t v = val(bit ? k : 0u);
 						word |= (uint64_t)(bit ? v : 0u) << (16 * q);
 						k += bit;
 					}
@@ -356,7 +379,7 @@ __global__ __launch_bounds__(64 * kCmpWaves) void k_dcmp_expand(DcmpArgs a)
 				for (int r = 0; r < h; r++) {
 					uint64_t word = 0;
 					for (int q = 0; q < w; q++, mm >>= 1)
-						if (mm & 1u) word |= (uint64_t)(uint16_t)sv[k++] << (16 * q);
+						if (mm & 1u) word |= (uint64_t)val(k++) << (16 * q);
 					if (w == 4) *gp((uint64_t*)(band + (long)r * a.pitch[b])) = word;
 					else
 						for (int q = 0; q < w; q++) gp(band)[(long)r * a.pitch[b] + q] = (int16_t)(word >> (16 * q));
