@@ -343,15 +343,18 @@ struct YieldFlag {
 	~YieldFlag() { (void)lower(); }
 };
 
-// RIC_GC_YIELD 2 (the default): the coder waves yield only around the host
-// frames' forward level 0, not around their other levels and inverse levels
-// (those run beside the coder waves unpaused); 1: around all of them; 0:
-// never.  C3 step, 3072 coder streams (profiles/r04_yield_ab.json): 1 10491,
-// 2 10561-10576, 0 10624 Mpix/s, with level 0 in the step at 0.35 / 0.34 /
-// 0.25 of HBM peak.
+// RIC_GC_YIELD 1 (the default since round 6): the coder waves yield around
+// every level kernel of the host frames (forward and inverse); 2: only around
+// their forward level 0 (the others run beside the coder waves unpaused); 0:
+// never.  Round 4 (profiles/r04_yield_ab.json): 1 10491, 2 10561-10576, 0
+// 10624 Mpix/s.  Round 6, with the waves levelled by rank (gcoder.hip mode 4)
+// and the yield flag read a chunk ahead, same box, 4 timed steps each
+// (profiles/r06_yield_ab.txt): 1 11,922-11,947 Mpix/s with the whole encode
+// in the step at 0.396 of HBM peak; 2 11,745-11,947 at 0.363; 0 11,928-11,933
+// at 0.342.
 bool yield_level0_only()
 {
-	static const bool v = [] { const char* e = getenv("RIC_GC_YIELD"); return !e || atoi(e) == 2; }();
+	static const bool v = [] { const char* e = getenv("RIC_GC_YIELD"); return e && atoi(e) == 2; }();
 	return v;
 }
 
