@@ -203,6 +203,10 @@ struct ric_batch {
 	long ndigest = 0;
 	// the fused pixel output's partial digest words (16 per frame of a group)
 	unsigned long long* d_dpart = nullptr;
+	// the step's front: a host group's band copies on a stream of their own
+	// (xst), after the batch stream's compaction (ev_fork)
+	hipStream_t xst = nullptr;
+	hipEvent_t ev_fork = nullptr;
 	// ric_batch_set_ready: per frame of a call, its .ric file's length once the
 	// file is complete in out[i] (host words the caller polls)
 	uint32_t* ready = nullptr;
@@ -370,7 +374,7 @@ int lambda_of(int q, int p) { return q ? quants(q + 13 + (p ? 8 : 0)) : 0; }
 // frames keeps a frame's three plane pyramids side by side (amul 3).
 // yflag: the GPU stream coder's yield flag (coder_yield, gcoder.hip), raised
 // around the level kernels only (not the copies), or null
-int d2h_slots(ric_batch* b, int set, int n);
+int d2h_slots(ric_batch* b, int set, int n, hipStream_t cst = nullptr);
 
 // pool (the GPU stream coder's pool, pstr bytes per frame): regions A and B
 // of frame i go to pool + i * pstr instead of its arena -- written there by
@@ -484,10 +488,21 @@ int gpu_encode_plane(ric_batch* b, int set, int n, int p, const uint8_t* const* 
 // levels) to the host mirrors: the compacted 16-bit values and the dense rest
 // (or the dense arenas).  Colour frames of a hybrid host group take C slots
 // each (plane p of frame i in slot C i + p), so n counts slots, not frames.
-int d2h_slots(ric_batch* b, int set, int n)
+// cst (or null: the batch stream): the stream of the copies (the compaction
+// kernels stay on the batch stream; cst waits for them) -- the step's front
+// puts its second host group's copies beside the pool's forward levels
+int d2h_slots(ric_batch* b, int set, int n, hipStream_t cst)
 {
 	Pyramid& P = b->P;
 	const int s0 = set * b->slots;
+	hipStream_t xs = cst ? cst : b->st;
+	auto fork = [&]() -> int {
+		if (xs == b->st) return RIC_OK;
+		if (!b->ev_fork) BCHK(hipEventCreateWithFlags(&b->ev_fork, hipEventDisableTiming));
+		BCHK(hipEventRecord(b->ev_fork, b->st));
+		BCHK(hipStreamWaitEvent(xs, b->ev_fork, 0));
+		return RIC_OK;
+	};
 	if (b->compact) {
 		// the 16-bit bands' values in walk order (compact.hip), written by a
 		// kernel into the head of each frame's host mirror (only the values,
@@ -499,9 +514,10 @@ int d2h_slots(ric_batch* b, int set, int n)
 			if (launch_compact(b->d_cmp_args + set, b->cmp_nchunk, n, b->st)) return bfail(hipGetLastError(), "compact") ? RIC_E_HIP : RIC_E_HIP;
 			b->prof.end(sc);
 		}
-		BCHK(hipMemcpyAsync(b->h_cmp_total + s0, b->d_cmp_total + s0, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, b->st));
+		if (int r = fork()) return r;
+		BCHK(hipMemcpyAsync(b->h_cmp_total + s0, b->d_cmp_total + s0, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, xs));
 		{
-			auto sv = b->prof.begin(B_D2HV, n, b->st);
+			auto sv = b->prof.begin(B_D2HV, n, xs);
 			// In the serving step (cmp_dma): the values' whole capacity by the
 			// copy engine -- about twice the bytes of the values, but no CUs
 			// taken from the stream coder's launch: a kernel writing each frame's
@@ -511,23 +527,24 @@ int d2h_slots(ric_batch* b, int set, int n)
 			// (only the values cross PCIe).  RIC_CMP_DMA=0/1 forces either.
 			static const int dma_env = [] { const char* e = getenv("RIC_CMP_DMA"); return e ? atoi(e) : -1; }();
 			const bool dma = dma_env >= 0 ? dma_env != 0 : b->cmp_dma;
-			if (dma) {
+			if (dma || xs != b->st) {
 				BCHK(hipMemcpy2DAsync(b->harena(s0), b->hstride, b->d_cmp + (size_t)s0 * b->cmp_stride, b->cmp_stride,
-				                      std::min(b->cmp_stride, b->hstride), n, hipMemcpyDeviceToHost, b->st));
+				                      std::min(b->cmp_stride, b->hstride), n, hipMemcpyDeviceToHost, xs));
 			} else if (launch_cmp_to_host(b->d_cmp + (size_t)s0 * b->cmp_stride, b->cmp_stride, b->h_arena_dev + (size_t)s0 * b->hstride,
 			                              b->hstride, b->d_cmp_total + s0, n, b->st))
 				return bfail(hipGetLastError(), "compact to host") ? RIC_E_HIP : RIC_E_HIP;
 			b->prof.end(sv);
 		}
-		auto sp = b->prof.begin(B_D2H, n, b->st);
+		auto sp = b->prof.begin(B_D2H, n, xs);
 		BCHK(hipMemcpy2DAsync(b->harena(s0) + b->cmp_dense, b->hstride, b->arena(s0) + b->cmp_dense, b->astride,
-		                      P.b_end - b->cmp_dense, n, hipMemcpyDeviceToHost, b->st));
+		                      P.b_end - b->cmp_dense, n, hipMemcpyDeviceToHost, xs));
 		b->prof.end(sp);
 		for (int i = 0; i < n; i++) b->cmp_ok[s0 + i] = 1;
 		return RIC_OK;
 	}
-	auto sp = b->prof.begin(B_D2H, n, b->st);
-	BCHK(hipMemcpy2DAsync(b->harena(s0), b->hstride, b->arena(s0), b->astride, P.b_end, n, hipMemcpyDeviceToHost, b->st));
+	if (int r = fork()) return r;
+	auto sp = b->prof.begin(B_D2H, n, xs);
+	BCHK(hipMemcpy2DAsync(b->harena(s0), b->hstride, b->arena(s0), b->astride, P.b_end, n, hipMemcpyDeviceToHost, xs));
 	b->prof.end(sp);
 	return RIC_OK;
 }
@@ -1009,6 +1026,9 @@ void ric_batch_destroy(ric_batch* b)
 		if (c.h_post) (void)pinned_free(c.h_post);
 		if (c.d_yield) (void)dev_free(c.d_yield);
 		if (b->d_dpart) (void)dev_free(b->d_dpart);
+		if (b->xst) (void)hipStreamSynchronize(b->xst);
+		if (b->ev_fork) (void)hipEventDestroy(b->ev_fork);
+		if (b->xst) (void)hipStreamDestroy(b->xst);
 		if (c.d_pcmp) (void)dev_free(c.d_pcmp);
 		if (c.d_pcnt) (void)dev_free(c.d_pcnt);
 		if (c.d_ptotal) (void)dev_free(c.d_ptotal);
@@ -2028,15 +2048,23 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 	std::vector<hipEvent_t> evs(2, nullptr);
 	for (auto& e : evs) BCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
 	bool set_busy[2] = {false, false};
-	auto launch_group = [&](const HGroup& g) -> int {
+	// RIC_FRONT_SIDE_COPY=0: the front's second host group copies in stream order
+	static const bool side_copy_on = [] { const char* e = getenv("RIC_FRONT_SIDE_COPY"); return !e || atoi(e) != 0; }();
+	// side_copy: the group's band copies on a stream of their own (the step's
+	// front: slot set 1's copies beside the pool's forward levels, which use
+	// slot set 0 as scratch and would otherwise wait for them in stream order)
+	auto launch_group = [&](const HGroup& g, bool side_copy = false) -> int {
 		const int set = set_busy[0] ? 1 : 0;
 		set_busy[set] = true;
 		fl.emplace_back();
 		Flight& F = fl.back();
 		F.g = g; F.set = set; F.ev = evs[set];
+		side_copy = side_copy && C == 1 && set == 1 && !g.gpu;
+		if (side_copy && !b->xst) BCHK(hipStreamCreateWithFlags(&b->xst, hipStreamNonBlocking));
 		if (!g.gpu) {
 			if (C == 1) {
-				int r = gpu_encode_plane(b, set, g.m, 0, pix + g.f0, q, trans, true, -1, 1, yflag);
+				int r = gpu_encode_plane(b, set, g.m, 0, pix + g.f0, q, trans, !side_copy, -1, 1, yflag);
+				if (!r && side_copy) r = d2h_slots(b, set, g.m, b->xst);
 				if (r) return r;
 			} else {
 				// plane p of frame i in slot C i + p, then every slot's bands to the host
@@ -2048,7 +2076,7 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 				int r = d2h_slots(b, set, C * g.m);
 				if (r) return r;
 			}
-			BCHK(hipEventRecord(F.ev, b->st));
+			BCHK(hipEventRecord(F.ev, side_copy ? b->xst : b->st));
 			if (trace > 2) tr("  forward issued", g.f0);
 		}
 		F.done.reset(g.m);
@@ -2168,7 +2196,7 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 			while (rc == RIC_OK && fl.size() < 2 && !ready_host.empty()) {
 				const HGroup g = ready_host.front();
 				ready_host.pop_front();
-				rc = launch_group(g);
+				rc = launch_group(g, side_copy_on);
 			}
 			if (rc == RIC_OK) rc = kick_fwd(0);
 			if (rc == RIC_OK) rc = kick_fwd(1);
