@@ -698,7 +698,9 @@ def main():
         # the coder's issue counters (SQ_INSTS_SALU / VALU, SQ_WAIT_ANY, ... per stream)
         # cannot be read inside this process: rocprofv3 --pmc over one serving step
         # of this path at C3 (scripts/gpu_sq.sh), committed under profiles/
-        sqf = os.path.join(REPO, "profiles", "r05_stream_coder_sq.json")
+        sqf = os.path.join(REPO, "profiles", "r06_stream_coder_sq.json")
+        if not os.path.exists(sqf):
+            sqf = os.path.join(REPO, "profiles", "r05_stream_coder_sq.json")
         if not os.path.exists(sqf):
             sqf = os.path.join(REPO, "profiles", "r04_stream_coder_sq.json")
         if os.path.exists(sqf) and a.workload == "C3":

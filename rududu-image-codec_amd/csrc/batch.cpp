@@ -2048,8 +2048,20 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 	std::vector<hipEvent_t> evs(2, nullptr);
 	for (auto& e : evs) BCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
 	bool set_busy[2] = {false, false};
-	// RIC_FRONT_SIDE_COPY=0: the front's second host group copies in stream order
-	static const bool side_copy_on = [] { const char* e = getenv("RIC_FRONT_SIDE_COPY"); return !e || atoi(e) != 0; }();
+	// RIC_SIDE_COPY: the host groups' band copies on a side stream -- 0 none
+	// (stream order), 1 the step's front only, 2 (default) every host group
+	static const int side_copy_mode = [] { const char* e = getenv("RIC_SIDE_COPY"); return e ? atoi(e) : 2; }();
+	const bool side_copy_on = side_copy_mode >= 1;
+	bool pool_direct = C == 1;                           // (gpu_encode_plane's direct-write condition)
+	{
+		P.set_weight(trans);
+		const int lambda = lambda_of(q, 0);
+		int qin = quant_of(q, 0);
+		for (int l = 0; l < P.nlev && pool_direct; l++) {
+			const int mode = fwdq_mode(P.L[l], trans, level_qp(P, l, qin, lambda), 1);
+			pool_direct = mode != FQ_NONE && (l + 1 < P.nlev || mode == FQ_GENERIC);
+		}
+	}
 	// side_copy: the group's band copies on a stream of their own (the step's
 	// front: slot set 1's copies beside the pool's forward levels, which use
 	// slot set 0 as scratch and would otherwise wait for them in stream order)
@@ -2059,7 +2071,11 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 		fl.emplace_back();
 		Flight& F = fl.back();
 		F.g = g; F.set = set; F.ev = evs[set];
-		side_copy = side_copy && C == 1 && set == 1 && !g.gpu;
+		// set 0 too when the pool's forward levels write it straight (every
+		// level fused): the scratch the pool front and the harvests use in slot
+		// set 0 ([0, lo) and region C) is then disjoint from what the copies
+		// read ([cmp_dense, b_end) and d_cmp)
+		side_copy = side_copy && C == 1 && !g.gpu && (set == 1 || pool_direct);
 		if (side_copy && !b->xst) BCHK(hipStreamCreateWithFlags(&b->xst, hipStreamNonBlocking));
 		if (!g.gpu) {
 			if (C == 1) {
@@ -2224,7 +2240,7 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 			HGroup g;
 			if (!ready_dec.empty()) { g = ready_dec.front(); ready_dec.pop_front(); }
 			else { g = ready_host.front(); ready_host.pop_front(); }
-			rc = launch_group(g);
+			rc = launch_group(g, side_copy_mode >= 2);
 			if (rc) break;
 		}
 		if (rc) break;
