@@ -2049,8 +2049,9 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 	for (auto& e : evs) BCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
 	bool set_busy[2] = {false, false};
 	// RIC_SIDE_COPY: the host groups' band copies on a side stream -- 0 none
-	// (stream order), 1 the step's front only, 2 (default) every host group
-	static const int side_copy_mode = [] { const char* e = getenv("RIC_SIDE_COPY"); return e ? atoi(e) : 2; }();
+	// (stream order), 1 (default) the step's front only, 2 every host group (measured
+	// the same or lower: 11,691-11,913 against 11,907-11,969 Mpix/s, r6sc2)
+	static const int side_copy_mode = [] { const char* e = getenv("RIC_SIDE_COPY"); return e ? atoi(e) : 1; }();
 	const bool side_copy_on = side_copy_mode >= 1;
 	bool pool_direct = C == 1;                           // (gpu_encode_plane's direct-write condition)
 	{
