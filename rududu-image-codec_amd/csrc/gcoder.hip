@@ -178,7 +178,8 @@ struct GTabs {
 	uint32_t geo_ks;     // lane i < 25: kGeoK[i] | kGeoShift[i] << 8
 	uint32_t geo_thr;    // lane s in 1..10: kGeoThres[s - 1] | kGeoThres[s] << 16
 	uint32_t bit_thr;    // lane s in 0..9: kBitThres[s] | kBitThres[s + 1] << 16
-	uint32_t e16;        // enumDecode<16> table: lane k in 1..8 its offset (sum of C(16, j), j < k), lane 16 + k C(16, k)
+	uint32_t e16;        // enumDecode<16> table: lane k in 1..8 its offset (sum of C(16, j), j < k), lane 16 + k C(16, k),
+	                     // lane 32 + k CnkLen | CnkLost << 8 of (16, k) (the code part's lengths: enum16 needs no cnk[])
 	GC_DI void init()
 	{
 		const uint32_t l = lane_id();
@@ -190,6 +191,7 @@ struct GTabs {
 				if (j < (l & 15)) off += c;
 			}
 			e16 = l < 16 ? off : ck;
+			if (l >= 33 && l <= 40) e16 = (uint32_t)kCnkLen[15][l - 33] | (uint32_t)kCnkLost[15][l - 33] << 8;
 		}
 		geo_ks = l < 25 ? (uint32_t)kGeoK[l] | (uint32_t)kGeoShift[l] << 8 : 0;
 		geo_thr = (l >= 1 && l <= 10) ? (uint32_t)kGeoThres[l - 1] | (uint32_t)kGeoThres[l] << 16 : 0;
@@ -1234,7 +1236,14 @@ struct GDec {
 		const bool comp = k > 8;
 		const uint32_t kk = comp ? 16 - k : k;
 		const uint32_t off = lget(T.e16, kk), lim = lget(T.e16, 16 + kk);
-		uint32_t c = enum_code(cnk, kk, 16);
+		// enum_code(cnk, kk, 16) with the lengths from T.e16 (cnk[], two lane
+		// arrays used only by the edge blocks, is then not live across the
+		// block walk: at 88 VGPRs it was spilled to scratch and reloaded, with
+		// a full vmcnt wait, for every full block)
+		const uint32_t e = lget(T.e16, 32 + kk);
+		const uint32_t lost = e >> 8;
+		uint32_t c = bits((e & 255u) - 1);
+		if (c >= lost) c = ((c << 1) | bits(1)) - lost;
 		if (c >= lim) c = 0;                                 // the host reads code 0 past C(16, k) (corrupt streams)
 		const uint32_t i = off + c;
 		// RIC_GC_UNIFORM: the pattern made wave-uniform (a global-address-space
