@@ -83,6 +83,39 @@ def test_hybrid_roundtrip(ric, port, w, h, q, t, n, n_host, pool, slots, gpu_dec
             assert np.array_equal(outs[i].numpy(), port.decode_ric(r)[0]), (rep, i)
 
 
+def _pixel_digest(pix):
+    flat = np.ascontiguousarray(pix, np.uint8).reshape(-1).astype(np.uint64)
+    mult = np.arange(flat.size, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15) + np.uint64(1)
+    return np.uint64(np.sum(flat * mult, dtype=np.uint64))
+
+
+@pytest.mark.parametrize("w,h,q", [(640, 360, 9), (1004, 600, 9), (333, 201, 9), (512, 256, 0)])
+def test_hybrid_digests_and_fused_pixels(ric, port, w, h, q):
+    """The serving step's pixel output fused into the inverse level 0 of gray
+    9/7 frames (ZFrames::pix; widths a multiple of 4; others, e.g. 333, take
+    the separate pixel kernel): every frame's pixels and its digest
+    (ric_batch_set_digests, 16 partial words folded per frame) equal the
+    oracle's, for host-coded and GPU-coded frames, with and without the
+    fusion (RIC_PIX_FUSE is read once per process: the unfused form is the
+    odd width here)."""
+    n, n_host = 9, 3
+    host = [ric.synth(w, h, 1, 140 + i) for i in range(n)]
+    frames = [ric.DeviceArray.from_numpy(x) for x in host]
+    outs = [f.empty_like() for f in frames]
+    dig = ric.DeviceArray(n, np.uint64, zero=True)
+    b = ric.Batch(w, h, 1, slots=3, threads=3)
+    b.set_digests(dig, n)
+    b.hybrid_config(3, (w * h * 2 + 65536 + 15) // 16 * 16)
+    b.roundtrip_hybrid(frames, outs, n_host, q, 0, gpu_decode=1)
+    got = dig.numpy()
+    for i in range(n):
+        r = b.stream(i)
+        assert r == port.encode_ric(host[i], q, 0), i
+        want = port.decode_ric(r)[0]
+        assert np.array_equal(outs[i].numpy().reshape(want.shape), want), i
+        assert got[i] == _pixel_digest(want), i
+
+
 def _gpu_decode(ric, rics, w, h, c=1):
     istride = (max(len(r) for r in rics) + 4095) // 4096 * 4096
     buf = np.zeros(len(rics) * istride, np.uint8)
