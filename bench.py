@@ -555,9 +555,10 @@ def main():
     barrier()
     # the host share follows each step's own timeline (auto split): the next
     # step's host round trips are set so that the host side ends RIC_BENCH_MARGIN
-    # ms (default 60) before the GPU side did in this step.  The warmup's
+    # ms (default 120: a host side that overruns costs the step its time, one
+    # that ends early only a few frames) before the GPU side did in this step.  The warmup's
     # estimate alone left the two sides +-1 % apart from step to step.
-    margin = float(os.environ.get("RIC_BENCH_MARGIN", "60"))
+    margin = float(os.environ.get("RIC_BENCH_MARGIN", "120"))
     per_step = []
 
     def rebalance():
