@@ -35,6 +35,17 @@
 #ifndef RIC_GC_ELOW_V
 #define RIC_GC_ELOW_V 0
 #endif
+// RIC_GC_EVALU: the encoder's range coder (range, low) on the VALU, its
+// branch conditions read back from lane 0.  The CU's one scalar unit serves
+// the coder waves of all four SIMDs and ran at 0.70 instructions per cycle in
+// the serving step (profiles/r06_stream_coder_sq.json); with the waves
+// levelled (level_apply) they all encode at the same time, the encoder's
+// bins then queueing on it.  Measured (one C3 serving step, 3072 streams,
+// same box, r6ev): 10.02 s against 10.40 s per launch, 12,185-12,306 against
+// 11,906 Mpix/s.
+#ifndef RIC_GC_EVALU
+#define RIC_GC_EVALU 1
+#endif
 // RIC_GC_UCOND: the decoder's state stays in VGPRs (the balanced SALU / VALU
 // mix, see GDec::enum16) but its branch conditions are read from lane 0
 // (v_readfirstlane): scalar branches instead of exec-mask ones
@@ -105,6 +116,21 @@ GC_DI uint64_t vf(uint64_t x)
 	asm volatile("" : "+v"(x));
 #endif
 	return x;
+}
+GC_DI uint32_t ev(uint32_t x)
+{
+#if RIC_GC_EVALU
+	asm volatile("" : "+v"(x));
+#endif
+	return x;
+}
+GC_DI uint32_t eu(uint32_t x)
+{
+#if RIC_GC_EVALU
+	return __builtin_amdgcn_readfirstlane(x);
+#else
+	return x;
+#endif
 }
 // RIC_GC_UCOND 4: 2 and the decoder's byte window in VGPRs (the raw-bit
 // reader's fills on the VALU; the range decoder reads its bytes back by lane 0)
@@ -453,23 +479,25 @@ struct GEnc {
 			put(q0, low >> 24);
 #if RIC_GC_ELOW_V
 			range = __builtin_amdgcn_readfirstlane(((low + range - 1) ^ low) >= 0x01000000u ? (0u - low) & 4095u : range);
+#elif RIC_GC_EVALU
+			range = ev(((low + range - 1) ^ low) >= 0x01000000u ? (0u - low) & 4095u : range);
 #else
 			if (((low + range - 1) ^ low) >= 0x01000000u) range = (0u - low) & 4095u;
 #endif
 			q0 = q1; q1 = q2; q2 = q3; q3 = p++;
-			range <<= 8;
-			low <<= 8;
+			range = ev(range << 8);
+			low = ev(low << 8);
 			// a zero range would spin here forever (never on a valid stream;
 			// a wave that never ends takes the whole GPU down): stop and flag
-			if (__builtin_expect(++it > 4, 0)) { ovf |= 4; range = 1u << 16; }
-		} while (range <= 4096u);
+			if (__builtin_expect(++it > 4, 0)) { ovf |= 4; range = ev(1u << 16); }
+		} while (eu(range) <= 4096u);
 	}
 	GC_DI void bin(uint32_t freq, uint32_t bit)         // codeBin, muxcodec.h:156-163
 	{
-		if (__builtin_expect(range <= 4096u, 0)) norm();
+		if (__builtin_expect(eu(range) <= 4096u, 0)) norm();
 		const uint32_t t = (range * freq) >> 12;
-		low += t & (0u - bit);
-		range = t + ((range - 2 * t) & (0u - bit));
+		low = ev(low + (t & (0u - bit)));
+		range = ev(t + ((range - 2 * t) & (0u - bit)));
 	}
 	GC_DI void bits(uint32_t v, uint32_t len)           // bitsCode, 64-bit FIFO (entropy.h)
 	{
@@ -480,12 +508,12 @@ struct GEnc {
 	GC_DI void init(uint8_t* o, uint32_t c, uint32_t base)   // init_encoder at out + base
 	{
 		out_lo = vc((uint32_t)(uintptr_t)o); out_hi = vc((uint32_t)((uintptr_t)o >> 32)); cap = vc(c);
-#if RIC_GC_ELOW_V
+#if RIC_GC_ELOW_V || RIC_GC_EVALU
 		low = to_vgpr(0u);                               // (experiment: the coder's low on the VALU)
 #else
 		low = 0;
 #endif
-		range = 1u << 16;
+		range = ev(1u << 16);
 		ebits = 0; ebuf = 0;
 		reserved = 0;
 		q0 = base; q1 = base + 1; q2 = base + 2; q3 = base + 3;
