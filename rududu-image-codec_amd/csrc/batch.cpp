@@ -729,7 +729,7 @@ int host_encode_plane(ric_batch* b, int s, int p, int q, int trans, uint8_t* out
 	int32_t* status = (int32_t*)(b->harena(s) + P.status_off);
 	if (*status) {
 		*status = 0;
-		set_last_error("fused level kernel: LDS ring hand-off timed out (device status word set; output discarded)");
+		set_last_error("device status word set: a fused level kernel's LDS ring hand-off or the compaction's look-back timed out; output discarded");
 		return RIC_E_HIP;
 	}
 	const int16_t* cp = nullptr;
@@ -956,6 +956,7 @@ int ric_batch_create(ric_batch** out, int w, int h, int channels, int slots, int
 		bool bad = b->cmp_stride > b->cmp_dense ||      // the values land in the mirror's band area
 		           bfail(hipMalloc(&b->d_cmp, ns * b->cmp_stride), "hipMalloc compact") ||
 		           bfail(hipMalloc(&b->d_cmp_cnt, ns * b->cmp_cstride * sizeof(uint32_t)), "hipMalloc compact") ||
+		           bfail(hipMemset(b->d_cmp_cnt, 0, ns * b->cmp_cstride * sizeof(uint32_t)), "hipMemset compact") ||
 		           bfail(hipMalloc(&b->d_cmp_total, ns * sizeof(uint32_t)), "hipMalloc compact") ||
 		           bfail(hipHostMalloc(&b->h_cmp_total, ns * sizeof(uint32_t), 0), "hipHostMalloc compact") ||
 		           bfail(hipMalloc(&b->d_cmp_args, 2 * sizeof(CmpArgs)), "hipMalloc compact");
@@ -968,6 +969,8 @@ int ric_batch_create(ric_batch** out, int w, int h, int channels, int slots, int
 			h[set].out = b->d_cmp + s0 * b->cmp_stride; h[set].ostride = b->cmp_stride;
 			h[set].cnt = b->d_cmp_cnt + s0 * b->cmp_cstride; h[set].cstride = b->cmp_cstride;
 			h[set].total = b->d_cmp_total + s0;
+			// (the one-pass kernel's kCmpLookback: the status word fails the frame)
+			h[set].status = b->arena((int)s0) + b->P.status_off; h[set].sstride = b->astride;
 		}
 		if (!bad) bad = bfail(hipMemcpy(b->d_cmp_args, h, sizeof(h), hipMemcpyHostToDevice), "hipMemcpy compact");
 		if (bad) {
@@ -1265,7 +1268,7 @@ int ric_batch_encode_gpu(ric_batch* b, const uint8_t* const* pix, int n, int q, 
 		len[i] = b->h_res[2 * i];
 		if (b->h_res[2 * i + 1] == 2) {
 			clear_status(b);
-			set_last_error("fused level kernel: LDS ring hand-off timed out (device status word set; output discarded)");
+			set_last_error("device status word set: a fused level kernel's LDS ring hand-off or the compaction's look-back timed out; output discarded");
 			return RIC_E_HIP;
 		}
 		if (b->h_res[2 * i + 1]) return RIC_E_CAPACITY;
@@ -1468,6 +1471,7 @@ int ric_batch_hybrid_config_ex(ric_batch* b, int pool_frames, size_t stream_cap,
 			for (int k = 0; k < 3; k++) nch += c.dl.nch[k];
 			c.pcnt_stride = (size_t)(nch + 63) / 64 * 64;
 			BCHK(hipMalloc(&c.d_pcnt, sizeof(uint32_t) * c.pcnt_stride * b->slots));
+			BCHK(hipMemset(c.d_pcnt, 0, sizeof(uint32_t) * c.pcnt_stride * b->slots));
 			BCHK(hipMalloc(&c.d_ptotal, sizeof(uint32_t) * b->slots));
 			std::vector<CmpArgs> ca(2 * (size_t)c.pcmp_groups * b->channels);
 			for (int h = 0; h < 2; h++)
@@ -1981,7 +1985,7 @@ int ric_batch_roundtrip_hybrid(ric_batch* b, const uint8_t* const* pix, int n, i
 		for (int k = 0; k < m; k++) {
 			if (re[2 * k + 1] == 2) {
 				clear_status(b);
-				set_last_error("fused level kernel: LDS ring hand-off timed out (device status word set; output discarded)");
+				set_last_error("device status word set: a fused level kernel's LDS ring hand-off or the compaction's look-back timed out; output discarded");
 				return RIC_E_HIP;
 			}
 			if (re[2 * k + 1] == 4 && c.vcap) {

@@ -16,7 +16,9 @@ struct CmpBand {
 };
 
 // Frames f (blockIdx.z): arena + f * astride; the stream to out + f * ostride
-// (int16 values); cnt + f * cstride: per chunk, its count then its offset;
+// (int16 values); cnt + f * cstride: per chunk, its count then its offset
+// (three passes), or the one-pass kernel's ticket and look-back words -- at
+// least up(nchunk, 64) words, zeroed when allocated;
 // total[f]: the frame's value count.  band[]: the 16-bit bands in coding
 // order (coarse to fine, V, H, D).
 struct CmpArgs {
@@ -42,6 +44,9 @@ struct CmpArgs {
 };
 // a compacted pool frame over its capacity (the status word's bit)
 constexpr int32_t kCmpOverCap = 4;
+// the one-pass compaction's look-back gave up (the status word's bit; nothing
+// written: the frame is then left to the host, or its call fails)
+constexpr int32_t kCmpLookback = 8;
 
 // the band table of a pyramid (nb, nchunk, band[]); the pointers are the caller's
 void cmp_args(const Pyramid& P, CmpArgs& a);
@@ -50,7 +55,8 @@ size_t cmp_values(const Pyramid& P);
 // the arena offset from which the rest of the payload stays dense: the int
 // bands, the coarsest LL, then region B (status word, records, parent info)
 size_t cmp_dense_from(const Pyramid& P);
-// the three passes over nframes frames
+// the compaction of nframes frames: three passes (count, scan, write), or
+// one (k_cmp_one, RIC_CMP_PASS=1)
 int launch_compact(const CmpArgs* dev_args, int nchunk, int nframes, hipStream_t st);
 // frame f's values (total[f] int16, from src + f * sstride, rounded up to 16
 // bytes) to dst + f * dstride: a device-mapped host mirror, written by the kernel

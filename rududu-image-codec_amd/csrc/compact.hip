@@ -17,6 +17,8 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <algorithm>
+#include <atomic>
+#include <cstdlib>
 #include "ric_types.h"
 #include "symbols.h"
 #include "compact.h"
@@ -195,6 +197,7 @@ struct CmpChunk {
 	int bx, by;                      // the lane's block
 };
 
+template <bool BASE = true>
 __device__ __forceinline__ void cmp_load(const CmpArgs& a, const char* arena, const char* bsrc, int f, int c, int b0,
                                          CmpChunk& L)
 {
@@ -202,7 +205,7 @@ __device__ __forceinline__ void cmp_load(const CmpArgs& a, const char* arena, co
 	const CmpBand& B = a.band[b];
 	const int s0 = (c - B.chunk0) * 64, s = s0 + lane64();
 	L.b = b; L.s = s;
-	L.base = gp(a.cnt)[(size_t)f * a.cstride + c];
+	L.base = BASE ? gp(a.cnt)[(size_t)f * a.cstride + c] : 0u;
 	L.rec = 0;
 	L.v[0] = L.v[1] = L.v[2] = L.v[3] = 0;
 	int bx, by;
@@ -218,6 +221,45 @@ __device__ __forceinline__ void cmp_load(const CmpArgs& a, const char* arena, co
 		for (int r = 0; r < 4; r++)
 			if (r < h) L.v[r] = *gp((const uint64_t*)(band + (long)r * B.pitch));
 	}
+}
+
+// one chunk's values out: the lane's block holds its values from o on (its
+// prefix in the chunk), the chunk's tot values start at base.  They are
+// gathered in the wave's LDS slots sv, then stored with consecutive lanes on
+// consecutive values.
+__device__ __forceinline__ void cmp_put(const CmpArgs& a, int16_t* out, int16_t* sv, const CmpChunk& cur, uint32_t o,
+                                        uint32_t tot, uint32_t base)
+{
+	const int l = lane64();
+	uint32_t m = BlockRec::mask(cur.rec);
+	// over the pool's capacity: flagged (k_cmp_scan / k_cmp_one), nothing written
+	if (a.vcap && base + tot > a.vcap) return;
+	const CmpBand& B = a.band[cur.b];
+	const int w = B.dx - cur.bx * 4 < 4 ? B.dx - cur.bx * 4 : 4;
+	uint32_t k = o;
+	if (w == 4) {
+		// the 16 positions in raster order, straight through: a kept
+		// value to its slot, the others to the lane's dump slot
+		const uint32_t dump = 1024u + (uint32_t)l;
+#pragma unroll
+		for (int i = 0; i < 16; i++) {
+			const uint32_t bit = (m >> i) & 1u;
+			sv[bit ? k : dump] = (int16_t)(cur.v[i >> 2] >> (16 * (i & 3)));
+			k += bit;
+		}
+	} else if (m) {
+		// a block cut by the band's right edge: w values per row
+#pragma unroll
+		for (int r = 0; r < 4; r++) {
+			const uint32_t rm = m & ((1u << w) - 1u);
+			m >>= w;
+			for (uint32_t q = rm; q; q &= q - 1) sv[k++] = (int16_t)(cur.v[r] >> (16 * __builtin_ctz(q)));
+		}
+	}
+	__builtin_amdgcn_wave_barrier();
+	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+	for (uint32_t i = (uint32_t)l; i < tot; i += 64) gp(out)[base + i] = sv[i];
+	__builtin_amdgcn_wave_barrier();
 }
 
 __global__ __launch_bounds__(64 * kCmpWaves) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_cmp_write(const CmpArgs* __restrict__ ap)
@@ -238,41 +280,167 @@ __global__ __launch_bounds__(64 * kCmpWaves) __attribute__((amdgpu_waves_per_eu(
 	for (; c < a.nchunk; c += wave_count()) {
 		const int cn = c + wave_count();
 		if (cn < a.nchunk) cmp_load(a, arena, bsrc, f, cn, cur.b, nxt);
-		uint32_t m = BlockRec::mask(cur.rec);
 		uint32_t tot;
-		const uint32_t o = wave_prefix5((uint32_t)__popc(m), tot);
-		const uint32_t base = cur.base;
-		// over the pool's capacity: flagged by k_cmp_scan, nothing written
-		if (!(a.vcap && base + tot > a.vcap)) {
-			const CmpBand& B = a.band[cur.b];
-			const int w = B.dx - cur.bx * 4 < 4 ? B.dx - cur.bx * 4 : 4;
-			uint32_t k = o;
-			if (w == 4) {
-				// the 16 positions in raster order, straight through: a kept
-				// value to its slot, the others to the lane's dump slot
-				const uint32_t dump = 1024u + (uint32_t)l;
-#pragma unroll
-				for (int i = 0; i < 16; i++) {
-					const uint32_t bit = (m >> i) & 1u;
-					sv[bit ? k : dump] = (int16_t)(cur.v[i >> 2] >> (16 * (i & 3)));
-					k += bit;
-				}
-			} else if (m) {
-				// a block cut by the band's right edge: w values per row
-#pragma unroll
-				for (int r = 0; r < 4; r++) {
-					const uint32_t rm = m & ((1u << w) - 1u);
-					m >>= w;
-					for (uint32_t q = rm; q; q &= q - 1) sv[k++] = (int16_t)(cur.v[r] >> (16 * __builtin_ctz(q)));
-				}
-			}
-			__builtin_amdgcn_wave_barrier();
-			__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-			for (uint32_t i = (uint32_t)l; i < tot; i += 64) gp(out)[base + i] = sv[i];
-			__builtin_amdgcn_wave_barrier();
-		}
+		const uint32_t o = wave_prefix5((uint32_t)__popc(BlockRec::mask(cur.rec)), tot);
+		cmp_put(a, out, sv, cur, o, tot, cur.base);
 		cur = nxt;
 	}
+}
+
+// ---- one pass (RIC_CMP_PASS=1; the default is the three kernels above).
+// Counts, the frame's running value offset and the values in one kernel: a
+// workgroup takes the next ticket of its frame (an atomic counter, so every
+// lower ticket belongs to a workgroup already running), loads its kCpg chunks
+// once (records and band rows, all in flight together), publishes its value
+// count and looks back over the tickets before it for its offset (decoupled
+// look-back: the nearest inclusive prefix plus the counts between), then
+// writes its values.  The records are read once instead of twice, and the
+// scan pass and two launches are gone.
+// Per frame, the cnt array holds the ticket counter (u32 0) and one u64 status
+// per ticket from byte 8: epoch << 34 | flag << 32 | value, flag 1 = the
+// ticket's count, 2 = the count of every value up to and including it.  The
+// epoch (a per-launch number) tells this launch's words from the previous
+// ones', so nothing is reset between launches; the last ticket resets the
+// counter.  A look-back that waits too long (never on a working device) gives
+// up, sets kCmpLookback in the frame's status word and writes nothing.
+// Measured in the C3 serving step (profiles/r06_cmp_onepass_ab.txt), per frame:
+// 4 chunks per wave 45.7 us, 8 chunks 36.9, 4 at issue priority 3 41.4, 8 at
+// priority 3 31.9 -- against 32.3 for the three passes (count 7.3 + scan 2.4
+// + write 22.9): the look-back's round trips (ticket, status words) and its
+// waits on slower predecessors beside the coder waves cost what the saved
+// record reads and launches gain.  Kept as the opt-in form at 8 / 3.
+#ifndef RIC_CMP_CPW
+#define RIC_CMP_CPW 8
+#endif
+#ifndef RIC_CMP_PRIO
+#define RIC_CMP_PRIO 3
+#endif
+constexpr int kCpw = RIC_CMP_CPW;                // chunks per wave
+constexpr int kCpg = kCmpWaves * kCpw;           // chunks per workgroup (ticket)
+constexpr uint32_t kLbAgg = 1u, kLbInc = 2u;
+constexpr int kLbPolls = 1 << 20;
+
+__device__ __forceinline__ uint64_t lb_word(uint32_t epoch, uint32_t flag, uint32_t v)
+{
+	return (uint64_t)epoch << 34 | (uint64_t)flag << 32 | v;
+}
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v)
+{
+#pragma unroll
+	for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+	return v;
+}
+
+// (one wave) the values before ticket t; ok false: gave up
+__device__ __forceinline__ uint32_t lookback(uint64_t* stat, int t, uint32_t epoch, bool& ok)
+{
+	const int l = lane64();
+	uint32_t acc = 0;
+	int hi = t - 1, polls = 0;
+	while (hi >= 0) {
+		const int i = hi - l;
+		const uint64_t v = i >= 0 ? __hip_atomic_load(stat + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+		                          : lb_word(epoch, kLbInc, 0);
+		const uint32_t fl = (uint32_t)(v >> 32) & 3u;
+		const bool valid = (uint32_t)(v >> 34) == epoch && fl != 0;
+		const uint64_t incm = __ballot(valid && fl == kLbInc);
+		const uint64_t bad = __ballot(!valid);
+		// the lanes needed: up to the nearest inclusive prefix, or all 64
+		const int lim = incm ? __builtin_ctzll(incm) : 63;
+		const uint64_t need = lim == 63 ? ~0ull : ((2ull << lim) - 1);
+		if (bad & need) {
+			if (++polls > kLbPolls) { ok = false; return 0; }
+			__builtin_amdgcn_s_sleep(2);
+			continue;
+		}
+		acc += wave_sum(l <= lim ? (uint32_t)v : 0u);
+		if (incm) break;
+		hi -= 64;
+	}
+	ok = true;
+	return acc;
+}
+
+__global__ __launch_bounds__(64 * kCmpWaves) void k_cmp_one(const CmpArgs* __restrict__ ap, uint32_t epoch)
+{
+	const CmpArgs& a = *ap;
+	const int f = blockIdx.z;
+	const char* arena = a.arena + (size_t)f * a.astride;
+	const char* bsrc = a.bsrc ? a.bsrc + (size_t)f * a.bstride : arena;
+	int16_t* out = (int16_t*)(a.out + (size_t)f * a.ostride);
+	uint32_t* fc = a.cnt + (size_t)f * a.cstride;
+	uint64_t* stat = (uint64_t*)(fc + 2);
+	__shared__ int16_t stage[kCmpWaves][64 * 16 + 64];
+	__shared__ uint32_t s_t, s_pre, s_ok, s_wtot[kCmpWaves];
+	const int G = (int)gridDim.x;
+	if (RIC_CMP_PRIO) __builtin_amdgcn_s_setprio(RIC_CMP_PRIO);
+	if (threadIdx.x == 0) {
+		const uint32_t t = atomicAdd(fc, 1u);
+		// every ticket of this launch is taken: the counter back to 0 for the next
+		if (t == (uint32_t)G - 1) __hip_atomic_store(fc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		s_t = t;
+	}
+	__syncthreads();
+	const int t = (int)__builtin_amdgcn_readfirstlane(s_t);
+	const int w = (int)__builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+	const int l = lane64();
+	int16_t* sv = stage[w];
+	const int c0 = t * kCpg + w * kCpw;
+	CmpChunk ch[kCpw];
+	int b = 0;
+#pragma unroll
+	for (int u = 0; u < kCpw; u++) {
+		if (c0 + u < a.nchunk) {
+			cmp_load<false>(a, arena, bsrc, f, c0 + u, b, ch[u]);
+			b = ch[u].b;
+		} else {
+			ch[u].rec = 0; ch[u].b = b; ch[u].s = 0; ch[u].bx = ch[u].by = 0; ch[u].base = 0;
+		}
+	}
+	uint32_t op[kCpw], tot[kCpw], cb[kCpw], wsum = 0;
+#pragma unroll
+	for (int u = 0; u < kCpw; u++) {
+		op[u] = wave_prefix5((uint32_t)__popc(BlockRec::mask(ch[u].rec)), tot[u]);
+		cb[u] = wsum;
+		wsum += tot[u];
+	}
+	if (l == 0) s_wtot[w] = wsum;
+	__syncthreads();
+	uint32_t wpre = 0, gtot = 0;
+#pragma unroll
+	for (int k = 0; k < kCmpWaves; k++) {
+		const uint32_t v = s_wtot[k];
+		if (k < w) wpre += v;
+		gtot += v;
+	}
+	if (w == 0) {
+		uint32_t pre = 0;
+		bool ok = true;
+		if (t == 0) {
+			if (l == 0) __hip_atomic_store(stat, lb_word(epoch, kLbInc, gtot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		} else {
+			if (l == 0) __hip_atomic_store(stat + t, lb_word(epoch, kLbAgg, gtot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			pre = lookback(stat, t, epoch, ok);
+			if (l == 0 && ok)
+				__hip_atomic_store(stat + t, lb_word(epoch, kLbInc, pre + gtot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		}
+		if (l == 0) { s_pre = pre; s_ok = ok; }
+	}
+	__syncthreads();
+	if (!s_ok) {
+		if (threadIdx.x == 0 && a.status) atomicOr((int32_t*)(a.status + (size_t)f * a.sstride), kCmpLookback);
+		return;
+	}
+	const uint32_t base0 = s_pre + wpre;
+	if (t == G - 1 && threadIdx.x == 0) {
+		const uint32_t total = s_pre + gtot;
+		a.total[f] = total;
+		if (a.vcap && total > a.vcap && a.status) atomicOr((int32_t*)(a.status + (size_t)f * a.sstride), kCmpOverCap);
+	}
+#pragma unroll
+	for (int u = 0; u < kCpw; u++)
+		if (c0 + u < a.nchunk) cmp_put(a, out, sv, ch[u], op[u], tot[u], base0 + cb[u]);
 }
 
 // the decode side: one wave per chunk of 64 blocks (flattened over the three
@@ -483,6 +651,18 @@ size_t cmp_dense_from(const Pyramid& P)
 int launch_compact(const CmpArgs* dev_args, int nchunk, int nframes, hipStream_t st)
 {
 	if (nframes <= 0 || nchunk <= 0) return 0;
+	// (read per call: a test runs both forms in one process)
+	const char* pe = getenv("RIC_CMP_PASS");
+	if (pe && atoi(pe) == 1) {
+		// the look-back words: per frame, 8 + 8 G bytes of the cnt array's
+		// up(nchunk, 64) words (cstride, batch.cpp), G = nchunk / 16 rounded up
+		static std::atomic<uint32_t> epoch{0};
+		uint32_t e = (epoch.fetch_add(1) + 1) & 0x3FFFFFFFu;
+		if (!e) e = (epoch.fetch_add(1) + 1) & 0x3FFFFFFFu;
+		const int g = (nchunk + kCpg - 1) / kCpg;
+		hipLaunchKernelGGL(k_cmp_one, dim3(g, 1, nframes), dim3(64 * kCmpWaves), 0, st, dev_args, e);
+		return hipGetLastError() == hipSuccess ? 0 : -1;
+	}
 	// about 4 chunks per wave, at most 128 workgroups per frame
 	const int g = std::min(128, (nchunk + 4 * kCmpWaves - 1) / (4 * kCmpWaves));
 	hipLaunchKernelGGL(k_cmp_count, dim3(g, 1, nframes), dim3(64 * kCmpWaves), 0, st, dev_args);

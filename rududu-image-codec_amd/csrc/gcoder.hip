@@ -939,7 +939,9 @@ GC_DI uint32_t enc_frame(const GEncArgs& a, int f, uint32_t& end_out)
 	int32_t status = 0;
 	for (int p = 0; p < a.nplanes; p++) status |= *gld((const int32_t*)(arena + p * a.pstride + a.status_off));
 	status = __builtin_amdgcn_readfirstlane(status);
-	if (status & 4) { end_out = 0; return 4; }          // (not coded: over a compacted pool's capacity)
+	// not coded: over a compacted pool's capacity, or its compaction gave up
+	// (kCmpOverCap, kCmpLookback): the host takes the frame
+	if (status & (4 | 8)) { end_out = 0; return 4; }
 	GTabs T;
 	T.init();
 	GEnc<RING> e;
