@@ -601,13 +601,15 @@ def main():
         nlev_i = len(bmi["dwt"])
         l0_bytes_i = bmi["dwt"][0] + bmi["quant"][0]
         enc_bytes_i = sum(bmi["dwt"]) + sum(bmi["quant"]) + bmi["ll"]
-        iso_out = [f.empty_like() for f in frames[:slots]]
+        # the forward levels back to back, as in the step's front (the full
+        # encode + decode + pixel loop, ric_batch_diag_gpu, put level 0 at
+        # 0.91-1.08 ms per launch against 0.86 in the front: rocprofv3 kernel
+        # trace of the round-6 HEAD bench, profiles/r06_head_kernel_stats.csv)
         b.prof_enable(False)
-        b.diag_gpu(frames[:slots], a.q, a.trans, 5, iso_out)
+        b.diag_gpu_encode(frames[:slots], a.q, a.trans, 5)
         b.prof_enable(True)
-        b.diag_gpu(frames[:slots], a.q, a.trans, 10, iso_out)
+        b.diag_gpu_encode(frames[:slots], a.q, a.trans, 10)
         pi = b.prof_read()
-        del iso_out
         if pi["fwd_l0"][1]:
             t_iso = pi["fwd_l0"][0] / pi["fwd_l0"][1]
             ach = l0_bytes_i / (t_iso * 1e-3) / 1e9
@@ -618,8 +620,9 @@ def main():
                               "frac": round(ach / HBM_PEAK_GBS, 4)},
                    "per_level_us_per_frame": [round(x * 1e3, 2) for x in fi],
                    "gpu_wavelet_encode": we,
-                   "note": "GPU stages alone (ric_batch_diag_gpu), %d frames per launch, 10 iterations after 5 "
-                           "untimed ones, right after the timed region (before the verification)" % slots}
+                   "note": "the forward levels alone, back to back as in the step's front "
+                           "(ric_batch_diag_gpu_encode), %d frames per launch, 10 iterations after 5 untimed ones, "
+                           "right after the timed region (before the verification)" % slots}
         b.prof_enable(False)
 
     # ---- verification (outside the timed region): EVERY frame of the last

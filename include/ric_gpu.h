@@ -316,6 +316,10 @@ int ric_batch_hybrid_fallbacks(ric_batch* b, int* frames);
  * quantised, pixel output to pix_out if given); no host coding. */
 int ric_batch_diag_gpu(ric_batch* b, const uint8_t* const* pix, int n, int q, int trans, int iters,
                        uint8_t* const* pix_out);
+/* The forward levels alone, iters times back to back over n <= slots device
+ * frames (what the serving step's front runs before a coder launch; the
+ * bench's roofline_isolated). */
+int ric_batch_diag_gpu_encode(ric_batch* b, const uint8_t* const* pix, int n, int q, int trans, int iters);
 int ric_batch_prof_enable(ric_batch* b, int on);
 int ric_batch_prof_read(ric_batch* b, double* ms, long* frames, long* launches, int n);
 

@@ -443,9 +443,10 @@ int gpu_encode_plane(ric_batch* b, int set, int n, int p, const uint8_t* const* 
 		QuantParams qp = level_qp(P, l, qin, lambda);
 		const int mode = fwdq_mode(P.L[l], trans, qp, vec16);
 		fused[l] = mode != FQ_NONE;
-		auto sp = b->prof.begin(B_FWD + std::min(l, 7), n, b->st);
+		// (the yield flag's one-wave kernels outside the level's timed span)
 		if (y0only && l == 0 && yf.raise()) return RIC_E_HIP;
 		if (y0only && l == 1 && yf.lower()) return RIC_E_HIP;
+		auto sp = b->prof.begin(B_FWD + std::min(l, 7), n, b->st);
 		if (mode == FQ_PACKED) {
 			// the batch's planes are 8-bit pixels after the level shift (in8)
 			if (launch_fwdq_level_z(P, l, fr, vec8, vec16, qp, b->zf[set][l], b->st, 1)) return RIC_E_HIP;
@@ -2302,6 +2303,17 @@ int ric_batch_diag_gpu(ric_batch* b, const uint8_t* const* pix, int n, int q, in
 		if (!rc && pix_out) rc = gpu_pix_out(b, 0, n, qs.data(), pix_out, 1);
 		if (rc) return rc;
 	}
+	BCHK(hipStreamSynchronize(b->st));
+	b->prof.harvest();
+	return RIC_OK;
+}
+
+int ric_batch_diag_gpu_encode(ric_batch* b, const uint8_t* const* pix, int n, int q, int trans, int iters)
+{
+	if (!b || !pix || n < 1 || n > b->slots || iters < 0) return RIC_E_ARG;
+	if (set_dev(b->device)) return RIC_E_HIP;
+	for (int it = 0; it < iters; it++)
+		if (int rc = gpu_encode_plane(b, 0, n, 0, pix, q, trans)) return rc;
 	BCHK(hipStreamSynchronize(b->st));
 	b->prof.harvest();
 	return RIC_OK;

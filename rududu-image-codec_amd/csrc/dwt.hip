@@ -2740,15 +2740,101 @@ void launch_inv_level(const Level& L, const Band& lls, char* arena, void* out, l
 // The frames of a batch sit at fixed strides (arena, level input, output),
 // so every launch below is one grid over nz frames, its per-frame arguments
 // in a device array (ZArgs) that is only re-uploaded when it changes.
+namespace {
+uint64_t zargs_hash(const void* data, size_t bytes)
+{
+	// FNV-1a over 8-byte words (the images are arrays of pointers and ints)
+	uint64_t h = 1469598103934665603ull ^ bytes;
+	const unsigned char* p = (const unsigned char*)data;
+	size_t i = 0;
+	for (; i + 8 <= bytes; i += 8) {
+		uint64_t w;
+		memcpy(&w, p + i, 8);
+		h = (h ^ w) * 1099511628211ull;
+		h ^= h >> 29;
+	}
+	for (; i < bytes; i++) h = (h ^ p[i]) * 1099511628211ull;
+	return h;
+}
+
+// the cache (see ZArgsImage): an image seen before, or a new one while there
+// is room; -1 if neither
+int zargs_cached(ZArgs& z, const void* data, size_t bytes, hipStream_t st)
+{
+	static const bool on = [] { const char* e = getenv("RIC_ZARGS_CACHE"); return !e || atoi(e) != 0; }();
+	if (!on || bytes > ZArgs::kCacheBlock) return -1;
+	const uint64_t h = zargs_hash(data, bytes);
+	for (size_t i = 0; i < z.cache.size(); i++) {
+		ZArgsImage& e = z.cache[i];
+		if (e.hash == h && e.host.size() == bytes && memcmp(e.host.data(), data, bytes) == 0) {
+			// (another stream: after the upload)
+			if (e.st != st && hipStreamWaitEvent(st, e.ev, 0) != hipSuccess) return -2;
+			return (int)i;
+		}
+	}
+	const size_t need = (bytes + 255) & ~(size_t)255;
+	if (z.ctotal + need > ZArgs::kCacheBytes) return -1;
+	if (z.cdev.empty() || z.cused + need > ZArgs::kCacheBlock) {
+		char* d = nullptr;
+		char* hb = nullptr;
+		if (hipMalloc(&d, ZArgs::kCacheBlock) != hipSuccess) return -2;
+		if (hipHostMalloc(&hb, ZArgs::kCacheBlock, 0) != hipSuccess) { (void)dev_free(d); return -2; }
+		z.cdev.push_back(d);
+		z.chost.push_back(hb);
+		z.cused = 0;
+	}
+	char* d = z.cdev.back() + z.cused;
+	char* hb = z.chost.back() + z.cused;
+	z.cused += need;
+	z.ctotal += need;
+	memcpy(hb, data, bytes);          // (the pinned source is never rewritten)
+	ZArgsImage e;
+	e.hash = h;
+	e.dev = d;
+	e.host.assign((const char*)data, (const char*)data + bytes);
+	e.st = st;
+	e.ev = nullptr;
+	if (hipEventCreateWithFlags(&e.ev, hipEventDisableTiming) != hipSuccess) return -2;
+	if (hipMemcpyAsync(d, hb, bytes, hipMemcpyHostToDevice, st) != hipSuccess) return -2;
+	if (hipEventRecord(e.ev, st) != hipSuccess) return -2;
+	z.cache.push_back(std::move(e));
+	return (int)z.cache.size() - 1;
+}
+}  // namespace
+
 int zargs_put(ZArgs& z, const void* data, size_t bytes, hipStream_t st)
 {
-	if (z.cur >= 0 && z.img.size() == bytes && memcmp(z.img.data(), data, bytes) == 0) {
+	if (z.ccur >= 0) {
+		const ZArgsImage& e = z.cache[z.ccur];
+		if (e.host.size() == bytes && memcmp(e.host.data(), data, bytes) == 0) {
+			if (e.st != st && hipStreamWaitEvent(st, e.ev, 0) != hipSuccess) return -1;
+			return 0;
+		}
+	}
+	if (z.ccur < 0 && z.cur >= 0 && z.img.size() == bytes && memcmp(z.img.data(), data, bytes) == 0) {
 		if (z.st != st) {                            // (launches on another stream from here on: stream order)
 			if (hipEventRecord(z.ev[z.cur], z.st) != hipSuccess || hipStreamWaitEvent(st, z.ev[z.cur], 0) != hipSuccess) return -1;
 			z.st = st;
 		}
 		return 0;
 	}
+	{
+		const int ci = zargs_cached(z, data, bytes, st);
+		if (ci == -2) return -1;
+		if (ci >= 0) {
+			// leaving the ring's current slot: its launches are all queued, its
+			// event follows them (z.cur stays the ring's position)
+			if (z.ccur < 0 && z.cur >= 0) {
+				if (hipEventRecord(z.ev[z.cur], z.st) != hipSuccess) return -1;
+				z.evset[z.cur] = true;
+			}
+			z.ccur = ci;
+			z.dev = z.cache[ci].dev;
+			return 0;
+		}
+	}
+	const bool from_cache = z.ccur >= 0;
+	z.ccur = -1;
 	if (z.cap < bytes) {
 		// growth (rare: a larger group): every slot idle first
 		if (z.st && hipStreamSynchronize(z.st) != hipSuccess) return -1;
@@ -2768,7 +2854,8 @@ int zargs_put(ZArgs& z, const void* data, size_t bytes, hipStream_t st)
 		z.cap = c;
 	}
 	// the current slot's launches are all queued: its event follows them
-	if (z.cur >= 0) {
+	// (already recorded when the launches moved to a cached image)
+	if (z.cur >= 0 && !from_cache) {
 		if (hipEventRecord(z.ev[z.cur], z.st) != hipSuccess) return -1;
 		z.evset[z.cur] = true;
 	}
@@ -2789,6 +2876,12 @@ int zargs_put(ZArgs& z, const void* data, size_t bytes, hipStream_t st)
 void zargs_free(ZArgs& z)
 {
 	if (z.st) (void)hipStreamSynchronize(z.st);
+	for (ZArgsImage& e : z.cache) {
+		if (e.st) (void)hipStreamSynchronize(e.st);
+		if (e.ev) (void)hipEventDestroy(e.ev);
+	}
+	for (char* d : z.cdev) (void)dev_free(d);
+	for (char* h : z.chost) (void)pinned_free(h);
 	if (z.dbase) (void)dev_free(z.dbase);
 	if (z.hbase) (void)pinned_free(z.hbase);
 	for (int k = 0; k < ZArgs::kRing; k++)

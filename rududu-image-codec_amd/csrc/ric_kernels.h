@@ -132,8 +132,22 @@ struct ZFrames {
 // then waited out each level launch of the step's front, ~1000 per step, with
 // the GPU idle while it issued the next).  A slot is reused once the event
 // recorded after its last launch has passed (kRing uploads later: at once).
+// Images that come back (the serving step's groups reuse the same pool slots,
+// scratch arenas and output buffers step after step) are kept in a cache of
+// device copies, uploaded once: a step then issues its level launches without
+// an argument copy in front of each (round 6: ~1870 copies per step, each a
+// small blit kernel in the batch stream's order).  Up to kCacheBytes per
+// ZArgs; images past it take the ring.
+struct ZArgsImage {
+	uint64_t hash;
+	char* dev;
+	std::vector<char> host;
+	hipStream_t st;                  // the stream the upload was queued on
+	hipEvent_t ev;                   // after the upload
+};
 struct ZArgs {
 	static constexpr int kRing = 8;
+	static constexpr size_t kCacheBytes = 4u << 20, kCacheBlock = 256u << 10;
 	void* dev = nullptr;             // the current image's slot (the launches' argument)
 	char* dbase = nullptr;           // kRing slots of cap bytes
 	char* hbase = nullptr;           // pinned staging, the same
@@ -143,6 +157,12 @@ struct ZArgs {
 	hipEvent_t ev[kRing] = {};
 	bool evset[kRing] = {};
 	std::vector<char> img;
+	// the cache: images by hash, carved from device / pinned blocks
+	std::vector<ZArgsImage> cache;
+	std::vector<char*> cdev, chost;  // blocks of kCacheBlock
+	size_t cused = 0;                // bytes carved from the last block
+	size_t ctotal = 0;               // bytes cached
+	int ccur = -1;                   // the cache entry in use (then cur is only the ring's position), or -1
 };
 int zargs_put(ZArgs& z, const void* data, size_t bytes, hipStream_t st);
 void zargs_free(ZArgs& z);

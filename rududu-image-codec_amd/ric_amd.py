@@ -113,6 +113,7 @@ def lib():
         "ric_diag_gdec_dbg": (_I, [_P]),
         "ric_batch_roundtrip_hybrid": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
         "ric_batch_diag_gpu": (_I, [_P, _P, _I, _I, _I, _I, _P]),
+        "ric_batch_diag_gpu_encode": (_I, [_P, _P, _I, _I, _I, _I]),
         "ric_batch_prof_read": (_I, [_P, _P, _P, _P, _I]),
         "ric_video_create": (_I, [ctypes.POINTER(_P), _I, _I, _I, _I, _I]),
         "ric_video_destroy": (None, [_P]),
@@ -687,6 +688,11 @@ class Batch:
         """GPU stages only (kernel timing), see ric_batch_diag_gpu."""
         po = _ptrs(pix_out) if pix_out is not None else None
         _chk(lib().ric_batch_diag_gpu(self.h, _ptrs(frames), len(frames), q, trans, iters, po), "ric_batch_diag_gpu")
+
+    def diag_gpu_encode(self, frames, q=9, trans=0, iters=1):
+        """The forward levels alone, back to back (ric_batch_diag_gpu_encode)."""
+        _chk(lib().ric_batch_diag_gpu_encode(self.h, _ptrs(frames), len(frames), q, trans, iters),
+             "ric_batch_diag_gpu_encode")
 
     def prof_enable(self, on=True):
         _chk(lib().ric_batch_prof_enable(self.h, int(on)), "ric_batch_prof_enable")
