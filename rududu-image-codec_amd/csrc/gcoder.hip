@@ -54,6 +54,11 @@
 #ifndef RIC_GC_UCOND
 #define RIC_GC_UCOND 2
 #endif
+// RIC_GC_SIGREV: the decoder walks a full block's significant positions by
+// the lowest set bit of the bit-reversed mask
+#ifndef RIC_GC_SIGREV
+#define RIC_GC_SIGREV 1
+#endif
 // RIC_GC_NVGPR: the coder kernels' VGPR budget as amdgpu_num_vgpr takes it
 // on gfx950 (half the unified VGPR + AGPR count: 44 = 88 VGPRs; 0 = none).
 // Three coder waves of 96 VGPRs left a SIMD 224 of its 512 and RCCL's kernel
@@ -1573,11 +1578,19 @@ GC_DI void tree_dec(GDec& d, const GTabs& T, const GBandDesc& B, const GBandDesc
 					uint32_t sig = ru(k == 16 ? 0xFFFFu : ETAB ? d.enum16(cnk, T, etab, k) : d.enum_n(cnk, binom, k, 16, true));
 					GGeoD g;
 					g.load(geo, k - 1, T);
+#if RIC_GC_SIGREV
+					// bit i = raster i (one bit reverse per block): the values in
+					// raster order by the lowest set bit, two scalar ops per value
+					// fewer than the highest-bit walk
+					for (uint32_t rs = __builtin_bitreverse32(sig) >> 16; rs; rs &= rs - 1)
+						g_blk[ob + (uint32_t)__builtin_ctz(rs)] = g.decode<true>(d, T, lmax);
+#else
 					while (sig) {
 						const uint32_t b = 31u - (uint32_t)__builtin_clz(sig);      // bit 15 = raster 0
 						sig &= ~(1u << b);
 						g_blk[ob + 15 - b] = g.decode<true>(d, T, lmax);   // stc truncates a short band's value
 					}
+#endif
 					geo = lset(geo, k - 1, g.packed());
 				}
 				const uint32_t kk = high ? k - 1 : k;
