@@ -54,6 +54,15 @@
 #ifndef RIC_GC_UCOND
 #define RIC_GC_UCOND 2
 #endif
+// RIC_GC_GEOFAST: the geometric models' per-value scalar work trimmed (both
+// coders): k + 1 and the remainder mask kept with k, the frequency update
+// without its 16-bit mask and the re-index test as one unsigned compare (the
+// frequency stays in [1, 4096] and the thresholds below 4096, so both are
+// the reference's 16-bit arithmetic), and the decoder's empty-run path
+// without the run's shift
+#ifndef RIC_GC_GEOFAST
+#define RIC_GC_GEOFAST 0
+#endif
 // RIC_GC_SIGREV: the decoder walks a full block's significant positions by
 // the lowest set bit of the bit-reversed mask
 #ifndef RIC_GC_SIGREV
@@ -578,12 +587,13 @@ struct GBit {
 // adaptation shift 3 + s, the low threshold t0 and the span t1 - t0 of the
 // re-index test, so that test costs one subtract, mask and compare per value.
 struct GGeoCtx {
-	uint32_t freq, idx, k, s3, t0, span;
+	uint32_t freq, idx, k, s3, t0, span, k1, km;
 	GC_DI void params(const GTabs& T)
 	{
 		const uint32_t ks = lget(T.geo_ks, idx), s = ks >> 8;
 		const uint32_t thr = lget(T.geo_thr, s);
 		k = ks & 0xFFu; s3 = s + 3; t0 = thr & 0xFFFFu; span = (thr >> 16) - t0;
+		k1 = k + 1; km = (1u << k) - 1u;
 	}
 	GC_DI void load(uint32_t arr, uint32_t c, const GTabs& T) { const uint32_t v = lget(arr, c); freq = v & 0xFFFFu; idx = v >> 16; params(T); }
 	GC_DI uint32_t packed() const { return freq | idx << 16; }
@@ -604,10 +614,17 @@ struct GGeoCtx {
 				}
 		}
 		e.bin(f, 0);
+#if RIC_GC_GEOFAST
+		if (SIGNED) e.bits(((sym & km) << 1) | sign, k1);
+		else if (k > 0) e.bits(sym & km, k);
+		fr = fr + ((4096u - fr) >> s3);
+		if (__builtin_expect(fr - t0 > span, 0)) {
+#else
 		if (SIGNED) e.bits(((sym & ((1u << k) - 1)) << 1) | sign, k + 1);
 		else if (k > 0) e.bits(sym & ((1u << k) - 1), k);
 		fr = (fr + ((4096u - fr) >> s3)) & 0xFFFFu;
 		if (__builtin_expect(((fr - t0) & 0xFFFFu) > span, 0)) {
+#endif
 			if (fr < t0) { if (idx < 24) idx++; }
 			else if (idx > 0) idx--;
 			if (idx >= 9) fr = 2048;
@@ -1197,6 +1214,13 @@ struct GDec {
 		nbits = vv(nbits - len);
 		return (buffer >> nbits) & ((1u << len) - 1);
 	}
+	// the same with the mask (1 << len) - 1 given
+	GC_DI uint32_t bits_m(uint32_t len, uint32_t mask)
+	{
+		if ((int)ru(nbits - len) < 0) fill(len);
+		nbits = vv(nbits - len);
+		return (buffer >> nbits) & mask;
+	}
 	// huffDecode (muxcodec.h:241-276): lane s tests code s of the table row
 	// (hrow: (code << 5) | len per lane, 0 past the row); the first match wins
 	GC_DI uint32_t huff(uint32_t hrow, uint32_t nsym)
@@ -1359,12 +1383,13 @@ struct GBitD {                                          // CBitCodec::decode, bi
 };
 
 struct GGeoD {                                          // one CGeomCodec context in scalars (as GGeoCtx)
-	uint32_t freq, idx, k, s3, t0, span;
+	uint32_t freq, idx, k, s3, t0, span, k1, kmask;
 	GC_DI void params(const GTabs& T)
 	{
 		const uint32_t ks = lget(T.geo_ks, idx), s = ks >> 8;
 		const uint32_t thr = lget(T.geo_thr, s);
 		k = ks & 0xFFu; s3 = s + 3; t0 = thr & 0xFFFFu; span = (thr >> 16) - t0;
+		k1 = k + 1; kmask = (2u << k) - 1u;
 	}
 	GC_DI void load(uint32_t arr, uint32_t c, const GTabs& T) { const uint32_t v = lget(arr, c); freq = v & 0xFFFFu; idx = v >> 16; params(T); }
 	GC_DI uint32_t packed() const { return freq | idx << 16; }
@@ -1375,6 +1400,8 @@ struct GGeoD {                                          // one CGeomCodec contex
 	{
 		const uint32_t f = freq;
 		uint32_t fr = freq, l = 0;
+		int out;
+#if RIC_GC_GEOFAST == 1
 		if (__builtin_expect(ru(d.bit(f)), 0)) {         // most runs are empty: fall through
 			do {
 				fr -= fr >> s3;
@@ -1382,7 +1409,48 @@ struct GGeoD {                                          // one CGeomCodec contex
 				d.ensure();
 			} while (ru(d.bit(f)));
 		}
-		int out;
+		if (SIGNED) {
+			const uint32_t v = d.bits_m(k1, kmask);
+			const int mag = (int)((l << k) | (v >> 1)) + 1;
+			out = (v & 1) ? -mag : mag;
+		} else {
+			if (k > 0) l = (l << k) | d.bits(k);
+			out = (int)l;
+		}
+		fr = fr + ((4096u - fr) >> s3);
+		if (__builtin_expect(fr - t0 > span, 0)) {
+#elif RIC_GC_GEOFAST
+		if (__builtin_expect(ru(d.bit(f)), 0)) {         // most runs are empty: the other path
+			do {
+				fr -= fr >> s3;
+				if (++l > lmax) break;
+				d.ensure();
+			} while (ru(d.bit(f)));
+			if (SIGNED) {
+				const uint32_t v = d.bits(k1);
+				const int mag = (int)((l << k) | (v >> 1)) + 1;
+				out = (v & 1) ? -mag : mag;
+			} else {
+				if (k > 0) l = (l << k) | d.bits(k);
+				out = (int)l;
+			}
+		} else if (SIGNED) {
+			const uint32_t v = d.bits_m(k1, kmask);
+			const int mag = (int)(v >> 1) + 1;
+			out = (v & 1) ? -mag : mag;
+		} else {
+			out = k > 0 ? (int)d.bits(k) : 0;
+		}
+		fr = fr + ((4096u - fr) >> s3);
+		if (__builtin_expect(fr - t0 > span, 0)) {
+#else
+		if (__builtin_expect(ru(d.bit(f)), 0)) {         // most runs are empty: fall through
+			do {
+				fr -= fr >> s3;
+				if (++l > lmax) break;
+				d.ensure();
+			} while (ru(d.bit(f)));
+		}
 		if (SIGNED) {
 			const uint32_t v = d.bits(k + 1);
 			const int mag = (int)((l << k) | (v >> 1)) + 1;
@@ -1393,6 +1461,7 @@ struct GGeoD {                                          // one CGeomCodec contex
 		}
 		fr = (fr + ((4096u - fr) >> s3)) & 0xFFFFu;
 		if (__builtin_expect((int)ru(span - ((fr - t0) & 0xFFFFu)) < 0, 0)) {
+#endif
 			if (fr < t0) { if (idx < 24) idx++; }
 			else if (idx > 0) idx--;
 			if (idx >= 9) fr = 2048;
