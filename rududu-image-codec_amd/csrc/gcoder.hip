@@ -58,10 +58,12 @@
 // coders): k + 1 and the remainder mask kept with k, the frequency update
 // without its 16-bit mask and the re-index test as one unsigned compare (the
 // frequency stays in [1, 4096] and the thresholds below 4096, so both are
-// the reference's 16-bit arithmetic), and the decoder's empty-run path
-// without the run's shift
+// the reference's 16-bit arithmetic): launch 9.94 -> 9.77 s, two
+// interleaved pairs (profiles/r06_geofast_ab_b*.log).  Splitting the
+// decoder's empty-run path from the unary one as well was 3.8 % slower (the
+// compiler then copies the window registers on the fast path).
 #ifndef RIC_GC_GEOFAST
-#define RIC_GC_GEOFAST 0
+#define RIC_GC_GEOFAST 1
 #endif
 // RIC_GC_SIGREV: the decoder walks a full block's significant positions by
 // the lowest set bit of the bit-reversed mask
@@ -1401,7 +1403,7 @@ struct GGeoD {                                          // one CGeomCodec contex
 		const uint32_t f = freq;
 		uint32_t fr = freq, l = 0;
 		int out;
-#if RIC_GC_GEOFAST == 1
+#if RIC_GC_GEOFAST
 		if (__builtin_expect(ru(d.bit(f)), 0)) {         // most runs are empty: fall through
 			do {
 				fr -= fr >> s3;
@@ -1416,30 +1418,6 @@ struct GGeoD {                                          // one CGeomCodec contex
 		} else {
 			if (k > 0) l = (l << k) | d.bits(k);
 			out = (int)l;
-		}
-		fr = fr + ((4096u - fr) >> s3);
-		if (__builtin_expect(fr - t0 > span, 0)) {
-#elif RIC_GC_GEOFAST
-		if (__builtin_expect(ru(d.bit(f)), 0)) {         // most runs are empty: the other path
-			do {
-				fr -= fr >> s3;
-				if (++l > lmax) break;
-				d.ensure();
-			} while (ru(d.bit(f)));
-			if (SIGNED) {
-				const uint32_t v = d.bits(k1);
-				const int mag = (int)((l << k) | (v >> 1)) + 1;
-				out = (v & 1) ? -mag : mag;
-			} else {
-				if (k > 0) l = (l << k) | d.bits(k);
-				out = (int)l;
-			}
-		} else if (SIGNED) {
-			const uint32_t v = d.bits_m(k1, kmask);
-			const int mag = (int)(v >> 1) + 1;
-			out = (v & 1) ? -mag : mag;
-		} else {
-			out = k > 0 ? (int)d.bits(k) : 0;
 		}
 		fr = fr + ((4096u - fr) >> s3);
 		if (__builtin_expect(fr - t0 > span, 0)) {
