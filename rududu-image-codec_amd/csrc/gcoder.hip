@@ -67,6 +67,9 @@
 #endif
 // RIC_GC_OUTPIN: launch 9.73 -> 9.44 s, two interleaved pairs
 // (profiles/r06_outpin_ab_b*.log)
+#ifndef RIC_GC_VADDR
+#define RIC_GC_VADDR 0
+#endif
 #ifndef RIC_GC_OUTPIN
 #define RIC_GC_OUTPIN 1
 #endif
@@ -1640,8 +1643,17 @@ GC_DI void tree_dec(GDec& d, const GTabs& T, const GBandDesc& B, const GBandDesc
 					// bit i = raster i (one bit reverse per block): the values in
 					// raster order by the lowest set bit, two scalar ops per value
 					// fewer than the highest-bit walk
+#if RIC_GC_VADDR
+					// (the store's position found and addressed on the VALU)
+					for (uint32_t rs = __builtin_bitreverse32(sig) >> 16; rs; rs &= rs - 1) {
+						uint32_t rv = rs;
+						asm volatile("" : "+v"(rv));
+						g_blk[ob + (uint32_t)__builtin_ctz(rv)] = g.decode<true>(d, T, lmax);
+					}
+#else
 					for (uint32_t rs = __builtin_bitreverse32(sig) >> 16; rs; rs &= rs - 1)
 						g_blk[ob + (uint32_t)__builtin_ctz(rs)] = g.decode<true>(d, T, lmax);
+#endif
 #else
 					while (sig) {
 						const uint32_t b = 31u - (uint32_t)__builtin_clz(sig);      // bit 15 = raster 0
